@@ -1,0 +1,52 @@
+# Build of libqlx.so (HIP for gfx950 + C++ host) and the CPU oracle (test infrastructure).
+#   make            -> q-learning_amd/lib/libqlx.so + oracle/liboracle.so + oracle/cpu_baseline
+#   make lib        -> product only
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := q-learning_amd
+SRC := $(PKG)/csrc
+OUT := $(PKG)/lib
+JOBS ?= 8
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-result \
+            -I include -I $(SRC) -munsafe-fp-atomics
+# physics/raster must round every a*b+c twice like the reference (Rust never fuses)
+STRICT := -ffp-contract=off
+LDFLAGS := -shared -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
+
+OBJS := $(OUT)/obj/common.o $(OUT)/obj/env_breakout.o $(OUT)/obj/replay.o $(OUT)/obj/qnet.o $(OUT)/obj/learner.o
+
+HDRS := include/qlx.h $(wildcard $(SRC)/*.h)
+
+all: lib oracle
+
+lib: $(OUT)/libqlx.so
+
+$(OUT)/obj:
+	mkdir -p $@
+
+$(OUT)/obj/common.o: $(SRC)/common.cpp $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/obj/env_breakout.o: $(SRC)/env_breakout.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
+
+$(OUT)/obj/replay.o: $(SRC)/replay.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/obj/qnet.o: $(SRC)/qnet.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/obj/learner.o: $(SRC)/learner.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
+
+$(OUT)/libqlx.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) $(OBJS) $(LDFLAGS) -o $@
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(OUT) && $(MAKE) -C oracle clean
+
+.PHONY: all lib oracle clean

@@ -1,0 +1,202 @@
+/* qlx.h — C ABI of the MI355X-native DQN hot path (env-step -> replay-sample -> Q-net update).
+ *
+ * This is the drop-in boundary for bitmagier/q-learning's Breakout DQN path.  Every entry point
+ * names the reference interface it replaces (paths relative to the reference repo root):
+ *
+ *   ql::Environment / ql::Action         src/ql/src/prelude.rs:12-63
+ *   BreakoutEnvironment (+ mechanics)   src/_breakout-ml/src/breakout_environment.rs:131-207,
+ *                                        src/breakout-game/src/mechanics.rs:56-135
+ *   ReplayBuffer / get_many             src/ql-with-tensorflow/src/learn/replay_buffer.rs:52-138
+ *   generate_distinct_random_ids        src/ql-with-tensorflow/src/learn/self_driving_tf_q_learner.rs:276-296
+ *   DeepQLearningModel                  src/ql-with-tensorflow/src/ml_model/model.rs:29-77
+ *   SelfDrivingQLearner / Parameter     src/ql-with-tensorflow/src/learn/self_driving_tf_q_learner.rs:20-139
+ *
+ * Conventions
+ *   - Opaque handles; every call returns int32_t status (QLX_OK = 0, < 0 = error) and
+ *     qlx_last_error() returns a thread-local message.  This replaces the reference's
+ *     panic!/anyhow::Result (q_learning_model.rs:125,147; mechanics.rs:265,284,303,511).
+ *   - Host pointers are caller-owned.  Functions with a `_dev` suffix take device pointers and
+ *     enqueue on the object's HIP stream without synchronising (chain them; qlx_*_sync to wait).
+ *   - Calls on one handle are externally synchronised (the reference is single-threaded: Rc +
+ *     ThreadRng are !Send).
+ *   - Observation layout exposed to callers is the reference tensor view [n][x][y][slot] u8
+ *     (breakout_environment.rs:44-50: H axis = x, channel = ring slot, raw 0..255).
+ *   - No PyTorch/TF types; plain pointers and sizes only.
+ */
+#ifndef QLX_H
+#define QLX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QLX_OK 0
+#define QLX_E_INVALID (-1)
+#define QLX_E_HIP (-2)
+#define QLX_E_OOM (-3)
+#define QLX_E_STATE (-4)
+#define QLX_E_COMM (-5)
+#define QLX_E_IO (-6)
+
+#define QLX_ENV_BREAKOUT 1
+#define QLX_ARCH_NATURE_DQN 1 /* Conv(32,8,s4)-Conv(64,4,s2)-Conv(64,3,s1)-Dense512-Dense3 */
+
+const char* qlx_last_error(void);
+int32_t qlx_version(void);
+
+/* ---------------- Environment (ql::Environment for Breakout, batched) ---------------- */
+
+/* Mechanics snapshot of one env, for parity checks (BreakoutMechanics, mechanics.rs:46-54). */
+typedef struct qlx_breakout_state {
+  float ball_x, ball_y, dir_x, dir_y;
+  float panel_min_x, panel_min_y, panel_max_x, panel_max_y, panel_speed;
+  uint32_t score, finished, next_slot, fault, reset_count;
+  uint64_t bricks; /* bit i = brick i (creation order) still present */
+} qlx_breakout_state;
+
+typedef struct qlx_env qlx_env;
+
+/* Action::ACTION_SPACE (breakout_environment.rs:103) */
+int32_t qlx_env_action_space(int32_t kind);
+/* Environment::episode_reward_goal_mean (breakout_environment.rs:203-206): bricks - 1 = 59 */
+float qlx_env_reward_goal_mean(int32_t kind);
+
+/* BreakoutEnvironment::new x n_envs on `device`; env i draws its ball launch angle from the
+ * build's counter-based stream (seed, i, reset_count) instead of thread_rng (mechanics.rs:103). */
+int32_t qlx_env_create(int32_t kind, uint32_t n_envs, uint64_t seed, int32_t device, qlx_env** out);
+int32_t qlx_env_destroy(qlx_env* env);
+uint32_t qlx_env_count(const qlx_env* env);
+/* Environment::reset (breakout_environment.rs:177-180) for every env, or where mask[i] != 0. */
+int32_t qlx_env_reset(qlx_env* env, const uint8_t* mask_or_null);
+/* Environment::step (breakout_environment.rs:184-201) for all envs; host arrays of n_envs.
+ * Invalid actions (>= 3) fail with QLX_E_INVALID like Action::try_from_numeric. */
+int32_t qlx_env_step(qlx_env* env, const uint8_t* actions, float* rewards, uint8_t* dones);
+/* Device-pointer form: actions/rewards/dones are device arrays of n_envs. */
+int32_t qlx_env_step_dev(qlx_env* env, const uint8_t* d_actions, float* d_rewards, uint8_t* d_dones);
+/* ToMultiDimArray::batch_to_multi_dim_array view of the current states: out[n][84][84][4] (x,y,slot). */
+int32_t qlx_env_obs(qlx_env* env, uint8_t* out);
+int32_t qlx_env_states(qlx_env* env, qlx_breakout_state* out /* [n_envs] */);
+/* Running per-env checksum of every step (state + new frame), see DESIGN.md §parity. */
+int32_t qlx_env_hashes(qlx_env* env, uint64_t* out /* [n_envs] */);
+int32_t qlx_env_sync(qlx_env* env);
+
+/* ---------------- Replay buffer (ReplayBuffer, HBM-resident) ---------------- */
+
+typedef struct qlx_replay qlx_replay;
+
+/* FIFO of `capacity` transitions (history_buffer_len); logical index 0 = oldest (VecDeque). Frames
+ * are stored once (s' of step t is s of step t+1), 7,056 B per transition + metadata. */
+int32_t qlx_replay_create(uint64_t capacity, uint32_t n_envs, int32_t device, qlx_replay** out);
+int32_t qlx_replay_destroy(qlx_replay* rb);
+uint64_t qlx_replay_len(const qlx_replay* rb);
+/* ReplayBuffer::add for the transition each env of `env` just made (actions = device array used for
+ * that step, rewards/dones = its outputs).  Call once after every qlx_env_step[_dev]. */
+int32_t qlx_replay_push_dev(qlx_replay* rb, qlx_env* env, const uint8_t* d_actions, const float* d_rewards,
+                            const uint8_t* d_dones);
+/* Host-array form of qlx_replay_push_dev (synchronises). */
+int32_t qlx_replay_push(qlx_replay* rb, qlx_env* env, const uint8_t* actions, const float* rewards,
+                        const uint8_t* dones);
+/* generate_distinct_random_ids::<B>(rng, 0..len) from stream (seed, update_idx, rank); host out[B]. */
+int32_t qlx_replay_sample_distinct(qlx_replay* rb, uint64_t seed, uint32_t update_idx, uint32_t rank, uint32_t batch,
+                                   uint64_t* out_indices);
+/* ReplayBuffer::get_many + batch_to_multi_dim_array: host outputs, any may be NULL. */
+int32_t qlx_replay_get_many(qlx_replay* rb, const uint64_t* indices, uint32_t batch, uint8_t* s /*[B][84][84][4]*/,
+                            uint8_t* s_next, uint8_t* actions, float* rewards, uint8_t* dones);
+
+/* ---------------- Q-network (DeepQLearningModel) ---------------- */
+
+typedef struct qlx_model qlx_model;
+
+/* Nature-DQN with GlorotUniform weights from stream (seed, var, 0) and zero biases; fp32 master
+ * weights + Adam slots in HBM, bf16 MFMA copies. lr 2.5e-4, beta 0.9/0.999, eps 1e-7, clipnorm 1. */
+int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out);
+int32_t qlx_model_destroy(qlx_model* m);
+int32_t qlx_model_num_vars(void);
+int64_t qlx_model_var_size(int32_t var);
+/* which: 0 = weights, 1 = Adam m, 2 = Adam v.  Layout = Keras HWIO / [in,out]. */
+int32_t qlx_model_get_var(qlx_model* m, int32_t var, int32_t which, float* out);
+int32_t qlx_model_set_var(qlx_model* m, int32_t var, int32_t which, const float* in);
+int64_t qlx_model_iterations(qlx_model* m);
+int32_t qlx_model_copy_weights(qlx_model* dst, const qlx_model* src);
+/* predict_action for n states (model.rs:39-42): q_out [n][3] (may be NULL), actions [n] = argmax. */
+int32_t qlx_model_predict(qlx_model* m, const uint8_t* obs /*[n][84][84][4]*/, uint32_t n, float* q_out,
+                          uint8_t* actions);
+/* batch_predict_max_future_reward (model.rs:44-47). */
+int32_t qlx_model_batch_max_q(qlx_model* m, const uint8_t* obs, uint32_t n, float* out);
+/* train (model.rs:49-65): forward, Huber(1) mean, backward, clip_by_norm(1) per variable, Adam.
+ * loss_out (may be NULL) gets the batch loss; grads_out (may be NULL) the raw gradients of all vars
+ * concatenated; norms_out (may be NULL) the 10 per-variable L2 norms before clipping. */
+int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions, const float* y, uint32_t batch,
+                        float* loss_out, float* grads_out, float* norms_out);
+/* Debug view of intermediate activations of the last predict: layer 1..4 as fp32 host arrays. */
+int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out);
+/* write_checkpoint (model.rs:67-70): weights + Adam slots + iterations in a flat file. */
+int32_t qlx_model_write_checkpoint(qlx_model* m, const char* path);
+int32_t qlx_model_read_checkpoint(qlx_model* m, const char* path);
+int32_t qlx_model_sync(qlx_model* m);
+
+/* ---------------- Learner (SelfDrivingQLearner) ---------------- */
+
+typedef struct qlx_params { /* Parameter (self_driving_tf_q_learner.rs:20-67) + build fields */
+  float gamma;
+  float lowest_episode_reward_goal_threshold_pct;
+  double epsilon_max;
+  double epsilon_min;
+  double epsilon_greedy_steps;
+  uint64_t max_steps_per_episode;
+  uint64_t epsilon_pure_random_steps;
+  uint64_t history_buffer_len;
+  uint64_t update_after_actions;
+  uint64_t target_sync_steps; /* 0 = never (reference behaviour) */
+  uint64_t episode_reward_history_buffer_len;
+  uint32_t n_envs;
+  uint32_t batch_size;
+  uint64_t env_seed;
+  uint64_t learner_seed;
+  uint64_t init_seed;
+  uint32_t rank;
+  uint32_t pad;
+} qlx_params;
+
+void qlx_params_default(qlx_params* p);
+
+typedef struct qlx_learner qlx_learner;
+
+typedef struct qlx_learner_stats {
+  uint64_t step_count, vec_steps, update_count, episode_count, replay_len, solved;
+  double epsilon;
+  float running_reward, last_loss;
+} qlx_learner_stats;
+
+/* SelfDrivingQLearner::new: owns a batched env, replay, online + target ("stabilized") model. */
+int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** out);
+int32_t qlx_learner_destroy(qlx_learner* l);
+/* One vector step (n_envs env-steps + the updates they trigger), enqueued asynchronously. */
+int32_t qlx_learner_vector_step(qlx_learner* l);
+int32_t qlx_learner_run(qlx_learner* l, uint64_t n_vector_steps);
+int32_t qlx_learner_sync(qlx_learner* l);
+int32_t qlx_learner_stats_get(qlx_learner* l, qlx_learner_stats* out);
+/* Outputs of the last vector step (host copies; synchronises): actions/rewards/dones [n_envs],
+ * losses [n_updates], indices [n_updates][B], targets [n_updates][B]; any may be NULL. Returns the
+ * number of updates of that step in *n_updates. */
+int32_t qlx_learner_last(qlx_learner* l, uint8_t* actions, float* rewards, uint8_t* dones, float* losses,
+                         uint64_t* indices, float* targets, uint32_t* n_updates);
+qlx_env* qlx_learner_env(qlx_learner* l);
+qlx_replay* qlx_learner_replay(qlx_learner* l);
+qlx_model* qlx_learner_model(qlx_learner* l, int32_t which /* 0 online, 1 target */);
+/* Data-parallel: RCCL communicator over world ranks (one process per GPU); gradients are
+ * all-reduced (mean) before clip_by_norm + Adam. uid from qlx_dist_unique_id on rank 0. */
+int32_t qlx_dist_unique_id(uint8_t out[128]);
+int32_t qlx_learner_dist_init(qlx_learner* l, int32_t world, int32_t rank, const uint8_t uid[128]);
+/* Kernel timing: average device time (us) per launch of the named kernel class over the last run
+ * (measured with HIP events on the learner stream); names: "conv", "env", "replay", "adam", "all". */
+int32_t qlx_learner_profile(qlx_learner* l, int32_t enable);
+int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* avg_us, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QLX_H */

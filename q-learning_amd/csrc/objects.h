@@ -1,0 +1,52 @@
+// Host-side definitions of the opaque ABI objects (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qlx_internal.h"
+
+struct qlx_env {
+  int device = 0;
+  uint32_t n = 0;
+  uint64_t seed = 0;
+  hipStream_t stream = nullptr;   // owned unless adopted by a learner
+  bool own_stream = true;
+  qlx_breakout_state* d_state = nullptr;
+  uint32_t* d_ep_steps = nullptr;  // [n] steps taken in the current episode
+  uint8_t* d_obs = nullptr;        // [n][4][7056] ring frames, s2d layout
+  uint64_t* d_hash = nullptr;      // [n] running parity checksum
+  uint32_t* d_flags = nullptr;     // [4] bad-action flag
+  uint8_t* d_tmp_u8 = nullptr;     // [n] staging
+  uint8_t* d_tmp_u8b = nullptr;    // [n]
+  float* d_tmp_f32 = nullptr;      // [n]
+  float acos_thr = 0.0f;
+  bool hashing = true;
+};
+
+struct qlx_replay {
+  int device = 0;
+  uint64_t cap = 0;
+  uint32_t n = 0;
+  uint64_t F = 0;        // frame slots = cap + 4 n
+  uint64_t total = 0;    // transitions pushed so far
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  uint8_t* d_frames = nullptr;
+  uint8_t* d_action = nullptr;
+  float* d_reward = nullptr;
+  uint8_t* d_done = nullptr;
+  uint32_t* d_epstep = nullptr;
+  uint64_t* d_idx = nullptr;    // scratch for sampling [max_batch]
+  uint32_t idx_cap = 0;
+  uint64_t len() const { return total < cap ? total : cap; }
+};
+
+namespace qlx {
+void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, uint8_t* d_dones);
+void env_launch_reset(qlx_env* env, const uint8_t* d_mask, int bump);
+void replay_launch_push(qlx_replay* rb, qlx_env* env, hipStream_t s, const uint8_t* d_actions, const float* d_rewards,
+                        const uint8_t* d_dones);
+void replay_launch_sample(qlx_replay* rb, hipStream_t s, uint64_t seed, uint32_t first_update, uint32_t n_updates,
+                          uint32_t rank, uint32_t batch, uint64_t* d_out);
+}  // namespace qlx

@@ -1,0 +1,66 @@
+// Host-side Q-network object and the launch helpers the learner composes.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qlx_internal.h"
+
+namespace qlx {
+
+constexpr int kNumVars = 10;
+constexpr int64_t kNumParams = 1685667;   // sum of the 10 Keras variables (variables.index shapes)
+constexpr int kFc1Split = 7;              // split-K of the 3136-deep dense layer (14 MFMA k-steps each)
+constexpr size_t kWgradSlabFloats = 64 * 576 * 64;   // max chunks x KIN x N over the conv layers
+constexpr size_t kBiasSlabFloats = 128 * 64;
+extern const int kVarSize[kNumVars];
+
+struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
+  uint8_t* frames = nullptr;          // [B*4][7056] s2d staging for host observations
+  const uint8_t** table = nullptr;    // [B][4] frame pointers
+  __bf16 *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *a4 = nullptr;
+  __bf16 *dz1 = nullptr, *dz2 = nullptr, *dz3 = nullptr, *dz4 = nullptr;
+  float* q = nullptr;
+  float *gs = nullptr, *hs = nullptr, *y = nullptr, *rew = nullptr;
+  uint8_t *act = nullptr, *argmax = nullptr, *done = nullptr;
+  float* fc1slab = nullptr;
+  float* slab = nullptr;
+  float* bslab = nullptr;
+  float* g0_s2d = nullptr;
+  float* loss = nullptr;
+};
+
+}  // namespace qlx
+
+struct qlx_model {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  float* d_params = nullptr;   // fp32 master weights, Keras layouts, variables concatenated
+  float* d_m = nullptr;
+  float* d_v = nullptr;
+  float* d_grads = nullptr;
+  // bf16 MFMA operand copies ([n][k], k contiguous)
+  __bf16 *wf0 = nullptr, *wf1 = nullptr, *wb1 = nullptr, *wf2 = nullptr, *wb2 = nullptr, *wf3 = nullptr, *wb3 = nullptr;
+  int64_t iterations = 0;
+  float lr = 0.00025f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, clipnorm = 1.0f;
+  int n_ranges = 0;
+  int64_t *d_rbeg = nullptr, *d_rend = nullptr;
+  float* d_partial = nullptr;
+  int* d_var_first = nullptr;
+  float* d_norms = nullptr;
+  void* ws = nullptr;
+  int ws_batch = 0;
+  int last_batch = 0;
+  qlx::ModelWs w;
+};
+
+namespace qlx {
+struct Fc2Args;
+void model_workspace(qlx_model* m, int B);
+void model_pack(qlx_model* m);
+void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
+void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, hipStream_t s);
+void model_norms(qlx_model* m, hipStream_t s, float scale);
+void model_adam(qlx_model* m, hipStream_t s, float scale);
+}  // namespace qlx

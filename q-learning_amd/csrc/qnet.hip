@@ -1,0 +1,725 @@
+// DeepQLearningModel on MI355X: Nature-DQN forward / backward / Huber / clip_by_norm / Adam.
+//
+// Reference (restated): create_ql_model_breakout_84x84x4_3_32.py:20-33 (graph), :36-55 (predict_action,
+// batch_predict_max_future_reward), :63-82 (train_model; intended q_a = Q(s)[a] semantics of
+// create_ql_model_ballgame_3x3x4_5_512.py:71-78), legacy keras Adam(lr 2.5e-4, clipnorm 1.0) =
+// tf.clip_by_norm per variable + ResourceApplyAdam (saved_model.pb op names), Huber(delta=1) mean.
+// The reference runs this inside libtensorflow behind Session::run (q_learning_model.rs:107-189).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "objects.h"
+#include "qnet.h"
+#include "qnet_kernels.h"
+
+namespace qlx {
+
+using namespace qn;
+
+extern const int kVarSize[kNumVars];
+const int kVarSize[kNumVars] = {8 * 8 * 4 * 32, 32, 4 * 4 * 32 * 64, 64, 3 * 3 * 64 * 64, 64, 3136 * 512, 512, 512 * 3, 3};
+static int64_t var_offset(int v) {
+  int64_t o = 0;
+  for (int i = 0; i < v; ++i) o += kVarSize[i];
+  return o;
+}
+
+// ------------------------------------------------------------------------------------------
+// weight packing: fp32 master (Keras layouts) -> bf16 MFMA operand layouts
+
+__device__ __forceinline__ int conv1_s2d_k(int kh, int kw, int c) {
+  const int i = kh >> 2, dx = kh & 3, j = kw >> 2, dy = kw & 3;
+  return (((i * 2 + j) * 4 + c) * 16) + dx * 4 + dy;
+}
+
+struct PackPtrs {
+  bf16 *wf0, *wf1, *wb1, *wf2, *wb2, *wf3, *wb3;
+};
+
+// writes the bf16 copies of parameter element idx (global flat index) with value w
+__device__ __forceinline__ void pack_one(const PackPtrs& P, int64_t idx, float w) {
+  const bf16 v = (bf16)w;
+  if (idx < 8192) {   // conv1 kernel [8][8][4][32]
+    const int oc = idx & 31, c = (idx >> 5) & 3, kw = (idx >> 7) & 7, kh = (int)(idx >> 10);
+    P.wf0[oc * 256 + conv1_s2d_k(kh, kw, c)] = v;
+    return;
+  }
+  idx -= 8192 + 32;
+  if (idx < 0) return;
+  if (idx < 32768) {   // conv2 kernel [4][4][32][64]
+    const int oc = idx & 63, c = (idx >> 6) & 31, tap = (int)(idx >> 11);   // tap = kh*4 + kw
+    P.wf1[oc * 512 + tap * 32 + c] = v;
+    P.wb1[c * 1024 + tap * 64 + oc] = v;
+    return;
+  }
+  idx -= 32768 + 64;
+  if (idx < 0) return;
+  if (idx < 36864) {   // conv3 kernel [3][3][64][64]
+    const int oc = idx & 63, c = (idx >> 6) & 63, tap = (int)(idx >> 12);  // tap = kh*3 + kw
+    P.wf2[oc * 576 + tap * 64 + c] = v;
+    P.wb2[c * 576 + tap * 64 + oc] = v;
+    return;
+  }
+  idx -= 36864 + 64;
+  if (idx < 0) return;
+  if (idx < 3136 * 512) {   // full_layer kernel [3136][512]
+    const int n = idx & 511, k = (int)(idx >> 9);
+    P.wf3[(size_t)n * 3136 + k] = v;
+    P.wb3[idx] = v;
+  }
+}
+
+__global__ void k_pack_all(const float* w, int64_t count, PackPtrs P) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x)
+    pack_one(P, i, w[i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// host obs [B][x][y][slot] -> s2d frames [B*4][7056] + frame pointer table
+
+__global__ void k_pack_obs(const uint8_t* obs, int B, uint8_t* frames) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over B*84*84
+  if (i >= (int64_t)B * kFramePix) return;
+  const int b = (int)(i / kFramePix), xy = (int)(i - (int64_t)b * kFramePix);
+  const int x = xy / kFrame, y = xy - x * kFrame;
+  const uchar4 v = reinterpret_cast<const uchar4*>(obs)[i];
+  const int off = s2d_offset(x, y);
+  frames[((size_t)b * 4 + 0) * kFramePix + off] = v.x;
+  frames[((size_t)b * 4 + 1) * kFramePix + off] = v.y;
+  frames[((size_t)b * 4 + 2) * kFramePix + off] = v.z;
+  frames[((size_t)b * 4 + 3) * kFramePix + off] = v.w;
+}
+
+__global__ void k_frame_table(const uint8_t* frames, int B, const uint8_t** table) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B * 4) table[i] = frames + (size_t)i * kFramePix;
+}
+
+// ------------------------------------------------------------------------------------------
+// dense 512 -> 3 (linear) on VALU, one wave per sample; optional heads:
+//   mode 0: q only; mode 1: argmax actions (predict_action); mode 2: max -> Bellman target
+//   mode 3: Huber loss + dq for train (needs actions, y)
+struct Fc2Args {
+  const bf16* a4;          // [B][512]
+  const float* w4;         // [512][3] master
+  const float* b4;         // [3]
+  int B;
+  float* q;                // [B][3] out (may be null)
+  uint8_t* argmax;         // mode 1
+  const float* rewards;    // mode 2
+  const uint8_t* dones;    // mode 2
+  float gamma;             // mode 2
+  float* y_out;            // mode 2
+  const uint8_t* actions;  // mode 3
+  const float* y;          // mode 3
+  float* gsample;          // mode 3: dloss/dq_a per sample
+  float* hsample;          // mode 3: per-sample Huber value
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_fc2(Fc2Args A) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= A.B) return;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+  const bf16x8 v = ld8(A.a4 + (size_t)b * 512 + lane * 8);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = (float)v[e];
+    const float* w = A.w4 + (lane * 8 + e) * 3;
+    s0 += x * w[0];
+    s1 += x * w[1];
+    s2 += x * w[2];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  if (lane != 0) return;
+  const float q0 = s0 + A.b4[0], q1 = s1 + A.b4[1], q2 = s2 + A.b4[2];
+  if (A.q) { A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2; }
+  if (MODE == 1) {   // tf.argmax: first maximal index
+    int best = 0;
+    float bv = q0;
+    if (q1 > bv) { best = 1; bv = q1; }
+    if (q2 > bv) { best = 2; }
+    A.argmax[b] = (uint8_t)best;
+  } else if (MODE == 2) {   // max_a Q_target(s') -> r + max * gamma, or r if done
+    const float mx = fmaxf(fmaxf(q0, q1), q2);
+    const float r = A.rewards[b];
+    A.y_out[b] = A.dones[b] ? r : r + mx * A.gamma;
+  } else if (MODE == 3) {   // Huber(delta=1) of e = q_a - y, mean over batch
+    const int a = A.actions[b];
+    const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
+    const float e = qa - A.y[b];
+    const float ae = fabsf(e);
+    A.hsample[b] = ae <= 1.0f ? 0.5f * e * e : ae - 0.5f;
+    const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
+    A.gsample[b] = ge / (float)A.B;
+  }
+}
+
+// dz4[b][k] = g_b * W4[k][a_b] * (a4[b][k] > 0)
+__global__ void k_fc2_bwd_data(const bf16* a4, const float* w4, const uint8_t* actions, const float* gs, int B, bf16* dz4) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * 512) return;
+  const int b = i >> 9, k = i & 511;
+  const float v = (float)a4[i] > 0.0f ? gs[b] * w4[k * 3 + actions[b]] : 0.0f;
+  dz4[i] = (bf16)v;
+}
+
+// dW4[k][a] = sum_b a4[b][k] g_b [a_b == a]; db4[a] = sum_b g_b [a_b == a]   (block per k, k = 512 -> bias)
+__global__ __launch_bounds__(256) void k_fc2_wgrad(const bf16* a4, const uint8_t* actions, const float* gs, int B,
+                                                   float* g_w4, float* g_b4) {
+  __shared__ float red[3][256];
+  const int k = blockIdx.x;
+  float s[3] = {0.0f, 0.0f, 0.0f};
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float x = k < 512 ? (float)a4[(size_t)b * 512 + k] : 1.0f;
+    s[actions[b]] += x * gs[b];
+  }
+  for (int j = 0; j < 3; ++j) red[j][threadIdx.x] = s[j];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) {
+    if (k < 512) g_w4[k * 3 + threadIdx.x] = red[threadIdx.x][0];
+    else g_b4[threadIdx.x] = red[threadIdx.x][0];
+  }
+}
+
+// loss = sum_b h_b / B in fixed order (one block)
+__global__ void k_loss_sum(const float* h, int B, float* loss) {
+  __shared__ float red[256];
+  float s = 0.0f;
+  for (int b = threadIdx.x; b < B; b += 256) s += h[b];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0] / (float)B;
+}
+
+// conv1 weight gradient from s2d k order [256][32] into HWIO [8][8][4][32]
+__global__ void k_conv1_grad_unpermute(const float* g_s2d, float* g_hwio) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 8192) return;
+  const int oc = idx & 31, c = (idx >> 5) & 3, kw = (idx >> 7) & 7, kh = idx >> 10;
+  g_hwio[idx] = g_s2d[conv1_s2d_k(kh, kw, c) * 32 + oc];
+}
+
+// ------------------------------------------------------------------------------------------
+// clip_by_norm per variable + ResourceApplyAdam
+
+__global__ __launch_bounds__(256) void k_sumsq(const float* g, const int64_t* range_begin, const int64_t* range_end,
+                                               float scale, float* partial) {
+  __shared__ float red[256];
+  const int64_t b = range_begin[blockIdx.x], e = range_end[blockIdx.x];
+  float s = 0.0f;
+  for (int64_t i = b + threadIdx.x; i < e; i += 256) {
+    const float x = g[i] * scale;
+    s += x * x;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void k_norms(const float* partial, const int* var_first, float* norms) {
+  const int v = threadIdx.x;
+  if (v >= kNumVars) return;
+  float s = 0.0f;
+  for (int r = var_first[v]; r < var_first[v + 1]; ++r) s += partial[r];
+  norms[v] = s > 0.0f ? sqrtf(s) : s;   // tf.clip_by_norm: safe sqrt via where(l2sum > 0)
+}
+
+struct AdamArgs {
+  float* w;
+  float* m;
+  float* v;
+  const float* g;
+  const float* norms;
+  int64_t count;
+  float scale;     // 1/world for data-parallel mean
+  float alpha;     // lr * sqrt(1 - b2^t) / (1 - b1^t)
+  float beta1, beta2, eps, clipnorm;
+  PackPtrs pack;
+};
+
+__global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
+  __shared__ int64_t offs[kNumVars + 1];
+  if (threadIdx.x == 0) {
+    int64_t o = 0;
+    for (int i = 0; i < kNumVars; ++i) { offs[i] = o; o += kVarSize[i]; }
+    offs[kNumVars] = o;
+  }
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.count; i += (int64_t)gridDim.x * blockDim.x) {
+    int var = 0;
+    while (i >= offs[var + 1]) ++var;
+    const float denom = fmaxf(A.norms[var], A.clipnorm);
+    const float gc = (A.g[i] * A.scale * A.clipnorm) / denom;
+    float m = A.m[i], v = A.v[i], w = A.w[i];
+    m += (gc - m) * (1.0f - A.beta1);
+    v += (gc * gc - v) * (1.0f - A.beta2);
+    w -= (m * A.alpha) / (sqrtf(v) + A.eps);
+    A.m[i] = m;
+    A.v[i] = v;
+    A.w[i] = w;
+    pack_one(A.pack, i, w);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+void model_workspace(qlx_model* m, int B) {
+  if (B <= m->ws_batch) return;
+  QLX_HIP(hipStreamSynchronize(m->stream));
+  if (m->ws) (void)hipFree(m->ws);
+  m->ws = nullptr;
+  ModelWs& w = m->w;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off = align_up(off + bytes, 256); return o; };
+  const size_t o_frames = take((size_t)B * 4 * kFramePix);
+  const size_t o_table = take((size_t)B * 4 * sizeof(void*));
+  const size_t o_a1 = take((size_t)B * 12800 * 2), o_a2 = take((size_t)B * 5184 * 2), o_a3 = take((size_t)B * 3136 * 2);
+  const size_t o_a4 = take((size_t)B * 512 * 2), o_q = take((size_t)B * 3 * 4);
+  const size_t o_dz1 = take((size_t)B * 12800 * 2), o_dz2 = take((size_t)B * 5184 * 2), o_dz3 = take((size_t)B * 3136 * 2);
+  const size_t o_dz4 = take((size_t)B * 512 * 2);
+  const size_t o_gs = take((size_t)B * 4), o_hs = take((size_t)B * 4), o_y = take((size_t)B * 4);
+  const size_t o_act = take((size_t)B), o_argmax = take((size_t)B), o_rew = take((size_t)B * 4), o_done = take((size_t)B);
+  const size_t o_fc1slab = take((size_t)kFc1Split * B * 512 * 4);
+  const size_t o_slab = take(kWgradSlabFloats * 4);
+  const size_t o_bslab = take(kBiasSlabFloats * 4);
+  const size_t o_g0 = take(8192 * 4);
+  const size_t o_loss = take(64);
+  QLX_HIP(hipMalloc(&m->ws, off));
+  char* base = (char*)m->ws;
+  w.frames = (uint8_t*)(base + o_frames);
+  w.table = (const uint8_t**)(base + o_table);
+  w.a1 = (bf16*)(base + o_a1); w.a2 = (bf16*)(base + o_a2); w.a3 = (bf16*)(base + o_a3); w.a4 = (bf16*)(base + o_a4);
+  w.q = (float*)(base + o_q);
+  w.dz1 = (bf16*)(base + o_dz1); w.dz2 = (bf16*)(base + o_dz2); w.dz3 = (bf16*)(base + o_dz3); w.dz4 = (bf16*)(base + o_dz4);
+  w.gs = (float*)(base + o_gs); w.hs = (float*)(base + o_hs); w.y = (float*)(base + o_y);
+  w.act = (uint8_t*)(base + o_act); w.argmax = (uint8_t*)(base + o_argmax); w.rew = (float*)(base + o_rew);
+  w.done = (uint8_t*)(base + o_done);
+  w.fc1slab = (float*)(base + o_fc1slab);
+  w.slab = (float*)(base + o_slab);
+  w.bslab = (float*)(base + o_bslab);
+  w.g0_s2d = (float*)(base + o_g0);
+  w.loss = (float*)(base + o_loss);
+  m->ws_batch = B;
+}
+
+static PackPtrs pack_ptrs(qlx_model* m) {
+  PackPtrs P;
+  P.wf0 = m->wf0; P.wf1 = m->wf1; P.wb1 = m->wb1; P.wf2 = m->wf2; P.wb2 = m->wb2; P.wf3 = m->wf3; P.wb3 = m->wb3;
+  return P;
+}
+
+void model_pack(qlx_model* m) {
+  hipLaunchKernelGGL(k_pack_all, dim3(2048), dim3(256), 0, m->stream, m->d_params, (int64_t)kNumParams, pack_ptrs(m));
+  QLX_HIP(hipGetLastError());
+}
+
+// forward through fc1 (a1..a4 in the workspace); `table` = [B][4] frame pointers
+void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+  ModelWs& w = m->w;
+  m->last_batch = B;
+  const float* p = m->d_params;
+  {  // conv1: M = B*400, N = 32, K = 256
+    LoadConv1 la{table, B * 400};
+    EpiBiasRelu ep{w.a1, p + var_offset(1), 32};
+    hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, LoadConv1, EpiBiasRelu>), dim3((B * 400 + 127) / 128, 1, 1), dim3(256), 0, s,
+                       la, m->wf0, B * 400, 256, 256, ep);
+  }
+  {  // conv2: M = B*81, N = 64, K = 512
+    LoadIm2col<20, 20, 32, 4, 2, 9, 9> la{w.a1, B * 81};
+    EpiBiasRelu ep{w.a2, p + var_offset(3), 64};
+    hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiBiasRelu>), dim3((B * 81 + 127) / 128, 1, 1), dim3(256), 0, s,
+                       la, m->wf1, B * 81, 512, 512, ep);
+  }
+  {  // conv3: M = B*49, N = 64, K = 576
+    LoadIm2col<9, 9, 64, 3, 1, 7, 7> la{w.a2, B * 49};
+    EpiBiasRelu ep{w.a3, p + var_offset(5), 64};
+    hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiBiasRelu>), dim3((B * 49 + 127) / 128, 1, 1), dim3(256), 0, s,
+                       la, m->wf2, B * 49, 576, 576, ep);
+  }
+  {  // fc1: M = B, N = 512, K = 3136, split-K into kFc1Split partial slabs
+    LoadRows<3136> la{w.a3, B};
+    EpiSlab ep{w.fc1slab, 512, (size_t)B * 512};
+    hipLaunchKernelGGL((k_igemm<2, 2, 2, 2, LoadRows<3136>, EpiSlab>), dim3((B + 63) / 64, 512 / 64, kFc1Split), dim3(256), 0,
+                       s, la, m->wf3, B, 3136, 3136 / kFc1Split, ep);
+    hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, s, w.fc1slab,
+                       (size_t)B * 512, kFc1Split, B, 512, p + var_offset(7), w.a4);
+  }
+  QLX_HIP(hipGetLastError());
+}
+
+Fc2Args fc2_args(qlx_model* m, int B) {
+  Fc2Args a{};
+  a.a4 = m->w.a4;
+  a.w4 = m->d_params + var_offset(8);
+  a.b4 = m->d_params + var_offset(9);
+  a.B = B;
+  a.q = m->w.q;
+  return a;
+}
+
+// grads (raw, unclipped) of the Huber loss into m->d_grads; gs = per-sample dloss/dq_a, actions in ws
+void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, hipStream_t s) {
+  ModelWs& w = m->w;
+  float* G = m->d_grads;
+  // fc2
+  hipLaunchKernelGGL(k_fc2_bwd_data, dim3((B * 512 + 255) / 256), dim3(256), 0, s, w.a4, m->d_params + var_offset(8),
+                     actions, w.gs, B, w.dz4);
+  hipLaunchKernelGGL(k_fc2_wgrad, dim3(513), dim3(256), 0, s, w.a4, actions, w.gs, B, G + var_offset(8), G + var_offset(9));
+  // fc1: dW3 = a3^T dz4 (one chunk), db3; dz3 = (dz4 W3^T) * (a3 > 0)
+  {
+    LoadRows<3136> lx{w.a3, B};
+    hipLaunchKernelGGL((k_wgrad<64, LoadRows<3136>>), dim3(3136 / 64, 512 / 64, 1), dim3(256), 0, s, lx, w.dz4, B, 512,
+                       align_up(B, 32), G + var_offset(6), 512, (size_t)0, w.bslab);
+    hipLaunchKernelGGL(k_slab_reduce, dim3(2), dim3(256), 0, s, w.bslab, (size_t)512, 1, (size_t)512, G + var_offset(7));
+    LoadRows<512> la{w.dz4, B};
+    EpiReluMask ep{w.dz3, w.a3, 3136};
+    hipLaunchKernelGGL((k_igemm<1, 4, 4, 1, LoadRows<512>, EpiReluMask>), dim3((B + 63) / 64, 3136 / 64, 1), dim3(256), 0, s,
+                       la, m->wb3, B, 512, 512, ep);
+  }
+  auto wgrad_conv = [&](auto lx, const bf16* dz, int M, int KIN, int N, int target_chunks, float* gW, float* gb, auto nb_tag) {
+    constexpr int NB = decltype(nb_tag)::value;
+    int m_chunk = (int)align_up((M + target_chunks - 1) / target_chunks, 32);
+    if (m_chunk < 128) m_chunk = 128;
+    const int chunks = (M + m_chunk - 1) / m_chunk;
+    hipLaunchKernelGGL((k_wgrad<NB, decltype(lx)>), dim3(KIN / 64, N / NB, chunks), dim3(256), 0, s, lx, dz, M, N, m_chunk,
+                       w.slab, N, (size_t)KIN * N, w.bslab);
+    hipLaunchKernelGGL(k_slab_reduce, dim3(std::min(1024, (KIN * N + 255) / 256)), dim3(256), 0, s, w.slab, (size_t)KIN * N,
+                       chunks, (size_t)KIN * N, gW);
+    hipLaunchKernelGGL(k_slab_reduce, dim3(1), dim3(256), 0, s, w.bslab, (size_t)N, chunks, (size_t)N, gb);
+  };
+  // conv3: dW2 = im2col(a2)^T dz3; dz2 = convT(dz3, W2) * (a2 > 0)
+  wgrad_conv(LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 64, G + var_offset(4),
+             G + var_offset(5), std::integral_constant<int, 64>{});
+  {
+    LoadConvT<9, 9, 7, 7, 64, 3, 1> la{w.dz3, B * 81};
+    EpiReluMask ep{w.dz2, w.a2, 64};
+    hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiReluMask>), dim3((B * 81 + 127) / 128, 1, 1), dim3(256), 0, s, la,
+                       m->wb2, B * 81, 576, 576, ep);
+  }
+  // conv2: dW1 = im2col(a1)^T dz2; dz1 = convT(dz2, W1) * (a1 > 0)
+  wgrad_conv(LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 64, G + var_offset(2),
+             G + var_offset(3), std::integral_constant<int, 64>{});
+  {
+    LoadConvT<20, 20, 9, 9, 64, 4, 2> la{w.dz2, B * 400};
+    EpiReluMask ep{w.dz1, w.a1, 32};
+    hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, decltype(la), EpiReluMask>), dim3((B * 400 + 127) / 128, 1, 1), dim3(256), 0, s,
+                       la, m->wb1, B * 400, 1024, 1024, ep);
+  }
+  // conv1: dW0 = im2col_s2d(x)^T dz1 (s2d k order -> HWIO)
+  wgrad_conv(LoadConv1{table, B * 400}, w.dz1, B * 400, 256, 32, 128, w.g0_s2d, G + var_offset(1),
+             std::integral_constant<int, 32>{});
+  hipLaunchKernelGGL(k_conv1_grad_unpermute, dim3(32), dim3(256), 0, s, w.g0_s2d, G);
+  QLX_HIP(hipGetLastError());
+}
+
+void model_norms(qlx_model* m, hipStream_t s, float scale) {
+  hipLaunchKernelGGL(k_sumsq, dim3(m->n_ranges), dim3(256), 0, s, m->d_grads, m->d_rbeg, m->d_rend, scale, m->d_partial);
+  hipLaunchKernelGGL(k_norms, dim3(1), dim3(64), 0, s, m->d_partial, m->d_var_first, m->d_norms);
+  QLX_HIP(hipGetLastError());
+}
+
+void model_adam(qlx_model* m, hipStream_t s, float scale) {
+  const int64_t t = m->iterations + 1;
+  const float tf = (float)t;
+  const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
+  AdamArgs a;
+  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.norms = m->d_norms;
+  a.count = kNumParams; a.scale = scale;
+  a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
+  a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
+  a.pack = pack_ptrs(m);
+  hipLaunchKernelGGL(k_adam, dim3(2048), dim3(256), 0, s, a);
+  QLX_HIP(hipGetLastError());
+  m->iterations = t;
+}
+
+void model_frame_table_from_host(qlx_model* m, const uint8_t* obs_host, int B) {
+  model_workspace(m, B);
+  uint8_t* d_obs = nullptr;
+  const size_t bytes = (size_t)B * kFramePix * 4;
+  QLX_HIP(hipMalloc(&d_obs, bytes));
+  QLX_HIP(hipMemcpyAsync(d_obs, obs_host, bytes, hipMemcpyHostToDevice, m->stream));
+  hipLaunchKernelGGL(k_pack_obs, dim3((B * kFramePix + 255) / 256), dim3(256), 0, m->stream, d_obs, B, m->w.frames);
+  hipLaunchKernelGGL(k_frame_table, dim3((B * 4 + 255) / 256), dim3(256), 0, m->stream, m->w.frames, B, m->w.table);
+  QLX_HIP(hipGetLastError());
+  QLX_HIP(hipStreamSynchronize(m->stream));
+  QLX_HIP(hipFree(d_obs));
+}
+
+static void glorot_host(std::vector<float>& params, uint64_t seed) {
+  const int fan_in[5] = {8 * 8 * 4, 4 * 4 * 32, 3 * 3 * 64, 3136, 512};
+  const int fan_out[5] = {8 * 8 * 32, 4 * 4 * 64, 3 * 3 * 64, 512, 3};
+  params.assign(kNumParams, 0.0f);
+  int64_t off = 0;
+  for (int v = 0; v < kNumVars; ++v) {
+    if (v % 2 == 0) {
+      const int l = v / 2;
+      const float limit = std::sqrt(6.0f / (float)(fan_in[l] + fan_out[l]));
+      RngStream s(seed, (uint32_t)v, 0, P_INIT);
+      for (int i = 0; i < kVarSize[v]; ++i) params[off + i] = uniform_f32(s, -limit, limit);
+    }
+    off += kVarSize[v];
+  }
+}
+
+}  // namespace qlx
+
+using namespace qlx;
+
+extern "C" {
+
+int32_t qlx_model_num_vars(void) { return kNumVars; }
+int64_t qlx_model_var_size(int32_t v) { return (v >= 0 && v < kNumVars) ? kVarSize[v] : -1; }
+
+int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out) {
+  return guard([&] {
+    QLX_CHECK(arch == QLX_ARCH_NATURE_DQN && out, QLX_E_INVALID, "unknown model arch");
+    current_device_checked(device);
+    auto* m = new qlx_model;
+    m->device = device;
+    QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+    const size_t pb = kNumParams * sizeof(float);
+    QLX_HIP(hipMalloc(&m->d_params, pb));
+    QLX_HIP(hipMalloc(&m->d_m, pb));
+    QLX_HIP(hipMalloc(&m->d_v, pb));
+    QLX_HIP(hipMalloc(&m->d_grads, pb));
+    QLX_HIP(hipMalloc(&m->wf0, 32 * 256 * 2));
+    QLX_HIP(hipMalloc(&m->wf1, 64 * 512 * 2));
+    QLX_HIP(hipMalloc(&m->wb1, 32 * 1024 * 2));
+    QLX_HIP(hipMalloc(&m->wf2, 64 * 576 * 2));
+    QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
+    QLX_HIP(hipMalloc(&m->wf3, 512 * 3136 * 2));
+    QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
+    // norm ranges: chunks of <= 16384 elements that never cross a variable
+    std::vector<int64_t> rb, re;
+    std::vector<int> vf(kNumVars + 1, 0);
+    int64_t off = 0;
+    for (int v = 0; v < kNumVars; ++v) {
+      vf[v] = (int)rb.size();
+      for (int64_t i = 0; i < kVarSize[v]; i += 16384) {
+        rb.push_back(off + i);
+        re.push_back(off + std::min<int64_t>(kVarSize[v], i + 16384));
+      }
+      off += kVarSize[v];
+    }
+    vf[kNumVars] = (int)rb.size();
+    m->n_ranges = (int)rb.size();
+    QLX_HIP(hipMalloc(&m->d_rbeg, rb.size() * 8));
+    QLX_HIP(hipMalloc(&m->d_rend, re.size() * 8));
+    QLX_HIP(hipMalloc(&m->d_partial, rb.size() * 4));
+    QLX_HIP(hipMalloc(&m->d_var_first, vf.size() * 4));
+    QLX_HIP(hipMalloc(&m->d_norms, 64));
+    QLX_HIP(hipMemcpy(m->d_rbeg, rb.data(), rb.size() * 8, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_rend, re.data(), re.size() * 8, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_var_first, vf.data(), vf.size() * 4, hipMemcpyHostToDevice));
+    std::vector<float> params;
+    glorot_host(params, seed);
+    QLX_HIP(hipMemcpy(m->d_params, params.data(), pb, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemset(m->d_m, 0, pb));
+    QLX_HIP(hipMemset(m->d_v, 0, pb));
+    QLX_HIP(hipMemset(m->d_grads, 0, pb));
+    model_pack(m);
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    *out = m;
+  });
+}
+
+int32_t qlx_model_destroy(qlx_model* m) {
+  return guard([&] {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    (void)hipStreamSynchronize(m->stream);
+    void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wf3, m->wb3,
+                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->ws};
+    for (void* p : ptrs) (void)hipFree(p);
+    if (m->own_stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+  });
+}
+
+int32_t qlx_model_get_var(qlx_model* m, int32_t var, int32_t which, float* out) {
+  return guard([&] {
+    QLX_CHECK(m && out && var >= 0 && var < kNumVars && which >= 0 && which <= 2, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipSetDevice(m->device));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    const float* src = (which == 0 ? m->d_params : which == 1 ? m->d_m : m->d_v) + var_offset(var);
+    QLX_HIP(hipMemcpy(out, src, kVarSize[var] * sizeof(float), hipMemcpyDeviceToHost));
+  });
+}
+
+int32_t qlx_model_set_var(qlx_model* m, int32_t var, int32_t which, const float* in) {
+  return guard([&] {
+    QLX_CHECK(m && in && var >= 0 && var < kNumVars && which >= 0 && which <= 2, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipSetDevice(m->device));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    float* dst = (which == 0 ? m->d_params : which == 1 ? m->d_m : m->d_v) + var_offset(var);
+    QLX_HIP(hipMemcpy(dst, in, kVarSize[var] * sizeof(float), hipMemcpyHostToDevice));
+    if (which == 0) { model_pack(m); QLX_HIP(hipStreamSynchronize(m->stream)); }
+  });
+}
+
+int64_t qlx_model_iterations(qlx_model* m) { return m ? m->iterations : -1; }
+
+int32_t qlx_model_copy_weights(qlx_model* dst, const qlx_model* src) {
+  return guard([&] {
+    QLX_CHECK(dst && src, QLX_E_INVALID, "null model");
+    QLX_HIP(hipSetDevice(dst->device));
+    QLX_HIP(hipStreamSynchronize(src->stream));
+    QLX_HIP(hipMemcpyAsync(dst->d_params, src->d_params, kNumParams * sizeof(float), hipMemcpyDeviceToDevice, dst->stream));
+    model_pack(dst);
+    QLX_HIP(hipStreamSynchronize(dst->stream));
+  });
+}
+
+int32_t qlx_model_predict(qlx_model* m, const uint8_t* obs, uint32_t n, float* q_out, uint8_t* actions) {
+  return guard([&] {
+    QLX_CHECK(m && obs && n > 0, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipSetDevice(m->device));
+    model_frame_table_from_host(m, obs, (int)n);
+    model_forward_trunk(m, m->w.table, (int)n, m->stream);
+    Fc2Args a = fc2_args(m, (int)n);
+    a.argmax = m->w.argmax;
+    hipLaunchKernelGGL(k_fc2<1>, dim3((n + 3) / 4), dim3(256), 0, m->stream, a);
+    QLX_HIP(hipGetLastError());
+    if (q_out) QLX_HIP(hipMemcpyAsync(q_out, m->w.q, n * 3 * sizeof(float), hipMemcpyDeviceToHost, m->stream));
+    if (actions) QLX_HIP(hipMemcpyAsync(actions, m->w.argmax, n, hipMemcpyDeviceToHost, m->stream));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+  });
+}
+
+int32_t qlx_model_batch_max_q(qlx_model* m, const uint8_t* obs, uint32_t n, float* out) {
+  return guard([&] {
+    QLX_CHECK(m && obs && out && n > 0, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipSetDevice(m->device));
+    model_frame_table_from_host(m, obs, (int)n);
+    model_forward_trunk(m, m->w.table, (int)n, m->stream);
+    // y = 0 + max * 1 with done = 0: the bare reduce_max of the reference signature
+    QLX_HIP(hipMemsetAsync(m->w.rew, 0, n * 4, m->stream));
+    QLX_HIP(hipMemsetAsync(m->w.done, 0, n, m->stream));
+    Fc2Args a = fc2_args(m, (int)n);
+    a.rewards = m->w.rew; a.dones = m->w.done; a.gamma = 1.0f; a.y_out = m->w.y;
+    hipLaunchKernelGGL(k_fc2<2>, dim3((n + 3) / 4), dim3(256), 0, m->stream, a);
+    QLX_HIP(hipGetLastError());
+    QLX_HIP(hipMemcpyAsync(out, m->w.y, n * sizeof(float), hipMemcpyDeviceToHost, m->stream));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+  });
+}
+
+int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions, const float* y, uint32_t B,
+                        float* loss_out, float* grads_out, float* norms_out) {
+  return guard([&] {
+    QLX_CHECK(m && obs && actions && y && B > 0, QLX_E_INVALID, "bad argument");
+    for (uint32_t b = 0; b < B; ++b) QLX_CHECK(actions[b] < kActions, QLX_E_INVALID, "action out of range");
+    QLX_HIP(hipSetDevice(m->device));
+    model_frame_table_from_host(m, obs, (int)B);
+    hipStream_t s = m->stream;
+    QLX_HIP(hipMemcpyAsync(m->w.act, actions, B, hipMemcpyHostToDevice, s));
+    QLX_HIP(hipMemcpyAsync(m->w.y, y, B * 4, hipMemcpyHostToDevice, s));
+    model_forward_trunk(m, m->w.table, (int)B, s);
+    Fc2Args a = fc2_args(m, (int)B);
+    a.actions = m->w.act; a.y = m->w.y; a.gsample = m->w.gs; a.hsample = m->w.hs;
+    hipLaunchKernelGGL(k_fc2<3>, dim3((B + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, m->w.hs, (int)B, m->w.loss);
+    model_backward(m, m->w.table, (int)B, m->w.act, s);
+    if (grads_out) QLX_HIP(hipMemcpyAsync(grads_out, m->d_grads, kNumParams * 4, hipMemcpyDeviceToHost, s));
+    model_norms(m, s, 1.0f);
+    model_adam(m, s, 1.0f);
+    if (norms_out) QLX_HIP(hipMemcpyAsync(norms_out, m->d_norms, kNumVars * 4, hipMemcpyDeviceToHost, s));
+    if (loss_out) QLX_HIP(hipMemcpyAsync(loss_out, m->w.loss, 4, hipMemcpyDeviceToHost, s));
+    QLX_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
+  return guard([&] {
+    QLX_CHECK(m && out && layer >= 1 && layer <= 4 && m->ws_batch > 0, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    const size_t per[5] = {0, 12800, 5184, 3136, 512};
+    const bf16* src = layer == 1 ? m->w.a1 : layer == 2 ? m->w.a2 : layer == 3 ? m->w.a3 : m->w.a4;
+    const size_t count = per[layer] * (size_t)m->last_batch;
+    std::vector<uint16_t> tmp(count);
+    QLX_HIP(hipMemcpy(tmp.data(), src, count * 2, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < count; ++i) {
+      const uint32_t b = (uint32_t)tmp[i] << 16;
+      std::memcpy(&out[i], &b, 4);
+    }
+  });
+}
+
+int32_t qlx_model_write_checkpoint(qlx_model* m, const char* path) {
+  return guard([&] {
+    QLX_CHECK(m && path, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    std::vector<float> buf(kNumParams * 3);
+    QLX_HIP(hipMemcpy(buf.data(), m->d_params, kNumParams * 4, hipMemcpyDeviceToHost));
+    QLX_HIP(hipMemcpy(buf.data() + kNumParams, m->d_m, kNumParams * 4, hipMemcpyDeviceToHost));
+    QLX_HIP(hipMemcpy(buf.data() + 2 * kNumParams, m->d_v, kNumParams * 4, hipMemcpyDeviceToHost));
+    FILE* f = std::fopen(path, "wb");
+    QLX_CHECK(f, QLX_E_IO, std::string("cannot open ") + path);
+    const char magic[8] = {'Q', 'L', 'X', 'C', 'K', 'P', 'T', '1'};
+    const int64_t hdr[2] = {kNumParams, m->iterations};
+    bool ok = std::fwrite(magic, 1, 8, f) == 8 && std::fwrite(hdr, 8, 2, f) == 2 &&
+              std::fwrite(buf.data(), 4, buf.size(), f) == buf.size();
+    ok = (std::fclose(f) == 0) && ok;
+    QLX_CHECK(ok, QLX_E_IO, "checkpoint write failed");
+  });
+}
+
+int32_t qlx_model_read_checkpoint(qlx_model* m, const char* path) {
+  return guard([&] {
+    QLX_CHECK(m && path, QLX_E_INVALID, "bad argument");
+    FILE* f = std::fopen(path, "rb");
+    QLX_CHECK(f, QLX_E_IO, std::string("cannot open ") + path);
+    char magic[8];
+    int64_t hdr[2];
+    std::vector<float> buf(kNumParams * 3);
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "QLXCKPT1", 8) == 0 && std::fread(hdr, 8, 2, f) == 2 &&
+              hdr[0] == kNumParams && std::fread(buf.data(), 4, buf.size(), f) == buf.size();
+    std::fclose(f);
+    QLX_CHECK(ok, QLX_E_IO, "not a qlx checkpoint");
+    QLX_HIP(hipSetDevice(m->device));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    QLX_HIP(hipMemcpy(m->d_params, buf.data(), kNumParams * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_m, buf.data() + kNumParams, kNumParams * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_v, buf.data() + 2 * kNumParams, kNumParams * 4, hipMemcpyHostToDevice));
+    m->iterations = hdr[1];
+    model_pack(m);
+    QLX_HIP(hipStreamSynchronize(m->stream));
+  });
+}
+
+int32_t qlx_model_sync(qlx_model* m) {
+  return guard([&] {
+    QLX_CHECK(m, QLX_E_INVALID, "null model");
+    QLX_HIP(hipStreamSynchronize(m->stream));
+  });
+}
+
+}  // extern "C"

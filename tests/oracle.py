@@ -1,0 +1,331 @@
+"""ctypes view of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+The oracle is the checker: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.
+Struct layouts mirror oracle/oracle_api.cpp and oracle/learner_ref.h.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+STATE_DTYPE = np.dtype([
+    ("ball_x", "<f4"), ("ball_y", "<f4"), ("dir_x", "<f4"), ("dir_y", "<f4"),
+    ("panel_min_x", "<f4"), ("panel_min_y", "<f4"), ("panel_max_x", "<f4"), ("panel_max_y", "<f4"),
+    ("panel_speed", "<f4"),
+    ("score", "<u4"), ("finished", "<u4"), ("next_slot", "<u4"), ("fault", "<u4"), ("reset_count", "<u4"),
+    ("bricks", "<u8"),
+])
+assert STATE_DTYPE.itemsize == 64
+
+
+class LearnerParams(C.Structure):
+    _fields_ = [
+        ("gamma", C.c_float),
+        ("lowest_episode_reward_goal_threshold_pct", C.c_float),
+        ("epsilon_max", C.c_double),
+        ("epsilon_min", C.c_double),
+        ("epsilon_greedy_steps", C.c_double),
+        ("max_steps_per_episode", C.c_uint64),
+        ("epsilon_pure_random_steps", C.c_uint64),
+        ("history_buffer_len", C.c_uint64),
+        ("update_after_actions", C.c_uint64),
+        ("target_sync_steps", C.c_uint64),
+        ("episode_reward_history_buffer_len", C.c_uint64),
+        ("n_envs", C.c_uint32),
+        ("batch_size", C.c_uint32),
+        ("env_seed", C.c_uint64),
+        ("learner_seed", C.c_uint64),
+        ("init_seed", C.c_uint64),
+        ("rank", C.c_uint32),
+        ("pad", C.c_uint32),
+    ]
+
+
+def default_params(**kw):
+    """Parameter::default() (self_driving_tf_q_learner.rs:50-67) + build fields."""
+    p = LearnerParams(gamma=0.99, lowest_episode_reward_goal_threshold_pct=0.9, epsilon_max=1.0,
+                      epsilon_min=0.1, epsilon_greedy_steps=1_000_000.0, max_steps_per_episode=10_000,
+                      epsilon_pure_random_steps=50_000, history_buffer_len=1_000_000, update_after_actions=4,
+                      target_sync_steps=0, episode_reward_history_buffer_len=100, n_envs=1, batch_size=32,
+                      env_seed=0x51A5EED, learner_seed=1, init_seed=2, rank=0, pad=0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+VAR_SHAPES = [(8, 8, 4, 32), (32,), (4, 4, 32, 64), (64,), (3, 3, 64, 64), (64,), (3136, 512), (512,), (512, 3), (3,)]
+VAR_SIZES = [int(np.prod(s)) for s in VAR_SHAPES]
+STATE_BYTES = 84 * 84 * 4
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(LIB_PATH)
+        vp, u64, u32, f32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_float, C.c_int
+        L.orc_philox.argtypes = [vp, vp, vp]
+        L.orc_stream_u32.argtypes = [u64, u32, u32, u32, u64, i32, vp]
+        L.orc_gen_range_f32.argtypes = [u64, u32, u32, u32, f32, f32]
+        L.orc_gen_range_f32.restype = f32
+        L.orc_gen_f64_01.argtypes = [u64, u32, u32, u32]
+        L.orc_gen_f64_01.restype = C.c_double
+        L.orc_gen_u8.argtypes = [u64, u32, u32, u32, u64, i32]
+        L.orc_sample_distinct.argtypes = [u64, u32, u32, u64, i32, vp]
+        L.orc_synth_actions.argtypes = [u64, u32, u32, vp]
+        for n in ("orc_wall_left", "orc_wall_right"):
+            getattr(L, n).argtypes = [f32] * 5 + [vp]
+        L.orc_rect_check.argtypes = [f32] * 9 + [vp]
+        L.orc_acos_threshold.restype = f32
+        L.orc_env_new.argtypes = [u64, u32]
+        L.orc_env_new.restype = vp
+        L.orc_env_free.argtypes = [vp]
+        L.orc_env_reset.argtypes = [vp]
+        L.orc_env_step.argtypes = [vp, i32, vp, vp]
+        L.orc_env_state.argtypes = [vp, vp]
+        L.orc_env_tensor.argtypes = [vp, vp]
+        L.orc_env_frame.argtypes = [vp, i32, vp]
+        L.orc_envs_run.argtypes = [u64, u32, u32, u64, u64, vp, vp, vp, vp, vp]
+        L.orc_qnet_new.argtypes = [u64]
+        L.orc_qnet_new.restype = vp
+        L.orc_qnet_free.argtypes = [vp]
+        L.orc_qnet_get.argtypes = [vp, i32, i32, vp]
+        L.orc_qnet_set.argtypes = [vp, i32, i32, vp]
+        L.orc_qnet_iterations.argtypes = [vp]
+        L.orc_qnet_iterations.restype = C.c_int64
+        L.orc_qnet_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+        L.orc_qnet_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
+        L.orc_qnet_train.restype = f32
+        L.orc_learner_new.argtypes = [C.POINTER(LearnerParams)]
+        L.orc_learner_new.restype = vp
+        L.orc_learner_free.argtypes = [vp]
+        L.orc_learner_vector_step.argtypes = [vp]
+        L.orc_learner_qnet.argtypes = [vp, i32]
+        L.orc_learner_qnet.restype = vp
+        L.orc_learner_counters.argtypes = [vp, vp, C.POINTER(C.c_double), C.POINTER(C.c_float)]
+        L.orc_learner_last.argtypes = [vp] * 8
+        L.orc_learner_last.restype = i32
+        L.orc_learner_env_state.argtypes = [vp, u32, vp]
+        L.orc_learner_env_tensor.argtypes = [vp, u32, vp]
+        L.orc_learner_replay_get.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+        L.orc_learner_params_size.restype = C.c_size_t
+        L.orc_state_size.restype = C.c_size_t
+        assert L.orc_learner_params_size() == C.sizeof(LearnerParams)
+        assert L.orc_state_size() == STATE_DTYPE.itemsize
+        _lib = L
+    return _lib
+
+
+def philox(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().orc_philox(_p(c), _p(k), _p(out))
+    return out
+
+
+def stream_u32(seed, c1, c2, purpose, start, n):
+    out = np.zeros(n, dtype=np.uint32)
+    lib().orc_stream_u32(seed, c1, c2, purpose, start, n, _p(out))
+    return out
+
+
+def sample_distinct(seed, update_idx, rank, length, B):
+    out = np.zeros(B, dtype=np.uint64)
+    lib().orc_sample_distinct(seed, update_idx, rank, length, B, _p(out))
+    return out
+
+
+def synth_actions(action_seed, n_envs, step):
+    out = np.zeros(n_envs, dtype=np.uint8)
+    lib().orc_synth_actions(action_seed, n_envs, step, _p(out))
+    return out
+
+
+def _surface(fn, *args):
+    out = np.zeros(4, dtype=np.float32)
+    hit = fn(*[float(a) for a in args], _p(out))
+    return (float(out[0]), float(out[1]), float(out[2]), float(out[3])) if hit else None
+
+
+def wall_left(center, radius, mv):
+    return _surface(lib().orc_wall_left, center[0], center[1], radius, mv[0], mv[1])
+
+
+def wall_right(center, radius, mv):
+    return _surface(lib().orc_wall_right, center[0], center[1], radius, mv[0], mv[1])
+
+
+def rect_check(center, radius, mv, lo, hi):
+    return _surface(lib().orc_rect_check, center[0], center[1], radius, mv[0], mv[1], lo[0], lo[1], hi[0], hi[1])
+
+
+class Env:
+    """Single Breakout env (BreakoutEnvironment restatement)."""
+
+    def __init__(self, seed, env_id=0):
+        self.h = lib().orc_env_new(seed, env_id)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_env_free(self.h)
+            self.h = None
+
+    def reset(self):
+        lib().orc_env_reset(self.h)
+
+    def step(self, action):
+        r = C.c_float()
+        d = C.c_int()
+        lib().orc_env_step(self.h, int(action), C.byref(r), C.byref(d))
+        return r.value, bool(d.value)
+
+    def state(self):
+        s = np.zeros(1, dtype=STATE_DTYPE)
+        lib().orc_env_state(self.h, _p(s))
+        return s[0]
+
+    def tensor(self):
+        t = np.zeros((84, 84, 4), dtype=np.uint8)
+        lib().orc_env_tensor(self.h, _p(t))
+        return t
+
+    def frame(self, slot):
+        f = np.zeros((84, 84), dtype=np.uint8)
+        lib().orc_env_frame(self.h, slot, _p(f))
+        return f
+
+
+def envs_run(env_seed, n_envs, n_steps, action_seed, max_steps=10_000, want_tensors=False):
+    st = np.zeros(n_envs, dtype=STATE_DTYPE)
+    h = np.zeros(n_envs, dtype=np.uint64)
+    tr = np.zeros(n_envs, dtype=np.float32)
+    ep = np.zeros(n_envs, dtype=np.uint32)
+    tens = np.zeros((n_envs, 84, 84, 4), dtype=np.uint8) if want_tensors else None
+    lib().orc_envs_run(env_seed, n_envs, n_steps, action_seed, max_steps, _p(st), _p(h), _p(tr), _p(ep), _p(tens))
+    return st, h, tr, ep, tens
+
+
+class QNet:
+    def __init__(self, seed=2, handle=None, owned=True):
+        self.owned = handle is None and owned
+        self.h = handle if handle is not None else lib().orc_qnet_new(seed)
+
+    def __del__(self):
+        if getattr(self, "owned", False) and self.h:
+            lib().orc_qnet_free(self.h)
+            self.h = None
+
+    def get(self, var, which=0):
+        out = np.zeros(VAR_SIZES[var], dtype=np.float32)
+        lib().orc_qnet_get(self.h, var, which, _p(out))
+        return out.reshape(VAR_SHAPES[var])
+
+    def set(self, var, arr, which=0):
+        a = np.ascontiguousarray(arr, dtype=np.float32).reshape(-1)
+        assert a.size == VAR_SIZES[var]
+        lib().orc_qnet_set(self.h, var, which, _p(a))
+
+    def weights(self):
+        return [self.get(v) for v in range(10)]
+
+    def iterations(self):
+        return lib().orc_qnet_iterations(self.h)
+
+    def forward(self, x, acts=False):
+        x = np.ascontiguousarray(x, dtype=np.uint8)
+        B = x.shape[0]
+        q = np.zeros((B, 3), dtype=np.float32)
+        a = [np.zeros((B, 20, 20, 32), np.float32), np.zeros((B, 9, 9, 64), np.float32),
+             np.zeros((B, 7, 7, 64), np.float32), np.zeros((B, 512), np.float32)] if acts else [None] * 4
+        lib().orc_qnet_forward(self.h, _p(x), B, _p(q), *[_p(t) for t in a])
+        return (q, a) if acts else q
+
+    def train(self, x, actions, y):
+        x = np.ascontiguousarray(x, dtype=np.uint8)
+        a = np.ascontiguousarray(actions, dtype=np.uint8)
+        y = np.ascontiguousarray(y, dtype=np.float32)
+        grads = np.zeros(sum(VAR_SIZES), dtype=np.float32)
+        norms = np.zeros(10, dtype=np.float32)
+        loss = lib().orc_qnet_train(self.h, _p(x), _p(a), _p(y), x.shape[0], _p(grads), _p(norms))
+        out, off = [], 0
+        for v in range(10):
+            out.append(grads[off:off + VAR_SIZES[v]].reshape(VAR_SHAPES[v]))
+            off += VAR_SIZES[v]
+        return loss, out, norms
+
+
+class Learner:
+    def __init__(self, params):
+        self.params = params
+        self.N = params.n_envs
+        self.B = params.batch_size
+        self.h = lib().orc_learner_new(C.byref(params))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_learner_free(self.h)
+            self.h = None
+
+    def vector_step(self):
+        lib().orc_learner_vector_step(self.h)
+
+    def counters(self):
+        out = np.zeros(6, dtype=np.uint64)
+        eps = C.c_double()
+        rr = C.c_float()
+        lib().orc_learner_counters(self.h, _p(out), C.byref(eps), C.byref(rr))
+        keys = ["step_count", "vec_steps", "update_count", "episode_count", "replay_len", "solved"]
+        d = {k: int(v) for k, v in zip(keys, out)}
+        d["epsilon"] = eps.value
+        d["running_reward"] = rr.value
+        return d
+
+    def last(self, max_updates=4096):
+        N, B = self.N, self.B
+        a = np.zeros(N, np.uint8)
+        r = np.zeros(N, np.float32)
+        d = np.zeros(N, np.uint8)
+        losses = np.zeros(max_updates, np.float32)
+        idx = np.zeros(max_updates * B, np.uint64)
+        tg = np.zeros(max_updates * B, np.float32)
+        q = np.zeros((N, 3), np.float32)
+        n = lib().orc_learner_last(self.h, _p(a), _p(r), _p(d), _p(losses), _p(idx), _p(tg), _p(q))
+        return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
+                    targets=tg[:n * B].reshape(n, B), q=q)
+
+    def qnet(self, which=0):
+        return QNet(handle=lib().orc_learner_qnet(self.h, which), owned=False)
+
+    def env_state(self, e):
+        s = np.zeros(1, dtype=STATE_DTYPE)
+        lib().orc_learner_env_state(self.h, e, _p(s))
+        return s[0]
+
+    def env_tensor(self, e):
+        t = np.zeros((84, 84, 4), np.uint8)
+        lib().orc_learner_env_tensor(self.h, e, _p(t))
+        return t
+
+    def replay_get(self, idx):
+        idx = np.ascontiguousarray(idx, dtype=np.uint64)
+        B = idx.size
+        s = np.zeros((B, 84, 84, 4), np.uint8)
+        sn = np.zeros((B, 84, 84, 4), np.uint8)
+        a = np.zeros(B, np.uint8)
+        r = np.zeros(B, np.float32)
+        d = np.zeros(B, np.uint8)
+        lib().orc_learner_replay_get(self.h, _p(idx), B, _p(s), _p(sn), _p(a), _p(r), _p(d))
+        return s, sn, a, r, d
