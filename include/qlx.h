@@ -191,10 +191,15 @@ qlx_model* qlx_learner_model(qlx_learner* l, int32_t which /* 0 online, 1 target
  * all-reduced (mean) before clip_by_norm + Adam. uid from qlx_dist_unique_id on rank 0. */
 int32_t qlx_dist_unique_id(uint8_t out[128]);
 int32_t qlx_learner_dist_init(qlx_learner* l, int32_t world, int32_t rank, const uint8_t uid[128]);
-/* Kernel timing: average device time (us) per launch of the named kernel class over the last run
- * (measured with HIP events on the learner stream); names: "conv", "env", "replay", "adam", "all". */
+/* Kernel timing with HIP events on the learner stream.  Scopes are named per kernel ("conv1_fwd",
+ * "conv1_wgrad", "fc1_fwd", "adam", "env_step", "replay_push", ...) or per phase ("act_forward",
+ * "gather", "sample"); each carries its algorithmic work (FLOPs for GEMM kernels, bytes for
+ * HBM-bound ones).  filter = one scope name records only that scope (NULL = all). */
 int32_t qlx_learner_profile(qlx_learner* l, int32_t enable);
-int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* avg_us, uint64_t* launches);
+int32_t qlx_learner_profile_filter(qlx_learner* l, const char* name_or_null);
+int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* total_us, double* total_work,
+                                uint64_t* launches);
+int32_t qlx_learner_profile_names(qlx_learner* l, char* buf, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -164,6 +164,7 @@ void orc_qnet_set(void* h, int var, int which, const float* in) {
   std::memcpy(dst.data(), in, dst.size() * sizeof(float));
 }
 int64_t orc_qnet_iterations(void* h) { return ((QNet*)h)->iterations; }
+void orc_qnet_set_iterations(void* h, int64_t it) { ((QNet*)h)->iterations = it; }
 void orc_qnet_forward(void* h, const uint8_t* x, int B, float* q, float* a1, float* a2, float* a3, float* a4) {
   Acts a;
   qnet_forward(*(QNet*)h, x, B, a);

@@ -324,13 +324,14 @@ __device__ void time_step(State& s, uint32_t action, float acos_thr) {
 // ---------------------------------------------------------------------------------------
 // kernels
 
-__global__ void k_env_init(State* st, uint32_t* ep_steps, uint32_t n, uint64_t seed, const uint8_t* mask, int bump) {
+__global__ void k_env_init(State* st, uint32_t* ep_steps, uint32_t n, uint64_t seed, uint32_t id_offset, const uint8_t* mask,
+                           int bump) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   if (mask && !mask[e]) return;
   const uint32_t rc = bump ? st[e].reset_count + 1 : 0;
   State s;
-  init_state(s, seed, e, rc);
+  init_state(s, seed, id_offset + e, rc);
   st[e] = s;
   ep_steps[e] = 0;
 }
@@ -472,7 +473,7 @@ void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, u
 void env_launch_reset(qlx_env* env, const uint8_t* d_mask, int bump) {
   const uint32_t n = env->n;
   hipLaunchKernelGGL(k_env_init, dim3((n + 255) / 256), dim3(256), 0, env->stream, env->d_state, env->d_ep_steps, n,
-                     env->seed, d_mask, bump);
+                     env->seed, env->id_offset, d_mask, bump);
   hipLaunchKernelGGL(k_env_clear_frames, dim3(2, n), dim3(256), 0, env->stream, env->d_obs, n, d_mask);
   QLX_HIP(hipGetLastError());
 }

@@ -1,2 +1,549 @@
-// placeholder, replaced by the learner
+// SelfDrivingQLearner on one MI355X: the env-step -> replay-sample -> Q-net update loop, vectorised over
+// n_envs and enqueued on one HIP stream with no host synchronisation per step.
+//
+// Reference (restated): self_driving_tf_q_learner.rs:94-116 (new: online + stabilized model, same init),
+// :141-233 (learn_episode: epsilon-greedy with pure-random warm-up, epsilon decay per step, replay add,
+// train every update_after_actions steps once len > B, Bellman target r + gamma * max Q_target(s') or r
+// if done, episode bookkeeping + running_reward), :134-139 (solved), :276-296 (distinct ids).
+// Vector-step generalisation (N = 1 is the reference loop): DESIGN.md "Learner semantics".
+#include <hip/hip_runtime.h>
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
 #include "objects.h"
+#include "profiler.h"
+#include "qnet.h"
+#include "replay_dev.h"
+
+namespace qlx {
+
+ReplayView replay_view(const qlx_replay* rb);
+
+// ---- acting: epsilon-greedy (self_driving_tf_q_learner.rs:153-167) --------------------------
+// step_count of env e in this vector step = step_before + e + 1; epsilon used = eps_table[step_count - 1]
+// (value after step_count - 1 decrements). Draws: f64 from words 0-1, the random action from word 2 on.
+__global__ void k_select_actions(uint32_t n, uint64_t step_before, uint64_t pure_random, const double* eps_table,
+                                 uint64_t eps_len, double eps_min, uint64_t seed, uint32_t id_offset, uint32_t vec_step,
+                                 const float* q, uint8_t* actions) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint64_t sc = step_before + e + 1;
+  bool random = sc < pure_random;
+  if (!random) {
+    RngStream su(seed, id_offset + e, vec_step, P_ACT, 0);
+    const double eps = (sc - 1) < eps_len ? eps_table[sc - 1] : eps_min;
+    random = eps > uniform_f64_01(su);
+  }
+  uint8_t a;
+  if (random) {
+    RngStream sa(seed, id_offset + e, vec_step, P_ACT, 2);
+    a = (uint8_t)uniform_u8(sa, kActions);
+  } else {   // tf.argmax over Q(s): first maximal index
+    const float q0 = q[e * 3], q1 = q[e * 3 + 1], q2 = q[e * 3 + 2];
+    int best = 0;
+    float bv = q0;
+    if (q1 > bv) { best = 1; bv = q1; }
+    if (q2 > bv) best = 2;
+    a = (uint8_t)best;
+  }
+  actions[e] = a;
+}
+
+// ---- episode bookkeeping (learn_episode :172-174, :214-224) -----------------------------------
+struct Book {
+  uint64_t episode_count;
+  float running_reward;
+  uint32_t hist_len;     // current entries in the episode reward ring
+  uint32_t hist_head;    // index of the oldest entry
+};
+
+// One wave, envs in order: ep_reward += r; an env whose episode ended (done, or max_steps_per_episode
+// steps) pushes its reward into the FIFO of episode rewards, refreshes running_reward once
+// episode_count >= hist cap (sequential f32 sum, oldest first), counts the episode and is marked for reset.
+__global__ __launch_bounds__(64) void k_episode_book(uint32_t n, const float* rewards, const uint8_t* dones,
+                                                     const uint32_t* ep_steps, uint64_t max_steps, float* ep_reward,
+                                                     float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask) {
+  const int lane = threadIdx.x;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t e = base + lane;
+    bool end = false;
+    float er = 0.0f;
+    if (e < n) {
+      er = ep_reward[e] + rewards[e];
+      end = dones[e] || ep_steps[e] >= max_steps;
+      ep_reward[e] = end ? 0.0f : er;
+      reset_mask[e] = end ? 1 : 0;
+    }
+    unsigned long long bal = __ballot(end);
+    while (bal) {
+      const int l = __builtin_ctzll(bal);
+      bal &= bal - 1;
+      const float v = __shfl(er, l);
+      if (lane == 0) {
+        Book b = *book;
+        if (b.hist_len < hist_cap) {
+          hist[(b.hist_head + b.hist_len) % hist_cap] = v;
+          b.hist_len += 1;
+        } else {
+          hist[b.hist_head] = v;
+          b.hist_head = (b.hist_head + 1) % hist_cap;
+        }
+        if (b.episode_count >= hist_cap) {
+          float s = 0.0f;
+          for (uint32_t i = 0; i < b.hist_len; ++i) s += hist[(b.hist_head + i) % hist_cap];
+          b.running_reward = s / (float)b.hist_len;
+        }
+        b.episode_count += 1;
+        *book = b;
+      }
+    }
+  }
+}
+
+// ---- replay sample gather: frame pointer tables + metadata of one update ------------------------
+__global__ void k_gather(ReplayView r, const uint64_t* idx, uint32_t B, const uint8_t** tab_s, const uint8_t** tab_sn,
+                         uint8_t* act, float* rew, uint8_t* done) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t i = idx[b];
+  const uint8_t* f[4];
+  replay_frames(r, i, 0, f);
+  for (int j = 0; j < 4; ++j) tab_s[b * 4 + j] = f[j];
+  replay_frames(r, i, 1, f);
+  for (int j = 0; j < 4; ++j) tab_sn[b * 4 + j] = f[j];
+  const uint64_t t = (r.total - r.len + i) % r.cap;
+  act[b] = r.action[t];
+  rew[b] = r.reward[t];
+  done[b] = r.done[t];
+}
+
+__global__ void k_obs_table(const uint8_t* obs, uint32_t n, const uint8_t** table) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * 4) table[i] = obs + (size_t)i * kFramePix;
+}
+
+}  // namespace qlx
+
+struct qlx_learner {
+  qlx_params p{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  qlx_env* env = nullptr;
+  qlx_replay* rb = nullptr;
+  qlx_model* online = nullptr;
+  qlx_model* target = nullptr;
+  uint32_t N = 0, B = 0;
+  // device buffers
+  uint8_t* d_actions = nullptr;
+  float* d_rewards = nullptr;
+  uint8_t* d_dones = nullptr;
+  uint8_t* d_reset = nullptr;
+  const uint8_t** d_obs_table = nullptr;
+  double* d_eps = nullptr;
+  uint64_t eps_len = 0;
+  float* d_ep_reward = nullptr;
+  float* d_hist = nullptr;
+  qlx::Book* d_book = nullptr;
+  uint64_t* d_idx = nullptr;       // [max_updates][B]
+  const uint8_t** d_tab_s = nullptr;
+  const uint8_t** d_tab_sn = nullptr;
+  uint8_t* d_bact = nullptr;
+  float* d_brew = nullptr;
+  uint8_t* d_bdone = nullptr;
+  float* d_losses = nullptr;       // [max_updates]
+  float* d_targets = nullptr;      // [max_updates][B]
+  uint32_t max_updates = 0;
+  // host counters
+  uint64_t step_count = 0, vec_steps = 0, update_count = 0;
+  uint32_t last_updates = 0;
+  // data parallel
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  qlx::Profiler prof;
+};
+
+namespace qlx {
+
+static void learner_update(qlx_learner* L, uint32_t u_local) {
+  hipStream_t s = L->stream;
+  const uint32_t B = L->B;
+  qlx_model* on = L->online;
+  qlx_model* tg = L->target;
+  const ReplayView rv = replay_view(L->rb);
+  {
+    ProfScope ps(&L->prof, "gather", s);
+    hipLaunchKernelGGL(k_gather, dim3((B + 255) / 256), dim3(256), 0, s, rv, L->d_idx + (size_t)u_local * B, B, L->d_tab_s,
+                       L->d_tab_sn, L->d_bact, L->d_brew, L->d_bdone);
+  }
+  // target: y = r + gamma * max_a Q_target(s')  (or r if done)
+  model_forward_trunk(tg, L->d_tab_sn, (int)B, s);
+  Fc2Args ta = fc2_args(tg, (int)B);
+  ta.rewards = L->d_brew;
+  ta.dones = L->d_bdone;
+  ta.gamma = L->p.gamma;
+  ta.y_out = L->d_targets + (size_t)u_local * B;
+  launch_fc2(2, ta, (int)B, s);
+  // online: forward, Huber, backward
+  model_forward_trunk(on, L->d_tab_s, (int)B, s);
+  Fc2Args oa = fc2_args(on, (int)B);
+  oa.actions = L->d_bact;
+  oa.y = L->d_targets + (size_t)u_local * B;
+  oa.gsample = on->w.gs;
+  oa.hsample = on->w.hs;
+  launch_fc2(3, oa, (int)B, s);
+  launch_loss_sum(on->w.hs, (int)B, L->d_losses + u_local, s);
+  model_backward(on, L->d_tab_s, (int)B, L->d_bact, s);
+  float scale = 1.0f;
+  if (L->comm) {
+    ProfScope ps(&L->prof, "allreduce", s);
+    const ncclResult_t r = ncclAllReduce(on->d_grads, on->d_grads, (size_t)kNumParams, ncclFloat, ncclSum, L->comm, s);
+    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    scale = 1.0f / (float)L->world;
+  }
+  model_norms(on, s, scale);
+  model_adam(on, s, scale);
+  L->update_count += 1;
+}
+
+static void learner_vector_step(qlx_learner* L) {
+  hipStream_t s = L->stream;
+  const uint32_t N = L->N;
+  const uint64_t step_before = L->step_count;
+  // ---- act
+  const bool any_greedy = step_before + N >= L->p.epsilon_pure_random_steps;
+  if (any_greedy) {
+    ProfScope ps(&L->prof, "act_forward", s);
+    model_forward_trunk(L->online, L->d_obs_table, (int)N, s);
+    Fc2Args a = fc2_args(L->online, (int)N);
+    launch_fc2(0, a, (int)N, s);
+  }
+  {
+    ProfScope ps(&L->prof, "select", s);
+    hipLaunchKernelGGL(k_select_actions, dim3((N + 255) / 256), dim3(256), 0, s, N, step_before,
+                       L->p.epsilon_pure_random_steps, L->d_eps, L->eps_len, L->p.epsilon_min, L->p.learner_seed,
+                       (uint32_t)L->rank * N, (uint32_t)L->vec_steps, L->online->w.q, L->d_actions);
+  }
+  L->step_count += N;
+  // ---- env step (physics + frame) and replay push
+  {
+    ProfScope ps(&L->prof, "env_step", s, 7190.0 * N);   // state r/w + new frame + action/reward/done
+    env_launch_step(L->env, L->d_actions, L->d_rewards, L->d_dones);
+  }
+  {
+    ProfScope ps(&L->prof, "replay_push", s, 2.0 * 7056.0 * N + 10.0 * N);   // frame read + write + metadata
+    replay_launch_push(L->rb, L->env, s, L->d_actions, L->d_rewards, L->d_dones);
+  }
+  {
+    ProfScope ps(&L->prof, "episode_reset", s);
+    hipLaunchKernelGGL(k_episode_book, dim3(1), dim3(64), 0, s, N, L->d_rewards, L->d_dones, L->env->d_ep_steps,
+                       L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
+                       (uint32_t)L->p.episode_reward_history_buffer_len, L->d_book, L->d_reset);
+    env_launch_reset(L->env, L->d_reset, 1);
+  }
+  // ---- training updates
+  const uint64_t ua = L->p.update_after_actions;
+  const uint64_t triggers = L->step_count / ua - step_before / ua;
+  L->last_updates = 0;
+  if (L->rb->len() > L->B && triggers > 0) {
+    const uint32_t U = (uint32_t)triggers;
+    QLX_CHECK(U <= L->max_updates, QLX_E_STATE, "too many updates per vector step");
+    {
+      ProfScope ps(&L->prof, "sample", s);
+      replay_launch_sample(L->rb, s, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank, L->B, L->d_idx);
+    }
+    for (uint32_t u = 0; u < U; ++u) learner_update(L, u);
+    L->last_updates = U;
+  }
+  const uint64_t ts = L->p.target_sync_steps;
+  if (ts > 0 && L->step_count / ts != step_before / ts) {
+    QLX_HIP(hipMemcpyAsync(L->target->d_params, L->online->d_params, kNumParams * sizeof(float), hipMemcpyDeviceToDevice, s));
+    model_pack(L->target);
+  }
+  L->vec_steps += 1;
+  QLX_HIP(hipGetLastError());
+}
+
+}  // namespace qlx
+
+using namespace qlx;
+
+extern "C" {
+
+void qlx_params_default(qlx_params* p) {
+  std::memset(p, 0, sizeof(*p));
+  p->gamma = 0.99f;
+  p->lowest_episode_reward_goal_threshold_pct = 0.9f;
+  p->epsilon_max = 1.0;
+  p->epsilon_min = 0.1;
+  p->epsilon_greedy_steps = 1000000.0;
+  p->max_steps_per_episode = 10000;
+  p->epsilon_pure_random_steps = 50000;
+  p->history_buffer_len = 1000000;
+  p->update_after_actions = 4;
+  p->target_sync_steps = 0;
+  p->episode_reward_history_buffer_len = 100;
+  p->n_envs = 1;
+  p->batch_size = 32;
+  p->env_seed = 0x51A5EED;
+  p->learner_seed = 1;
+  p->init_seed = 2;
+}
+
+int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** out) {
+  return guard([&] {
+    QLX_CHECK(p && out, QLX_E_INVALID, "null argument");
+    QLX_CHECK(p->n_envs > 0 && p->batch_size > 0 && p->batch_size <= 4096, QLX_E_INVALID, "bad n_envs / batch_size");
+    QLX_CHECK(p->update_after_actions > 0 && p->history_buffer_len >= p->batch_size, QLX_E_INVALID, "bad parameters");
+    QLX_CHECK(p->episode_reward_history_buffer_len > 0, QLX_E_INVALID, "episode_reward_history_buffer_len must be > 0");
+    current_device_checked(device);
+    auto* L = new qlx_learner;
+    L->p = *p;
+    L->device = device;
+    L->N = p->n_envs;
+    L->B = p->batch_size;
+    L->rank = (int)p->rank;
+    QLX_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+    int32_t st;
+    st = qlx_env_create(QLX_ENV_BREAKOUT, L->N, p->env_seed, device, &L->env);
+    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+    st = qlx_replay_create(p->history_buffer_len, L->N, device, &L->rb);
+    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+    st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->online);
+    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+    st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->target);   // same initial weights
+    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+    // everything runs on the learner's stream
+    L->env->stream = L->stream; L->env->own_stream = false;
+    L->rb->stream = L->stream; L->rb->own_stream = false;
+    L->online->stream = L->stream; L->online->own_stream = false;
+    L->target->stream = L->stream; L->target->own_stream = false;
+    L->env->hashing = false;
+    // re-seat env ids for data-parallel ranks (ball launch streams are per global env id)
+    if (p->rank != 0) {
+      L->env->id_offset = p->rank * L->N;
+      env_launch_reset(L->env, nullptr, 0);
+    }
+    // epsilon table: eps_k after k decrements, k = 0.. until epsilon_min (repeated f64 subtraction)
+    std::vector<double> eps;
+    double e = p->epsilon_max;
+    const double delta = (p->epsilon_max - p->epsilon_min) / p->epsilon_greedy_steps;
+    const size_t cap = 1u << 26;
+    while (eps.size() < cap) {
+      eps.push_back(e);
+      if (e <= p->epsilon_min) break;
+      e = std::max(e - delta, p->epsilon_min);
+    }
+    L->eps_len = eps.size();
+    QLX_HIP(hipMalloc(&L->d_eps, eps.size() * sizeof(double)));
+    QLX_HIP(hipMemcpy(L->d_eps, eps.data(), eps.size() * sizeof(double), hipMemcpyHostToDevice));
+    const uint32_t N = L->N, B = L->B;
+    L->max_updates = (uint32_t)(N / p->update_after_actions + 2);
+    QLX_HIP(hipMalloc(&L->d_actions, N));
+    QLX_HIP(hipMalloc(&L->d_rewards, N * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_dones, N));
+    QLX_HIP(hipMalloc(&L->d_reset, N));
+    QLX_HIP(hipMalloc(&L->d_obs_table, N * 4 * sizeof(void*)));
+    QLX_HIP(hipMalloc(&L->d_ep_reward, N * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
+    QLX_HIP(hipMalloc(&L->d_idx, (size_t)L->max_updates * B * sizeof(uint64_t)));
+    QLX_HIP(hipMalloc(&L->d_tab_s, (size_t)B * 4 * sizeof(void*)));
+    QLX_HIP(hipMalloc(&L->d_tab_sn, (size_t)B * 4 * sizeof(void*)));
+    QLX_HIP(hipMalloc(&L->d_bact, B));
+    QLX_HIP(hipMalloc(&L->d_brew, B * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_bdone, B));
+    QLX_HIP(hipMalloc(&L->d_losses, L->max_updates * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_targets, (size_t)L->max_updates * B * sizeof(float)));
+    QLX_HIP(hipMemsetAsync(L->d_ep_reward, 0, N * sizeof(float), L->stream));
+    QLX_HIP(hipMemsetAsync(L->d_book, 0, sizeof(Book), L->stream));
+    QLX_HIP(hipMemsetAsync(L->d_actions, 0, N, L->stream));
+    QLX_HIP(hipMemsetAsync(L->d_rewards, 0, N * sizeof(float), L->stream));
+    QLX_HIP(hipMemsetAsync(L->d_dones, 0, N, L->stream));
+    hipLaunchKernelGGL(k_obs_table, dim3((N * 4 + 255) / 256), dim3(256), 0, L->stream, L->env->d_obs, N, L->d_obs_table);
+    QLX_HIP(hipGetLastError());
+    model_workspace(L->online, (int)std::max(N, B));
+    model_workspace(L->target, (int)B);
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    *out = L;
+  });
+}
+
+int32_t qlx_learner_destroy(qlx_learner* L) {
+  return guard([&] {
+    if (!L) return;
+    (void)hipSetDevice(L->device);
+    (void)hipStreamSynchronize(L->stream);
+    if (L->comm) (void)ncclCommDestroy(L->comm);
+    qlx_env_destroy(L->env);
+    qlx_replay_destroy(L->rb);
+    qlx_model_destroy(L->online);
+    qlx_model_destroy(L->target);
+    void* ptrs[] = {L->d_actions, L->d_rewards, L->d_dones, L->d_reset, (void*)L->d_obs_table, L->d_eps, L->d_ep_reward,
+                    L->d_hist, L->d_book, L->d_idx, (void*)L->d_tab_s, (void*)L->d_tab_sn, L->d_bact, L->d_brew,
+                    L->d_bdone, L->d_losses, L->d_targets};
+    for (void* p : ptrs) (void)hipFree(p);
+    (void)hipStreamDestroy(L->stream);
+    delete L;
+  });
+}
+
+int32_t qlx_learner_vector_step(qlx_learner* L) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipSetDevice(L->device));
+    learner_vector_step(L);
+  });
+}
+
+int32_t qlx_learner_run(qlx_learner* L, uint64_t n) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipSetDevice(L->device));
+    for (uint64_t i = 0; i < n; ++i) learner_vector_step(L);
+  });
+}
+
+int32_t qlx_learner_sync(qlx_learner* L) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    QLX_HIP(hipDeviceSynchronize());
+    L->prof.collect();
+  });
+}
+
+int32_t qlx_learner_stats_get(qlx_learner* L, qlx_learner_stats* out) {
+  return guard([&] {
+    QLX_CHECK(L && out, QLX_E_INVALID, "null argument");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    Book b;
+    QLX_HIP(hipMemcpy(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost));
+    std::vector<float> hist(b.hist_len);
+    if (b.hist_len) {
+      std::vector<float> ring(L->p.episode_reward_history_buffer_len);
+      QLX_HIP(hipMemcpy(ring.data(), L->d_hist, ring.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (uint32_t i = 0; i < b.hist_len; ++i) hist[i] = ring[(b.hist_head + i) % ring.size()];
+    }
+    out->step_count = L->step_count;
+    out->vec_steps = L->vec_steps;
+    out->update_count = L->update_count;
+    out->episode_count = b.episode_count;
+    out->replay_len = L->rb->len();
+    // epsilon after step_count decrements
+    double e = L->p.epsilon_max;
+    if (L->step_count < L->eps_len) {
+      QLX_HIP(hipMemcpy(&e, L->d_eps + L->step_count, sizeof(double), hipMemcpyDeviceToHost));
+    } else {
+      e = L->p.epsilon_min;
+    }
+    out->epsilon = e;
+    out->running_reward = b.running_reward;
+    // solved (:134-139): running_reward >= goal && min episode reward >= goal * pct
+    const float goal = (float)(kNumBricks - 1);
+    float mn = hist.empty() ? 0.0f : hist[0];
+    for (float v : hist) mn = std::min(mn, v);
+    out->solved = (!hist.empty() && b.running_reward >= goal && mn >= goal * L->p.lowest_episode_reward_goal_threshold_pct) ? 1 : 0;
+    float loss = 0.0f;
+    if (L->last_updates) QLX_HIP(hipMemcpy(&loss, L->d_losses + L->last_updates - 1, 4, hipMemcpyDeviceToHost));
+    out->last_loss = loss;
+  });
+}
+
+int32_t qlx_learner_last(qlx_learner* L, uint8_t* actions, float* rewards, uint8_t* dones, float* losses,
+                         uint64_t* indices, float* targets, uint32_t* n_updates) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    const uint32_t U = L->last_updates;
+    if (actions) QLX_HIP(hipMemcpy(actions, L->d_actions, L->N, hipMemcpyDeviceToHost));
+    if (rewards) QLX_HIP(hipMemcpy(rewards, L->d_rewards, L->N * sizeof(float), hipMemcpyDeviceToHost));
+    if (dones) QLX_HIP(hipMemcpy(dones, L->d_dones, L->N, hipMemcpyDeviceToHost));
+    if (U && losses) QLX_HIP(hipMemcpy(losses, L->d_losses, U * sizeof(float), hipMemcpyDeviceToHost));
+    if (U && indices) QLX_HIP(hipMemcpy(indices, L->d_idx, (size_t)U * L->B * 8, hipMemcpyDeviceToHost));
+    if (U && targets) QLX_HIP(hipMemcpy(targets, L->d_targets, (size_t)U * L->B * 4, hipMemcpyDeviceToHost));
+    if (n_updates) *n_updates = U;
+  });
+}
+
+qlx_env* qlx_learner_env(qlx_learner* L) { return L ? L->env : nullptr; }
+qlx_replay* qlx_learner_replay(qlx_learner* L) { return L ? L->rb : nullptr; }
+qlx_model* qlx_learner_model(qlx_learner* L, int32_t which) { return L ? (which == 0 ? L->online : L->target) : nullptr; }
+
+int32_t qlx_dist_unique_id(uint8_t out[128]) {
+  return guard([&] {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(out, &id, 128);
+  });
+}
+
+int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const uint8_t uid[128]) {
+  return guard([&] {
+    QLX_CHECK(L && uid && world >= 1 && rank >= 0 && rank < world, QLX_E_INVALID, "bad argument");
+    QLX_CHECK(rank == L->rank, QLX_E_INVALID, "rank differs from qlx_params.rank");
+    if (world == 1) return;
+    QLX_HIP(hipSetDevice(L->device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid, 128);
+    const ncclResult_t r = ncclCommInitRank(&L->comm, world, id, rank);
+    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    L->world = world;
+    L->rank = rank;
+  });
+}
+
+int32_t qlx_learner_profile(qlx_learner* L, int32_t enable) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    L->prof.reset();
+    L->prof.enabled = enable != 0;
+    L->online->prof = enable ? &L->prof : nullptr;
+    L->target->prof = enable ? &L->prof : nullptr;
+  });
+}
+
+int32_t qlx_learner_profile_filter(qlx_learner* L, const char* name) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    L->prof.collect();
+    L->prof.filter = name ? name : "";
+  });
+}
+
+int32_t qlx_learner_profile_get(qlx_learner* L, const char* name, double* total_us, double* total_work,
+                                uint64_t* launches) {
+  return guard([&] {
+    QLX_CHECK(L && name && total_us && total_work && launches, QLX_E_INVALID, "null argument");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    L->prof.collect();
+    auto it = L->prof.acc.find(name);
+    if (it == L->prof.acc.end()) { *total_us = 0.0; *total_work = 0.0; *launches = 0; return; }
+    *total_us = it->second.us;
+    *total_work = it->second.work;
+    *launches = it->second.launches;
+  });
+}
+
+int32_t qlx_learner_profile_names(qlx_learner* L, char* buf, size_t cap) {
+  return guard([&] {
+    QLX_CHECK(L && buf && cap > 0, QLX_E_INVALID, "null argument");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    L->prof.collect();
+    std::string s;
+    for (auto& kv : L->prof.acc) { if (!s.empty()) s += ","; s += kv.first; }
+    QLX_CHECK(s.size() < cap, QLX_E_INVALID, "buffer too small");
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+  });
+}
+
+}  // extern "C"

@@ -10,6 +10,7 @@ struct qlx_env {
   int device = 0;
   uint32_t n = 0;
   uint64_t seed = 0;
+  uint32_t id_offset = 0;         // global id of env 0 (data-parallel ranks own disjoint ids)
   hipStream_t stream = nullptr;   // owned unless adopted by a learner
   bool own_stream = true;
   qlx_breakout_state* d_state = nullptr;

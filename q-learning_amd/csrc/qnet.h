@@ -4,6 +4,7 @@
 
 #include <cstdint>
 
+#include "profiler.h"
 #include "qlx_internal.h"
 
 namespace qlx {
@@ -53,10 +54,29 @@ struct qlx_model {
   int ws_batch = 0;
   int last_batch = 0;
   qlx::ModelWs w;
+  qlx::Profiler* prof = nullptr;   // set by the learner while profiling
 };
 
 namespace qlx {
-struct Fc2Args;
+struct Fc2Args {
+  const __bf16* a4;          // [B][512]
+  const float* w4;         // [512][3] master
+  const float* b4;         // [3]
+  int B;
+  float* q;                // [B][3] out (may be null)
+  uint8_t* argmax;         // mode 1
+  const float* rewards;    // mode 2
+  const uint8_t* dones;    // mode 2
+  float gamma;             // mode 2
+  float* y_out;            // mode 2
+  const uint8_t* actions;  // mode 3
+  const float* y;          // mode 3
+  float* gsample;          // mode 3: dloss/dq_a per sample
+  float* hsample;          // mode 3: per-sample Huber value
+};
+Fc2Args fc2_args(qlx_model* m, int B);
+void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s);
+void launch_loss_sum(const float* h, int B, float* out, hipStream_t s);
 void model_workspace(qlx_model* m, int B);
 void model_pack(qlx_model* m);
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);

@@ -16,6 +16,7 @@
 #include "objects.h"
 #include "qnet.h"
 #include "qnet_kernels.h"
+#include "profiler.h"
 
 namespace qlx {
 
@@ -54,7 +55,9 @@ __device__ __forceinline__ void pack_one(const PackPtrs& P, int64_t idx, float w
   if (idx < 32768) {   // conv2 kernel [4][4][32][64]
     const int oc = idx & 63, c = (idx >> 6) & 31, tap = (int)(idx >> 11);   // tap = kh*4 + kw
     P.wf1[oc * 512 + tap * 32 + c] = v;
-    P.wb1[c * 1024 + tap * 64 + oc] = v;
+    // backward data by parity class p = (kh&1)*2 + (kw&1): [p*32 + c][(kh>>1)*2 + (kw>>1)][oc]
+    const int kh = tap >> 2, kw = tap & 3, p = (kh & 1) * 2 + (kw & 1);
+    P.wb1[(p * 32 + c) * 256 + ((kh >> 1) * 2 + (kw >> 1)) * 64 + oc] = v;
     return;
   }
   idx -= 32768 + 64;
@@ -104,22 +107,7 @@ __global__ void k_frame_table(const uint8_t* frames, int B, const uint8_t** tabl
 // dense 512 -> 3 (linear) on VALU, one wave per sample; optional heads:
 //   mode 0: q only; mode 1: argmax actions (predict_action); mode 2: max -> Bellman target
 //   mode 3: Huber loss + dq for train (needs actions, y)
-struct Fc2Args {
-  const bf16* a4;          // [B][512]
-  const float* w4;         // [512][3] master
-  const float* b4;         // [3]
-  int B;
-  float* q;                // [B][3] out (may be null)
-  uint8_t* argmax;         // mode 1
-  const float* rewards;    // mode 2
-  const uint8_t* dones;    // mode 2
-  float gamma;             // mode 2
-  float* y_out;            // mode 2
-  const uint8_t* actions;  // mode 3
-  const float* y;          // mode 3
-  float* gsample;          // mode 3: dloss/dq_a per sample
-  float* hsample;          // mode 3: per-sample Huber value
-};
+
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_fc2(Fc2Args A) {
@@ -197,8 +185,19 @@ __global__ __launch_bounds__(256) void k_fc2_wgrad(const bf16* a4, const uint8_t
   }
 }
 
+void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s) {
+  const dim3 g((B + 3) / 4), blk(256);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(k_fc2<0>, g, blk, 0, s, a); break;
+    case 1: hipLaunchKernelGGL(k_fc2<1>, g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_fc2<2>, g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_fc2<3>, g, blk, 0, s, a); break;
+  }
+  QLX_HIP(hipGetLastError());
+}
+
 // loss = sum_b h_b / B in fixed order (one block)
-__global__ void k_loss_sum(const float* h, int B, float* loss) {
+__global__ void k_loss_sum(const float* h, int B, float* loss) {  // loss = sum_b h_b / B
   __shared__ float red[256];
   float s = 0.0f;
   for (int b = threadIdx.x; b < B; b += 256) s += h[b];
@@ -240,12 +239,22 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* g, const int64_t* ra
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-__global__ void k_norms(const float* partial, const int* var_first, float* norms) {
-  const int v = threadIdx.x;
-  if (v >= kNumVars) return;
+// one block per variable; fixed strided + tree order -> deterministic
+__global__ __launch_bounds__(256) void k_norms(const float* partial, const int* var_first, float* norms) {
+  __shared__ float red[256];
+  const int v = blockIdx.x;
   float s = 0.0f;
-  for (int r = var_first[v]; r < var_first[v + 1]; ++r) s += partial[r];
-  norms[v] = s > 0.0f ? sqrtf(s) : s;   // tf.clip_by_norm: safe sqrt via where(l2sum > 0)
+  for (int r = var_first[v] + threadIdx.x; r < var_first[v + 1]; r += 256) s += partial[r];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float t = red[0];
+    norms[v] = t > 0.0f ? sqrtf(t) : t;   // tf.clip_by_norm: safe sqrt via where(l2sum > 0)
+  }
 }
 
 struct AdamArgs {
@@ -346,24 +355,28 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
   m->last_batch = B;
   const float* p = m->d_params;
   {  // conv1: M = B*400, N = 32, K = 256
+    ProfScope ps(m->prof, "conv1_fwd", s, 2.0 * B * 400 * 32 * 256);
     LoadConv1 la{table, B * 400};
     EpiBiasRelu ep{w.a1, p + var_offset(1), 32};
     hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, LoadConv1, EpiBiasRelu>), dim3((B * 400 + 127) / 128, 1, 1), dim3(256), 0, s,
                        la, m->wf0, B * 400, 256, 256, ep);
   }
   {  // conv2: M = B*81, N = 64, K = 512
+    ProfScope ps(m->prof, "conv2_fwd", s, 2.0 * B * 81 * 64 * 512);
     LoadIm2col<20, 20, 32, 4, 2, 9, 9> la{w.a1, B * 81};
     EpiBiasRelu ep{w.a2, p + var_offset(3), 64};
     hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiBiasRelu>), dim3((B * 81 + 127) / 128, 1, 1), dim3(256), 0, s,
                        la, m->wf1, B * 81, 512, 512, ep);
   }
   {  // conv3: M = B*49, N = 64, K = 576
+    ProfScope ps(m->prof, "conv3_fwd", s, 2.0 * B * 49 * 64 * 576);
     LoadIm2col<9, 9, 64, 3, 1, 7, 7> la{w.a2, B * 49};
     EpiBiasRelu ep{w.a3, p + var_offset(5), 64};
     hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiBiasRelu>), dim3((B * 49 + 127) / 128, 1, 1), dim3(256), 0, s,
                        la, m->wf2, B * 49, 576, 576, ep);
   }
   {  // fc1: M = B, N = 512, K = 3136, split-K into kFc1Split partial slabs
+    ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
     LoadRows<3136> la{w.a3, B};
     EpiSlab ep{w.fc1slab, 512, (size_t)B * 512};
     hipLaunchKernelGGL((k_igemm<2, 2, 2, 2, LoadRows<3136>, EpiSlab>), dim3((B + 63) / 64, 512 / 64, kFc1Split), dim3(256), 0,
@@ -389,21 +402,30 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
   ModelWs& w = m->w;
   float* G = m->d_grads;
   // fc2
-  hipLaunchKernelGGL(k_fc2_bwd_data, dim3((B * 512 + 255) / 256), dim3(256), 0, s, w.a4, m->d_params + var_offset(8),
-                     actions, w.gs, B, w.dz4);
-  hipLaunchKernelGGL(k_fc2_wgrad, dim3(513), dim3(256), 0, s, w.a4, actions, w.gs, B, G + var_offset(8), G + var_offset(9));
+  {
+    ProfScope ps(m->prof, "fc2_bwd", s);
+    hipLaunchKernelGGL(k_fc2_bwd_data, dim3((B * 512 + 255) / 256), dim3(256), 0, s, w.a4, m->d_params + var_offset(8),
+                       actions, w.gs, B, w.dz4);
+    hipLaunchKernelGGL(k_fc2_wgrad, dim3(513), dim3(256), 0, s, w.a4, actions, w.gs, B, G + var_offset(8), G + var_offset(9));
+  }
   // fc1: dW3 = a3^T dz4 (one chunk), db3; dz3 = (dz4 W3^T) * (a3 > 0)
   {
     LoadRows<3136> lx{w.a3, B};
+    ProfScope ps(m->prof, "fc1_wgrad", s, 2.0 * B * 512 * 3136);
     hipLaunchKernelGGL((k_wgrad<64, LoadRows<3136>>), dim3(3136 / 64, 512 / 64, 1), dim3(256), 0, s, lx, w.dz4, B, 512,
                        align_up(B, 32), G + var_offset(6), 512, (size_t)0, w.bslab);
     hipLaunchKernelGGL(k_slab_reduce, dim3(2), dim3(256), 0, s, w.bslab, (size_t)512, 1, (size_t)512, G + var_offset(7));
+  }
+  {
+    ProfScope ps(m->prof, "fc1_dgrad", s, 2.0 * B * 512 * 3136);
     LoadRows<512> la{w.dz4, B};
     EpiReluMask ep{w.dz3, w.a3, 3136};
     hipLaunchKernelGGL((k_igemm<1, 4, 4, 1, LoadRows<512>, EpiReluMask>), dim3((B + 63) / 64, 3136 / 64, 1), dim3(256), 0, s,
                        la, m->wb3, B, 512, 512, ep);
   }
-  auto wgrad_conv = [&](auto lx, const bf16* dz, int M, int KIN, int N, int target_chunks, float* gW, float* gb, auto nb_tag) {
+  auto wgrad_conv = [&](const char* name, auto lx, const bf16* dz, int M, int KIN, int N, int target_chunks, float* gW, float* gb,
+                        auto nb_tag) {
+    ProfScope ps(m->prof, name, s, 2.0 * M * KIN * N);
     constexpr int NB = decltype(nb_tag)::value;
     int m_chunk = (int)align_up((M + target_chunks - 1) / target_chunks, 32);
     if (m_chunk < 128) m_chunk = 128;
@@ -415,33 +437,41 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     hipLaunchKernelGGL(k_slab_reduce, dim3(1), dim3(256), 0, s, w.bslab, (size_t)N, chunks, (size_t)N, gb);
   };
   // conv3: dW2 = im2col(a2)^T dz3; dz2 = convT(dz3, W2) * (a2 > 0)
-  wgrad_conv(LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 64, G + var_offset(4),
+  wgrad_conv("conv3_wgrad", LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 64, G + var_offset(4),
              G + var_offset(5), std::integral_constant<int, 64>{});
   {
+    ProfScope ps(m->prof, "conv3_dgrad", s, 2.0 * B * 49 * 64 * 576);
     LoadConvT<9, 9, 7, 7, 64, 3, 1> la{w.dz3, B * 81};
     EpiReluMask ep{w.dz2, w.a2, 64};
     hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiReluMask>), dim3((B * 81 + 127) / 128, 1, 1), dim3(256), 0, s, la,
                        m->wb2, B * 81, 576, 576, ep);
   }
   // conv2: dW1 = im2col(a1)^T dz2; dz1 = convT(dz2, W1) * (a1 > 0)
-  wgrad_conv(LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 64, G + var_offset(2),
+  wgrad_conv("conv2_wgrad", LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 64, G + var_offset(2),
              G + var_offset(3), std::integral_constant<int, 64>{});
   {
-    LoadConvT<20, 20, 9, 9, 64, 4, 2> la{w.dz2, B * 400};
-    EpiReluMask ep{w.dz1, w.a1, 32};
-    hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, decltype(la), EpiReluMask>), dim3((B * 400 + 127) / 128, 1, 1), dim3(256), 0, s,
-                       la, m->wb1, B * 400, 1024, 1024, ep);
+    ProfScope ps(m->prof, "conv2_dgrad", s, 2.0 * B * 81 * 64 * 512);
+    LoadConv2T la{w.dz2, B * 100};
+    EpiReluMaskConv2T ep{w.dz1, w.a1};
+    hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, LoadConv2T, EpiReluMaskConv2T>), dim3((B * 100 + 127) / 128, 4, 1), dim3(256), 0,
+                       s, la, m->wb1, B * 100, 256, 256, ep);
   }
   // conv1: dW0 = im2col_s2d(x)^T dz1 (s2d k order -> HWIO)
-  wgrad_conv(LoadConv1{table, B * 400}, w.dz1, B * 400, 256, 32, 128, w.g0_s2d, G + var_offset(1),
+  wgrad_conv("conv1_wgrad", LoadConv1{table, B * 400}, w.dz1, B * 400, 256, 32, 128, w.g0_s2d, G + var_offset(1),
              std::integral_constant<int, 32>{});
   hipLaunchKernelGGL(k_conv1_grad_unpermute, dim3(32), dim3(256), 0, s, w.g0_s2d, G);
   QLX_HIP(hipGetLastError());
 }
 
+void launch_loss_sum(const float* h, int B, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, h, B, out);
+  QLX_HIP(hipGetLastError());
+}
+
 void model_norms(qlx_model* m, hipStream_t s, float scale) {
+  ProfScope ps(m->prof, "norms", s);
   hipLaunchKernelGGL(k_sumsq, dim3(m->n_ranges), dim3(256), 0, s, m->d_grads, m->d_rbeg, m->d_rend, scale, m->d_partial);
-  hipLaunchKernelGGL(k_norms, dim3(1), dim3(64), 0, s, m->d_partial, m->d_var_first, m->d_norms);
+  hipLaunchKernelGGL(k_norms, dim3(kNumVars), dim3(256), 0, s, m->d_partial, m->d_var_first, m->d_norms);
   QLX_HIP(hipGetLastError());
 }
 
@@ -455,6 +485,7 @@ void model_adam(qlx_model* m, hipStream_t s, float scale) {
   a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
   a.pack = pack_ptrs(m);
+  ProfScope ps(m->prof, "adam", s, 32.0 * kNumParams);
   hipLaunchKernelGGL(k_adam, dim3(2048), dim3(256), 0, s, a);
   QLX_HIP(hipGetLastError());
   m->iterations = t;
@@ -517,15 +548,15 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
     QLX_HIP(hipMalloc(&m->wf3, 512 * 3136 * 2));
     QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
-    // norm ranges: chunks of <= 16384 elements that never cross a variable
+    // norm ranges: chunks of <= 2048 elements (~830 blocks) that never cross a variable
     std::vector<int64_t> rb, re;
     std::vector<int> vf(kNumVars + 1, 0);
     int64_t off = 0;
     for (int v = 0; v < kNumVars; ++v) {
       vf[v] = (int)rb.size();
-      for (int64_t i = 0; i < kVarSize[v]; i += 16384) {
+      for (int64_t i = 0; i < kVarSize[v]; i += 2048) {
         rb.push_back(off + i);
-        re.push_back(off + std::min<int64_t>(kVarSize[v], i + 16384));
+        re.push_back(off + std::min<int64_t>(kVarSize[v], i + 2048));
       }
       off += kVarSize[v];
     }

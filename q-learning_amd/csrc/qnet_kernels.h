@@ -106,6 +106,23 @@ struct LoadConvT {
   }
 };
 
+// conv2 backward data (4x4 stride 2, 20x20x32 <- 9x9x64) split by output parity class p = blockIdx.y:
+// (ih, iw) = (2i + ph, 2j + pw), rows m = (b*10 + i)*10 + j of one class; only taps kh = ph + 2th,
+// kw = pw + 2tw reach the class, so k = (th*2 + tw)*64 + oc (K = 256 instead of 1024 mostly-zero taps).
+struct LoadConv2T {
+  const bf16* dout;   // dz2 [B][9][9][64]
+  int M;              // B * 100 rows per class
+  __device__ __forceinline__ bf16x8 load(int m, int k0) const {
+    if (m >= M) return zero8();
+    const int b = m / 100, pos = m - b * 100;
+    const int i = pos / 10, j = pos - i * 10;
+    const int tap = k0 >> 6, oc = k0 & 63;
+    const int oh = i - (tap >> 1), ow = j - (tap & 1);
+    if (oh < 0 || ow < 0 || oh >= 9 || ow >= 9) return zero8();
+    return ld8(dout + (((size_t)b * 9 + oh) * 9 + ow) * 64 + oc);
+  }
+};
+
 // ------------------------------------------------------------------------------------------
 // Epilogues: consume acc tile element (m, n, value).
 
@@ -126,6 +143,18 @@ struct EpiReluMask {   // backward data: dz[m][n] = v * (act[m][n] > 0)
   __device__ __forceinline__ void operator()(int m, int n, float v) const {
     const size_t i = (size_t)m * ldo + n;
     out[i] = (bf16)((float)act[i] > 0.0f ? v : 0.0f);
+  }
+};
+
+struct EpiReluMaskConv2T {   // parity-class rows -> dz1[b][2i+ph][2j+pw][c] * (a1 > 0); n = p*32 + c
+  bf16* out;
+  const bf16* act;
+  __device__ __forceinline__ void operator()(int m, int n, float v) const {
+    const int p = n >> 5, c = n & 31;
+    const int b = m / 100, pos = m - b * 100;
+    const int i = pos / 10, j = pos - i * 10;
+    const size_t idx = (((size_t)b * 20 + 2 * i + (p >> 1)) * 20 + 2 * j + (p & 1)) * 32 + c;
+    out[idx] = (bf16)((float)act[idx] > 0.0f ? v : 0.0f);
   }
 };
 

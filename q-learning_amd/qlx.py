@@ -126,7 +126,9 @@ def lib():
         "qlx_learner_env": ([vp], vp), "qlx_learner_replay": ([vp], vp), "qlx_learner_model": ([vp, i32], vp),
         "qlx_dist_unique_id": ([vp], i32), "qlx_learner_dist_init": ([vp, i32, i32, vp], i32),
         "qlx_learner_profile": ([vp, i32], i32),
-        "qlx_learner_profile_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(u64)], i32),
+        "qlx_learner_profile_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)], i32),
+        "qlx_learner_profile_filter": ([vp, C.c_char_p], i32),
+        "qlx_learner_profile_names": ([vp, C.c_char_p, C.c_size_t], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name, None)
@@ -393,11 +395,21 @@ class SelfDrivingQLearner:
     def profile(self, enable=True):
         _check(lib().qlx_learner_profile(self.h, 1 if enable else 0))
 
+    def profile_filter(self, name=None):
+        _check(lib().qlx_learner_profile_filter(self.h, None if name is None else name.encode()))
+
     def profile_get(self, name):
+        """(total_us, total_work, launches) of a profiler scope since profile() was enabled."""
         us = C.c_double()
+        work = C.c_double()
         n = C.c_uint64()
-        _check(lib().qlx_learner_profile_get(self.h, name.encode(), C.byref(us), C.byref(n)))
-        return us.value, n.value
+        _check(lib().qlx_learner_profile_get(self.h, name.encode(), C.byref(us), C.byref(work), C.byref(n)))
+        return us.value, work.value, n.value
+
+    def profile_names(self):
+        buf = C.create_string_buffer(8192)
+        _check(lib().qlx_learner_profile_names(self.h, buf, 8192))
+        return [n for n in buf.value.decode().split(",") if n]
 
 
 def dist_unique_id():

@@ -105,6 +105,7 @@ def lib():
         L.orc_qnet_set.argtypes = [vp, i32, i32, vp]
         L.orc_qnet_iterations.argtypes = [vp]
         L.orc_qnet_iterations.restype = C.c_int64
+        L.orc_qnet_set_iterations.argtypes = [vp, C.c_int64]
         L.orc_qnet_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.orc_qnet_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
         L.orc_qnet_train.restype = f32
@@ -180,7 +181,8 @@ class Env:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_env_free(self.h)
+            if _lib is not None:
+                _lib.orc_env_free(self.h)
             self.h = None
 
     def reset(self):
@@ -225,7 +227,8 @@ class QNet:
 
     def __del__(self):
         if getattr(self, "owned", False) and self.h:
-            lib().orc_qnet_free(self.h)
+            if _lib is not None:
+                _lib.orc_qnet_free(self.h)
             self.h = None
 
     def get(self, var, which=0):
@@ -243,6 +246,16 @@ class QNet:
 
     def iterations(self):
         return lib().orc_qnet_iterations(self.h)
+
+    def set_iterations(self, it):
+        lib().orc_qnet_set_iterations(self.h, int(it))
+
+    def load_state_from(self, model):
+        """Copy weights, Adam slots and iteration count from a product model (lockstep tests)."""
+        for v in range(10):
+            for which in range(3):
+                self.set(v, model.get(v, which), which)
+        self.set_iterations(model.iterations())
 
     def forward(self, x, acts=False):
         x = np.ascontiguousarray(x, dtype=np.uint8)
@@ -276,7 +289,8 @@ class Learner:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_learner_free(self.h)
+            if _lib is not None:
+                _lib.orc_learner_free(self.h)
             self.h = None
 
     def vector_step(self):
