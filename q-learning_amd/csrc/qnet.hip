@@ -349,6 +349,23 @@ void model_pack(qlx_model* m) {
   QLX_HIP(hipGetLastError());
 }
 
+// k_igemm2 launch: persistent blocks (as many as LDS lets reside, <= 4 per CU on 256 CUs) over M tiles
+template <int BN, int WMT, int K, class LoadA, class Epi>
+static void launch_igemm2(LoadA la, const bf16* Bt, int M, int N, Epi epi, hipStream_t s) {
+  constexpr int BM = 4 * WMT * 32;
+  constexpr size_t lds = (size_t)BN * (K + 8) * sizeof(bf16);
+  static bool attr = false;
+  if (!attr) {
+    QLX_HIP(hipFuncSetAttribute((const void*)k_igemm2<BN, WMT, K, LoadA, Epi>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr = true;
+  }
+  const int n_mtiles = (M + BM - 1) / BM;
+  const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / lds)));
+  const int grid_x = std::min(n_mtiles, 256 * per_cu);
+  hipLaunchKernelGGL((k_igemm2<BN, WMT, K, LoadA, Epi>), dim3(grid_x, N / BN), dim3(256), lds, s, la, Bt, M, n_mtiles, epi);
+}
+
 // forward through fc1 (a1..a4 in the workspace); `table` = [B][4] frame pointers
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
   ModelWs& w = m->w;
@@ -356,24 +373,17 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
   const float* p = m->d_params;
   {  // conv1: M = B*400, N = 32, K = 256
     ProfScope ps(m->prof, "conv1_fwd", s, 2.0 * B * 400 * 32 * 256);
-    LoadConv1 la{table, B * 400};
-    EpiBiasRelu ep{w.a1, p + var_offset(1), 32};
-    hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, LoadConv1, EpiBiasRelu>), dim3((B * 400 + 127) / 128, 1, 1), dim3(256), 0, s,
-                       la, m->wf0, B * 400, 256, 256, ep);
+    launch_igemm2<32, 2, 256>(LoadConv1{table, B * 400}, m->wf0, B * 400, 32, EpiBiasRelu{w.a1, p + var_offset(1), 32}, s);
   }
   {  // conv2: M = B*81, N = 64, K = 512
     ProfScope ps(m->prof, "conv2_fwd", s, 2.0 * B * 81 * 64 * 512);
-    LoadIm2col<20, 20, 32, 4, 2, 9, 9> la{w.a1, B * 81};
-    EpiBiasRelu ep{w.a2, p + var_offset(3), 64};
-    hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiBiasRelu>), dim3((B * 81 + 127) / 128, 1, 1), dim3(256), 0, s,
-                       la, m->wf1, B * 81, 512, 512, ep);
+    launch_igemm2<64, 2, 512>(LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, m->wf1, B * 81, 64,
+                              EpiBiasRelu{w.a2, p + var_offset(3), 64}, s);
   }
   {  // conv3: M = B*49, N = 64, K = 576
     ProfScope ps(m->prof, "conv3_fwd", s, 2.0 * B * 49 * 64 * 576);
-    LoadIm2col<9, 9, 64, 3, 1, 7, 7> la{w.a2, B * 49};
-    EpiBiasRelu ep{w.a3, p + var_offset(5), 64};
-    hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiBiasRelu>), dim3((B * 49 + 127) / 128, 1, 1), dim3(256), 0, s,
-                       la, m->wf2, B * 49, 576, 576, ep);
+    launch_igemm2<64, 2, 576>(LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, m->wf2, B * 49, 64,
+                              EpiBiasRelu{w.a3, p + var_offset(5), 64}, s);
   }
   {  // fc1: M = B, N = 512, K = 3136, split-K into kFc1Split partial slabs
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
@@ -414,14 +424,11 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     ProfScope ps(m->prof, "fc1_wgrad", s, 2.0 * B * 512 * 3136);
     hipLaunchKernelGGL((k_wgrad<64, LoadRows<3136>>), dim3(3136 / 64, 512 / 64, 1), dim3(256), 0, s, lx, w.dz4, B, 512,
                        align_up(B, 32), G + var_offset(6), 512, (size_t)0, w.bslab);
-    hipLaunchKernelGGL(k_slab_reduce, dim3(2), dim3(256), 0, s, w.bslab, (size_t)512, 1, (size_t)512, G + var_offset(7));
+    hipLaunchKernelGGL(k_slab_reduce, dim3(512 / 64), dim3(256), 0, s, w.bslab, (size_t)512, 1, (size_t)512, G + var_offset(7));
   }
   {
     ProfScope ps(m->prof, "fc1_dgrad", s, 2.0 * B * 512 * 3136);
-    LoadRows<512> la{w.dz4, B};
-    EpiReluMask ep{w.dz3, w.a3, 3136};
-    hipLaunchKernelGGL((k_igemm<1, 4, 4, 1, LoadRows<512>, EpiReluMask>), dim3((B + 63) / 64, 3136 / 64, 1), dim3(256), 0, s,
-                       la, m->wb3, B, 512, 512, ep);
+    launch_igemm2<64, 2, 512>(LoadRows<512>{w.dz4, B}, m->wb3, B, 3136, EpiReluMask{w.dz3, w.a3, 3136}, s);
   }
   auto wgrad_conv = [&](const char* name, auto lx, const bf16* dz, int M, int KIN, int N, int target_chunks, float* gW, float* gb,
                         auto nb_tag) {
@@ -432,29 +439,24 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     const int chunks = (M + m_chunk - 1) / m_chunk;
     hipLaunchKernelGGL((k_wgrad<NB, decltype(lx)>), dim3(KIN / 64, N / NB, chunks), dim3(256), 0, s, lx, dz, M, N, m_chunk,
                        w.slab, N, (size_t)KIN * N, w.bslab);
-    hipLaunchKernelGGL(k_slab_reduce, dim3(std::min(1024, (KIN * N + 255) / 256)), dim3(256), 0, s, w.slab, (size_t)KIN * N,
-                       chunks, (size_t)KIN * N, gW);
-    hipLaunchKernelGGL(k_slab_reduce, dim3(1), dim3(256), 0, s, w.bslab, (size_t)N, chunks, (size_t)N, gb);
+    hipLaunchKernelGGL(k_slab_reduce, dim3((KIN * N + 63) / 64), dim3(256), 0, s, w.slab, (size_t)KIN * N, chunks,
+                       (size_t)KIN * N, gW);
+    hipLaunchKernelGGL(k_slab_reduce, dim3((N + 63) / 64), dim3(256), 0, s, w.bslab, (size_t)N, chunks, (size_t)N, gb);
   };
   // conv3: dW2 = im2col(a2)^T dz3; dz2 = convT(dz3, W2) * (a2 > 0)
   wgrad_conv("conv3_wgrad", LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 64, G + var_offset(4),
              G + var_offset(5), std::integral_constant<int, 64>{});
   {
     ProfScope ps(m->prof, "conv3_dgrad", s, 2.0 * B * 49 * 64 * 576);
-    LoadConvT<9, 9, 7, 7, 64, 3, 1> la{w.dz3, B * 81};
-    EpiReluMask ep{w.dz2, w.a2, 64};
-    hipLaunchKernelGGL((k_igemm<2, 4, 4, 1, decltype(la), EpiReluMask>), dim3((B * 81 + 127) / 128, 1, 1), dim3(256), 0, s, la,
-                       m->wb2, B * 81, 576, 576, ep);
+    launch_igemm2<64, 2, 576>(LoadConvT<9, 9, 7, 7, 64, 3, 1>{w.dz3, B * 81}, m->wb2, B * 81, 64,
+                              EpiReluMask{w.dz2, w.a2, 64}, s);
   }
   // conv2: dW1 = im2col(a1)^T dz2; dz1 = convT(dz2, W1) * (a1 > 0)
   wgrad_conv("conv2_wgrad", LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 64, G + var_offset(2),
              G + var_offset(3), std::integral_constant<int, 64>{});
   {
     ProfScope ps(m->prof, "conv2_dgrad", s, 2.0 * B * 81 * 64 * 512);
-    LoadConv2T la{w.dz2, B * 100};
-    EpiReluMaskConv2T ep{w.dz1, w.a1};
-    hipLaunchKernelGGL((k_igemm<2, 2, 4, 1, LoadConv2T, EpiReluMaskConv2T>), dim3((B * 100 + 127) / 128, 4, 1), dim3(256), 0,
-                       s, la, m->wb1, B * 100, 256, 256, ep);
+    launch_igemm2<32, 2, 256>(LoadConv2T{w.dz2, B * 100}, m->wb1, B * 100, 128, EpiReluMaskConv2T{w.dz1, w.a1}, s);
   }
   // conv1: dW0 = im2col_s2d(x)^T dz1 (s2d k order -> HWIO)
   wgrad_conv("conv1_wgrad", LoadConv1{table, B * 400}, w.dz1, B * 400, 256, 32, 128, w.g0_s2d, G + var_offset(1),

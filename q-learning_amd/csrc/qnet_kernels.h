@@ -220,6 +220,79 @@ __global__ __launch_bounds__(256) void k_igemm(LoadA la, const bf16* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
+// Implicit GEMM v2 for the conv-shaped layers (N = 32 / 64 per block, K <= 576):
+//   C[m][n] = sum_k A(m,k) Bt[n][k] with v_mfma_f32_32x32x16_bf16.
+// The block's B panel [BN][K] is staged once into LDS (row stride K+8 bf16: 16-B slot rotation makes the
+// 32-row ds_read_b128 fragment reads conflict-free) and reused by every M tile the persistent block
+// walks.  Each wave owns WMT x 32 rows x BN columns; A fragments (32 rows x 16 k, 16 B per lane) are
+// gathered by the loader straight into a depth-4 register ring, issued 4 k-steps ahead of their MFMAs.
+// Fragment maps (gfx950): A lane l = (row l&31, k 8(l>>5)+j); B lane l = (col l&31, k 8(l>>5)+j);
+// D reg i of lane l = (row (i&3) + 8(i>>2) + 4(l>>5), col l&31).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int BN, int WMT, int K, class LoadA, class Epi>
+__global__ __launch_bounds__(256, 2) void k_igemm2(LoadA la, const bf16* __restrict__ Bt, int M, int n_mtiles, Epi epi) {
+  constexpr int KP = K + 8;
+  constexpr int NT = BN / 32;
+  constexpr int BM = 4 * WMT * 32;
+  constexpr int KS = K / 16;
+  constexpr int D = 4;
+  static_assert(KS % D == 0, "K/16 must be a multiple of the pipeline depth");
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
+  const int n0 = blockIdx.y * BN;
+  for (int i = threadIdx.x; i < BN * (K / 8); i += 256) {
+    const int row = i / (K / 8), c = i - row * (K / 8);
+    *reinterpret_cast<uint4*>(lds_b + row * KP + c * 8) = *reinterpret_cast<const uint4*>(Bt + (size_t)(n0 + row) * K + c * 8);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const bf16* bbase = lds_b + r * KP + 8 * h;
+  for (int tile = blockIdx.x; tile < n_mtiles; tile += gridDim.x) {
+    const int m0 = tile * BM + wave * WMT * 32;
+    f32x16 acc[WMT][NT];
+#pragma unroll
+    for (int t = 0; t < WMT; ++t)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][j][e] = 0.0f;
+    bf16x8 a[D][WMT];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int t = 0; t < WMT; ++t) a[d][t] = la.load(m0 + t * 32 + r, d * 16 + 8 * h);
+#pragma unroll 1
+    for (int ks = 0; ks < KS; ks += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int k0 = (ks + d) * 16;
+        bf16x8 b[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bbase + j * 32 * KP + k0);
+#pragma unroll
+        for (int t = 0; t < WMT; ++t)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[t][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[d][t], b[j], acc[t][j], 0, 0, 0);
+        if (ks + d + D < KS) {
+#pragma unroll
+          for (int t = 0; t < WMT; ++t) a[d][t] = la.load(m0 + t * 32 + r, k0 + D * 16 + 8 * h);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < WMT; ++t)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + t * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (m < M) epi(m, n0 + j * 32 + r, acc[t][j][e]);
+        }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Weight gradient: dW[k][n] = sum_m X(m,k) dY[m][n]  (+ optional bias gradient db[n] = sum_m dY[m][n]).
 // Block = 4 waves, output tile 64 (k) x NB (n); grid = (KIN/64, N/NB, chunks); each block reduces its
 // m-chunk in steps of 32 rows staged in LDS, and writes an fp32 partial slab (reduced in fixed order
@@ -294,13 +367,29 @@ __global__ __launch_bounds__(256) void k_wgrad(LoadX lx, const bf16* __restrict_
   if (do_bias && tid < NB) bias_slab[(size_t)blockIdx.z * N + n0 + tid] = bsum;
 }
 
-// out[i] = sum_c slab[c][i] in chunk order (deterministic); optional bias/relu epilogue for split-K GEMMs
-__global__ void k_slab_reduce(const float* slab, size_t zstride, int chunks, size_t count, float* out) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int c = 0; c < chunks; ++c) s += slab[c * zstride + i];
-    out[i] = s;
+// out[i] = sum_c slab[c][i] (deterministic): block = 64 outputs x 4 waves; wave w sums chunk quarter w
+// (8 loads in flight per lane), the quarters are added in fixed order through LDS.  grid = ceil(count/64)
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* slab, size_t zstride, int chunks, size_t count,
+                                                     float* out) {
+  __shared__ float part[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t i = (size_t)blockIdx.x * 64 + lane;
+  const int q = (chunks + 3) / 4, c0 = wave * q, c1 = min(chunks, c0 + q);
+  float s = 0.0f;
+  if (i < count) {
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(size_t)(c + u) * zstride + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; c < c1; ++c) s += slab[(size_t)c * zstride + i];
   }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && i < count) out[i] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 __global__ void k_slab_reduce_bias_relu(const float* slab, size_t zstride, int chunks, int M, int N,

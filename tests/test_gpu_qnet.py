@@ -127,12 +127,15 @@ def test_train_step_parity(B):
     print("\n".join(report))
     # Adam's first step is lr * g/|g| (m/sqrt(v) at t = 1): weights move by exactly +-lr where the gradient
     # signs agree, so the difference is bounded by 2 lr and is ~0 for almost every element
+    # components whose gradient is clearly non-zero (|g| > 0.5 rms) must take the same step
     lr = 2.5e-4
     for v in range(10):
         d = np.abs(m.get(v) - ref.get(v))
         assert d.max() <= 2 * lr * 1.001, f"weights of var {v} after Adam"
-        n_diff = int((d > 0.1 * lr).sum())
-        assert n_diff <= max(3, 0.05 * d.size), f"var {v}: {n_diff} of {d.size} steps differ"
+        gr = np.abs(grads_r[v])
+        big = gr > 0.5 * np.sqrt(np.mean(gr.astype(np.float64) ** 2))
+        n_diff = int((d[big] > 0.1 * lr).sum())
+        assert n_diff <= max(2, 0.01 * big.sum()), f"var {v}: {n_diff} of {big.sum()} large-gradient steps differ"
     assert m.iterations() == 1
 
 
