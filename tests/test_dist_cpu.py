@@ -1,0 +1,87 @@
+"""Data-parallel semantics on CPU (gloo, world_size 2, 127.0.0.1).
+
+The product's multi-GPU path (learner.hip) shards envs per rank and all-reduces (sums) the per-rank
+gradients over RCCL, then clip_by_norm + Adam use sum / world.  With equal per-rank batches that is the
+gradient of the Huber *mean over the union batch*, i.e. exactly the single-process train step on the
+concatenated batch.  These tests check that identity with the fp32 oracle in two gloo processes, and
+exercise bench.py's control plane (barrier, max-reduce, unique-id broadcast).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _batch(rank, B):
+    rng = np.random.default_rng(100 + rank)
+    x = np.zeros((B, 84, 84, 4), np.uint8)
+    for b in range(B):
+        for _ in range(5):
+            i, j = rng.integers(0, 80, 2)
+            x[b, i:i + 4, j:j + 4, rng.integers(0, 4)] = rng.choice([96, 236, 255])
+    a = rng.integers(0, 3, B).astype(np.uint8)
+    y = rng.normal(0, 2, B).astype(np.float32)
+    return x, a, y
+
+
+def _worker(rank, world, port, B, out_path):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    net = O.QNet(seed=21)
+    x, a, y = _batch(rank, B)
+    _, grads, _ = net.train(x, a, y)          # local gradients (train also applies Adam locally; unused)
+    flat = torch.from_numpy(np.concatenate([g.ravel() for g in grads]).astype(np.float64))
+    dist.all_reduce(flat)                     # RCCL sum in the product
+    mean = (flat / world).numpy()
+    # control plane used by bench.py
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    obj = [bytes(range(128)) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    dist.barrier()
+    if rank == 0:
+        np.savez(out_path, mean=mean, tmax=t.item(), uid=np.frombuffer(obj[0], np.uint8))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp_allreduce_mean_equals_union_batch_gradient(tmp_path):
+    import oracle as O
+    world, B = 2, 4
+    out = str(tmp_path / "dp.npz")
+    mp.spawn(_worker, args=(world, _free_port(), B, out), nprocs=world, join=True)
+    r = np.load(out)
+    assert r["tmax"] == world
+    assert np.array_equal(r["uid"], np.arange(128, dtype=np.uint8))
+    # single process on the union batch
+    xs, as_, ys = zip(*[_batch(k, B) for k in range(world)])
+    net = O.QNet(seed=21)
+    _, grads, _ = net.train(np.concatenate(xs), np.concatenate(as_), np.concatenate(ys))
+    ref = np.concatenate([g.ravel() for g in grads]).astype(np.float64)
+    assert np.abs(r["mean"] - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_bench_control_single_process():
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.pop("WORLD_SIZE", None)
+    c = bench.Control()
+    assert c.world == 1 and c.max(3.5) == 3.5 and c.bcast_bytes(b"x") == b"x"
+    c.barrier()
