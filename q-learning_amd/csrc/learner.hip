@@ -170,35 +170,46 @@ struct qlx_learner {
 
 namespace qlx {
 
+// Targets of all U updates of one vector step in one pass: the target weights are fixed while the step's
+// updates run (a target sync happens only between vector steps) and all U batches were sampled up front
+// from the same replay state, so y = r + gamma * max_a Q_target(s') (or r if done) for the U*B sampled
+// transitions is one batched forward - the same values as U separate passes.
+static void learner_targets(qlx_learner* L, uint32_t U) {
+  hipStream_t s = L->stream;
+  const uint32_t n = U * L->B;
+  const ReplayView rv = replay_view(L->rb);
+  {
+    ProfScope ps(&L->prof, "gather", s);
+    hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, s, rv, L->d_idx, n, L->d_tab_s, L->d_tab_sn, L->d_bact,
+                       L->d_brew, L->d_bdone);
+  }
+  qlx_model* tg = L->target;
+  model_workspace(tg, (int)n);
+  model_forward_trunk(tg, L->d_tab_sn, (int)n, s, false);
+  Fc2Args ta = fc2_args(tg, (int)n);
+  ta.rewards = L->d_brew;
+  ta.dones = L->d_bdone;
+  ta.gamma = L->p.gamma;
+  ta.y_out = L->d_targets;
+  launch_fc2(2, ta, (int)n, s);
+}
+
 static void learner_update(qlx_learner* L, uint32_t u_local) {
   hipStream_t s = L->stream;
   const uint32_t B = L->B;
   qlx_model* on = L->online;
-  qlx_model* tg = L->target;
-  const ReplayView rv = replay_view(L->rb);
-  {
-    ProfScope ps(&L->prof, "gather", s);
-    hipLaunchKernelGGL(k_gather, dim3((B + 255) / 256), dim3(256), 0, s, rv, L->d_idx + (size_t)u_local * B, B, L->d_tab_s,
-                       L->d_tab_sn, L->d_bact, L->d_brew, L->d_bdone);
-  }
-  // target: y = r + gamma * max_a Q_target(s')  (or r if done)
-  model_forward_trunk(tg, L->d_tab_sn, (int)B, s);
-  Fc2Args ta = fc2_args(tg, (int)B);
-  ta.rewards = L->d_brew;
-  ta.dones = L->d_bdone;
-  ta.gamma = L->p.gamma;
-  ta.y_out = L->d_targets + (size_t)u_local * B;
-  launch_fc2(2, ta, (int)B, s);
+  const uint8_t* const* tab_s = L->d_tab_s + (size_t)u_local * B * 4;
+  const uint8_t* bact = L->d_bact + (size_t)u_local * B;
   // online: forward, Huber, backward
-  model_forward_trunk(on, L->d_tab_s, (int)B, s);
+  model_forward_trunk(on, tab_s, (int)B, s);
   Fc2Args oa = fc2_args(on, (int)B);
-  oa.actions = L->d_bact;
+  oa.actions = bact;
   oa.y = L->d_targets + (size_t)u_local * B;
   oa.gsample = on->w.gs;
   oa.hsample = on->w.hs;
   launch_fc2(3, oa, (int)B, s);
   launch_loss_sum(on->w.hs, (int)B, L->d_losses + u_local, s);
-  model_backward(on, L->d_tab_s, (int)B, L->d_bact, s);
+  model_backward(on, tab_s, (int)B, bact, s);
   float scale = 1.0f;
   if (L->comm) {
     ProfScope ps(&L->prof, "allreduce", s);
@@ -219,7 +230,7 @@ static void learner_vector_step(qlx_learner* L) {
   const bool any_greedy = step_before + N >= L->p.epsilon_pure_random_steps;
   if (any_greedy) {
     ProfScope ps(&L->prof, "act_forward", s);
-    model_forward_trunk(L->online, L->d_obs_table, (int)N, s);
+    model_forward_trunk(L->online, L->d_obs_table, (int)N, s, false);
     Fc2Args a = fc2_args(L->online, (int)N);
     launch_fc2(0, a, (int)N, s);
   }
@@ -257,6 +268,7 @@ static void learner_vector_step(qlx_learner* L) {
       ProfScope ps(&L->prof, "sample", s);
       replay_launch_sample(L->rb, s, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank, L->B, L->d_idx);
     }
+    learner_targets(L, U);
     for (uint32_t u = 0; u < U; ++u) learner_update(L, u);
     L->last_updates = U;
   }
@@ -353,11 +365,12 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
     QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * sizeof(float)));
     QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
     QLX_HIP(hipMalloc(&L->d_idx, (size_t)L->max_updates * B * sizeof(uint64_t)));
-    QLX_HIP(hipMalloc(&L->d_tab_s, (size_t)B * 4 * sizeof(void*)));
-    QLX_HIP(hipMalloc(&L->d_tab_sn, (size_t)B * 4 * sizeof(void*)));
-    QLX_HIP(hipMalloc(&L->d_bact, B));
-    QLX_HIP(hipMalloc(&L->d_brew, B * sizeof(float)));
-    QLX_HIP(hipMalloc(&L->d_bdone, B));
+    const size_t UB = (size_t)L->max_updates * B;   // all batches of one vector step
+    QLX_HIP(hipMalloc(&L->d_tab_s, UB * 4 * sizeof(void*)));
+    QLX_HIP(hipMalloc(&L->d_tab_sn, UB * 4 * sizeof(void*)));
+    QLX_HIP(hipMalloc(&L->d_bact, UB));
+    QLX_HIP(hipMalloc(&L->d_brew, UB * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_bdone, UB));
     QLX_HIP(hipMalloc(&L->d_losses, L->max_updates * sizeof(float)));
     QLX_HIP(hipMalloc(&L->d_targets, (size_t)L->max_updates * B * sizeof(float)));
     QLX_HIP(hipMemsetAsync(L->d_ep_reward, 0, N * sizeof(float), L->stream));
@@ -368,7 +381,7 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
     hipLaunchKernelGGL(k_obs_table, dim3((N * 4 + 255) / 256), dim3(256), 0, L->stream, L->env->d_obs, N, L->d_obs_table);
     QLX_HIP(hipGetLastError());
     model_workspace(L->online, (int)std::max(N, B));
-    model_workspace(L->target, (int)B);
+    model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
     QLX_HIP(hipStreamSynchronize(L->stream));
     *out = L;
   });

@@ -12,8 +12,8 @@ namespace qlx {
 constexpr int kNumVars = 10;
 constexpr int64_t kNumParams = 1685667;   // sum of the 10 Keras variables (variables.index shapes)
 constexpr int kFc1Split = 7;              // split-K of the 3136-deep dense layer (14 MFMA k-steps each)
-constexpr size_t kWgradSlabFloats = 64 * 576 * 64;   // max chunks x KIN x N over the conv layers
-constexpr size_t kBiasSlabFloats = 128 * 64;
+constexpr size_t kWgradSlabFloats = (size_t)256 * 576 * 64;   // >= max chunks x KIN x N over the conv layers
+constexpr size_t kBiasSlabFloats = 256 * 512;
 extern const int kVarSize[kNumVars];
 
 struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
@@ -79,7 +79,8 @@ void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s);
 void launch_loss_sum(const float* h, int B, float* out, hipStream_t s);
 void model_workspace(qlx_model* m, int B);
 void model_pack(qlx_model* m);
-void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
+// store_acts = false skips writing a1/a2 (only a3 is needed when no backward pass follows)
+void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts = true);
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, hipStream_t s);
 void model_norms(qlx_model* m, hipStream_t s, float scale);
 void model_adam(qlx_model* m, hipStream_t s, float scale);

@@ -16,6 +16,8 @@
 #include "objects.h"
 #include "qnet.h"
 #include "qnet_kernels.h"
+#include "trunk_kernels.h"
+#include "gemm_kernels.h"
 #include "profiler.h"
 
 namespace qlx {
@@ -367,32 +369,54 @@ static void launch_igemm2(LoadA la, const bf16* Bt, int M, int N, Epi epi, hipSt
 }
 
 // forward through fc1 (a1..a4 in the workspace); `table` = [B][4] frame pointers
-void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+// one block per CU (LDS-limited), persistent over samples
+static int trunk_grid(int B) { return std::max(1, std::min(B, 256)); }
+
+template <class Kern>
+static void set_lds_attr(Kern k, size_t bytes) {
+  QLX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+template <bool TN, class Epi>
+static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K, int splits, Epi epi, hipStream_t s,
+                        int ones_m = -1) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds_attr(k_gemm<TN, Epi>, GemmCfg<TN>::LDS);
+    attr = true;
+  }
+  const int kps = (K + splits - 1) / splits;
+  QLX_CHECK(TN || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID, "k_gemm NT needs K and K/splits multiples of 64");
+  const dim3 grid((M + 127) / 128, (N + 127) / 128, splits);
+  hipLaunchKernelGGL((k_gemm<TN, Epi>), grid, dim3(256), GemmCfg<TN>::LDS, s, A, lda, Bm, ldb, M, N, K, kps, ones_m, epi);
+}
+
+void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts) {
   ModelWs& w = m->w;
   m->last_batch = B;
   const float* p = m->d_params;
-  {  // conv1: M = B*400, N = 32, K = 256
-    ProfScope ps(m->prof, "conv1_fwd", s, 2.0 * B * 400 * 32 * 256);
-    launch_igemm2<32, 2, 256>(LoadConv1{table, B * 400}, m->wf0, B * 400, 32, EpiBiasRelu{w.a1, p + var_offset(1), 32}, s);
+  {  // conv1 -> conv2 -> conv3 fused per sample (trunk_kernels.h)
+    ProfScope ps(m->prof, "trunk_fwd", s, 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576));
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
+      set_lds_attr(k_trunk_fwd<false>, kTrunkFwdLds);
+      attr = true;
+    }
+    auto kern = store_acts ? k_trunk_fwd<true> : k_trunk_fwd<false>;
+    hipLaunchKernelGGL(kern, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkFwdLds, s, table, B, m->wf0, m->wf1, m->wf2,
+                       p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3);
   }
-  {  // conv2: M = B*81, N = 64, K = 512
-    ProfScope ps(m->prof, "conv2_fwd", s, 2.0 * B * 81 * 64 * 512);
-    launch_igemm2<64, 2, 512>(LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, m->wf1, B * 81, 64,
-                              EpiBiasRelu{w.a2, p + var_offset(3), 64}, s);
-  }
-  {  // conv3: M = B*49, N = 64, K = 576
-    ProfScope ps(m->prof, "conv3_fwd", s, 2.0 * B * 49 * 64 * 576);
-    launch_igemm2<64, 2, 576>(LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, m->wf2, B * 49, 64,
-                              EpiBiasRelu{w.a3, p + var_offset(5), 64}, s);
-  }
-  {  // fc1: M = B, N = 512, K = 3136, split-K into kFc1Split partial slabs
+  {  // fc1: M = B, N = 512, K = 3136.  Small batches split K into kFc1Split fp32 slabs (reduced with bias +
+     // ReLU in fixed order) to fill the chip; from 64 M tiles on (B >= 8192) one pass with the epilogue fused
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
-    LoadRows<3136> la{w.a3, B};
-    EpiSlab ep{w.fc1slab, 512, (size_t)B * 512};
-    hipLaunchKernelGGL((k_igemm<2, 2, 2, 2, LoadRows<3136>, EpiSlab>), dim3((B + 63) / 64, 512 / 64, kFc1Split), dim3(256), 0,
-                       s, la, m->wf3, B, 3136, 3136 / kFc1Split, ep);
-    hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, s, w.fc1slab,
-                       (size_t)B * 512, kFc1Split, B, 512, p + var_offset(7), w.a4);
+    if (B >= 64 * 128) {
+      launch_gemm<false>(w.a3, 3136, m->wf3, 3136, B, 512, 3136, 1, EpiBiasRelu{w.a4, p + var_offset(7), 512}, s);
+    } else {
+      launch_gemm<false>(w.a3, 3136, m->wf3, 3136, B, 512, 3136, kFc1Split, EpiSlab{w.fc1slab, 512, (size_t)B * 512}, s);
+      hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, s, w.fc1slab,
+                         (size_t)B * 512, kFc1Split, B, 512, p + var_offset(7), w.a4);
+    }
   }
   QLX_HIP(hipGetLastError());
 }
@@ -420,47 +444,60 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
   }
   // fc1: dW3 = a3^T dz4 (one chunk), db3; dz3 = (dz4 W3^T) * (a3 > 0)
   {
-    LoadRows<3136> lx{w.a3, B};
     ProfScope ps(m->prof, "fc1_wgrad", s, 2.0 * B * 512 * 3136);
-    hipLaunchKernelGGL((k_wgrad<64, LoadRows<3136>>), dim3(3136 / 64, 512 / 64, 1), dim3(256), 0, s, lx, w.dz4, B, 512,
-                       align_up(B, 32), G + var_offset(6), 512, (size_t)0, w.bslab);
-    hipLaunchKernelGGL(k_slab_reduce, dim3(512 / 64), dim3(256), 0, s, w.bslab, (size_t)512, 1, (size_t)512, G + var_offset(7));
+    // row 3136 of the output = the all-ones row = db3, which follows dW3 [3136][512] in the flat gradient
+    launch_gemm<true>(w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, EpiStoreF32{G + var_offset(6), 512}, s, 3136);
   }
   {
     ProfScope ps(m->prof, "fc1_dgrad", s, 2.0 * B * 512 * 3136);
-    launch_igemm2<64, 2, 512>(LoadRows<512>{w.dz4, B}, m->wb3, B, 3136, EpiReluMask{w.dz3, w.a3, 3136}, s);
+    launch_gemm<false>(w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, EpiReluMask{w.dz3, w.a3, 3136}, s);
   }
+  // conv weight gradients: k_wgrad2 over m-chunks into fp32 slabs, then the fixed-order slab reduction
   auto wgrad_conv = [&](const char* name, auto lx, const bf16* dz, int M, int KIN, int N, int target_chunks, float* gW, float* gb,
-                        auto nb_tag) {
+                        auto kwt_tag, auto nb_tag) {
     ProfScope ps(m->prof, name, s, 2.0 * M * KIN * N);
-    constexpr int NB = decltype(nb_tag)::value;
-    int m_chunk = (int)align_up((M + target_chunks - 1) / target_chunks, 32);
-    if (m_chunk < 128) m_chunk = 128;
+    constexpr int KWT = decltype(kwt_tag)::value, NB = decltype(nb_tag)::value, KT = 64 * KWT;
+    int m_chunk = (int)align_up((M + target_chunks - 1) / target_chunks, 64);
+    if (m_chunk < 256) m_chunk = 256;
     const int chunks = (M + m_chunk - 1) / m_chunk;
-    hipLaunchKernelGGL((k_wgrad<NB, decltype(lx)>), dim3(KIN / 64, N / NB, chunks), dim3(256), 0, s, lx, dz, M, N, m_chunk,
-                       w.slab, N, (size_t)KIN * N, w.bslab);
+    hipLaunchKernelGGL((k_wgrad2<KWT, NB, decltype(lx)>), dim3(KIN / KT, N / NB, chunks), dim3(256), 0, s, lx, dz, M, N,
+                       m_chunk, w.slab, N, (size_t)KIN * N, w.bslab);
     hipLaunchKernelGGL(k_slab_reduce, dim3((KIN * N + 63) / 64), dim3(256), 0, s, w.slab, (size_t)KIN * N, chunks,
                        (size_t)KIN * N, gW);
     hipLaunchKernelGGL(k_slab_reduce, dim3((N + 63) / 64), dim3(256), 0, s, w.bslab, (size_t)N, chunks, (size_t)N, gb);
   };
-  // conv3: dW2 = im2col(a2)^T dz3; dz2 = convT(dz3, W2) * (a2 > 0)
-  wgrad_conv("conv3_wgrad", LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 64, G + var_offset(4),
-             G + var_offset(5), std::integral_constant<int, 64>{});
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I64 = std::integral_constant<int, 64>;
+  // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
-    ProfScope ps(m->prof, "conv3_dgrad", s, 2.0 * B * 49 * 64 * 576);
-    launch_igemm2<64, 2, 576>(LoadConvT<9, 9, 7, 7, 64, 3, 1>{w.dz3, B * 81}, m->wb2, B * 81, 64,
-                              EpiReluMask{w.dz2, w.a2, 64}, s);
+    ProfScope ps(m->prof, "trunk_bwd_data", s, 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512));
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(k_trunk_bwd_data, kTrunkBwdLds);
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_trunk_bwd_data, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkBwdLds, s, w.dz3, w.a2, w.a1, B, m->wb2,
+                       m->wb1, w.dz2, w.dz1);
   }
-  // conv2: dW1 = im2col(a1)^T dz2; dz1 = convT(dz2, W1) * (a1 > 0)
-  wgrad_conv("conv2_wgrad", LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 64, G + var_offset(2),
-             G + var_offset(3), std::integral_constant<int, 64>{});
+  // conv3: dW2 = im2col(a2)^T dz3;  conv2: dW1 = im2col(a1)^T dz2
+  wgrad_conv("conv3_wgrad", LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 96, G + var_offset(4),
+             G + var_offset(5), I3{}, I64{});
+  wgrad_conv("conv2_wgrad", LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 128, G + var_offset(2),
+             G + var_offset(3), I4{}, I64{});
+  // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames (s2d k order -> HWIO)
   {
-    ProfScope ps(m->prof, "conv2_dgrad", s, 2.0 * B * 81 * 64 * 512);
-    launch_igemm2<32, 2, 256>(LoadConv2T{w.dz2, B * 100}, m->wb1, B * 100, 128, EpiReluMaskConv2T{w.dz1, w.a1}, s);
+    ProfScope ps(m->prof, "conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
+      attr = true;
+    }
+    const int grid = trunk_grid(B);
+    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B, w.slab, w.bslab);
+    hipLaunchKernelGGL(k_slab_reduce, dim3(8192 / 64), dim3(256), 0, s, w.slab, (size_t)8192, grid, (size_t)8192, w.g0_s2d);
+    hipLaunchKernelGGL(k_slab_reduce, dim3(1), dim3(256), 0, s, w.bslab, (size_t)32, grid, (size_t)32, G + var_offset(1));
   }
-  // conv1: dW0 = im2col_s2d(x)^T dz1 (s2d k order -> HWIO)
-  wgrad_conv("conv1_wgrad", LoadConv1{table, B * 400}, w.dz1, B * 400, 256, 32, 128, w.g0_s2d, G + var_offset(1),
-             std::integral_constant<int, 32>{});
   hipLaunchKernelGGL(k_conv1_grad_unpermute, dim3(32), dim3(256), 0, s, w.g0_s2d, G);
   QLX_HIP(hipGetLastError());
 }

@@ -367,6 +367,91 @@ __global__ __launch_bounds__(256) void k_wgrad(LoadX lx, const bf16* __restrict_
   if (do_bias && tid < NB) bias_slab[(size_t)blockIdx.z * N + n0 + tid] = bsum;
 }
 
+// Weight gradient v2: block tile KT (k) x NB (n) with KT = 4 waves x KW rows (KW = 16 * KWT); 64 m-rows
+// per LDS fill (two MFMA k-slices of 32), the global loads of fill i+1 in flight while fill i computes.
+// Row strides are padded by 16 bf16 so the 8 consecutive rows a 32-lane half reads with
+// ds_read_b64_tr_b16 land on disjoint 8-dword bank windows (same row permutation as k_wgrad).
+template <int KWT, int NB, class LoadX>
+__global__ __launch_bounds__(256) void k_wgrad2(LoadX lx, const bf16* __restrict__ dY, int M, int N, int m_chunk,
+                                                float* slab, int slab_ld, size_t slab_zstride, float* bias_slab) {
+  constexpr int KT = 4 * 16 * KWT;
+  constexpr int XS = KT + 16, YS = NB + 16;
+  constexpr int TN = NB / 16;
+  constexpr int XCH = 64 * KT / 8 / 256;        // 16-byte X chunks per thread per fill
+  constexpr int YCH = (64 * NB / 8 + 255) / 256;
+  static_assert(XCH >= 1 && (64 * KT / 8) % 256 == 0, "X tile must split evenly over 256 threads");
+  __shared__ __attribute__((aligned(16))) bf16 lds[64 * XS + 64 * YS];
+  bf16* xl = lds;
+  bf16* yl = lds + 64 * XS;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int k0 = blockIdx.x * KT, n0 = blockIdx.y * NB;
+  const int mb = blockIdx.z * m_chunk, me = min(M, mb + m_chunk);
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  f32x4 acc[KWT][TN];
+#pragma unroll
+  for (int i = 0; i < KWT; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float bsum = 0.0f;
+  const bool do_bias = bias_slab != nullptr && blockIdx.x == 0;
+  bf16x8 xv[XCH], yv[YCH];
+  auto fetch = [&](int m) {
+#pragma unroll
+    for (int c = 0; c < XCH; ++c) {
+      const int idx = tid + c * 256, row = idx / (KT / 8), col = (idx - row * (KT / 8)) * 8;
+      xv[c] = lx.load(m + row < me ? m + row : M, k0 + col);
+    }
+#pragma unroll
+    for (int c = 0; c < YCH; ++c) {
+      const int idx = tid + c * 256, row = idx / (NB / 8), col = (idx - row * (NB / 8)) * 8;
+      yv[c] = (idx < 64 * NB / 8 && m + row < me) ? ld8(dY + (size_t)(m + row) * N + n0 + col) : zero8();
+    }
+  };
+  fetch(mb);
+  for (int m = mb; m < me; m += 64) {
+    __syncthreads();   // readers of the previous fill are done
+#pragma unroll
+    for (int c = 0; c < XCH; ++c) {
+      const int idx = tid + c * 256, row = idx / (KT / 8), col = (idx - row * (KT / 8)) * 8;
+      *reinterpret_cast<uint4*>(xl + row * XS + col) = __builtin_bit_cast(uint4, xv[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < YCH; ++c) {
+      const int idx = tid + c * 256, row = idx / (NB / 8), col = (idx - row * (NB / 8)) * 8;
+      if (idx < 64 * NB / 8) *reinterpret_cast<uint4*>(yl + row * YS + col) = __builtin_bit_cast(uint4, yv[c]);
+    }
+    __syncthreads();
+    if (m + 64 < me) fetch(m + 64);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const bf16* xh = xl + half * 32 * XS;
+      const bf16* yh = yl + half * 32 * YS;
+      bf16x8 bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_pair(yh, YS, g, p, q, j * 16);
+#pragma unroll
+      for (int i = 0; i < KWT; ++i) {
+        const bf16x8 af = tr_pair(xh, XS, g, p, q, (wave * KWT + i) * 16);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (do_bias && tid < NB) {
+#pragma unroll 8
+      for (int rr = 0; rr < 64; ++rr) bsum += (float)yl[rr * YS + tid];
+    }
+  }
+  float* out = slab + blockIdx.z * slab_zstride;
+#pragma unroll
+  for (int i = 0; i < KWT; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        out[(size_t)(k0 + (wave * KWT + i) * 16 + g * 4 + e) * slab_ld + n0 + j * 16 + li] = acc[i][j][e];
+  if (do_bias && tid < NB) bias_slab[(size_t)blockIdx.z * N + n0 + tid] = bsum;
+}
+
 // out[i] = sum_c slab[c][i] (deterministic): block = 64 outputs x 4 waves; wave w sums chunk quarter w
 // (8 loads in flight per lane), the quarters are added in fixed order through LDS.  grid = ceil(count/64)
 __global__ __launch_bounds__(256) void k_slab_reduce(const float* slab, size_t zstride, int chunks, size_t count,

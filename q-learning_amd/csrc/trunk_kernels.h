@@ -1,0 +1,421 @@
+// Per-sample fused conv-trunk kernels for gfx950 (Nature-DQN conv1 -> conv2 -> conv3).
+//
+// One persistent 512-thread block (8 waves, one block per CU by LDS) walks the batch sample by sample.
+// A sample's four space-to-depth frames (4 x 7056 B) are staged ONCE into LDS as bf16 [441 pos][64 ch]
+// (ch = ring slot * 16 + 4x4 sub-pixel), so conv1's 2x2 s2d convolution reads its im2col rows straight
+// from LDS; conv1 writes A1 into LDS for conv2, conv2 writes A2 for conv3.  Activations leave the CU
+// with 16-byte coalesced stores (they are needed by the backward pass and fc1).  All conv weights stay
+// in VGPRs as MFMA B fragments for the block's lifetime: each wave owns one 16-column output slice of
+// every layer (conv1 32 + conv2 64 + conv3 72 VGPRs per lane), so the weights cross L2 once per block.
+//
+// The conv1 weight-gradient kernel reuses the staging: dW0[k][n] = sum_m X(m,k) dz1[m][n] with the
+// m-reduction in the MFMA k slot, both operands read with ds_read_b64_tr_b16 (4 rows x 16 columns per
+// 16-lane group, per-lane row addresses = the im2col gather for free).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qnet_kernels.h"
+
+namespace qlx {
+namespace qn {
+
+constexpr int kTrunkThreads = 512;
+// Row strides: 40 dwords (80 bf16) puts the 16 (row, k-group) 16-byte windows of every ds_read_b128 lane group
+// of a 16x16x32 fragment, and the 8 rows a 32-lane half reads with ds_read_b64_tr_b16, in distinct banks.
+constexpr int kXS = 80;                  // staged input row stride (bf16): 64 channels + 16 pad
+constexpr int kA1S = 40;                 // A1 [400][32] row stride
+constexpr int kA2S = 80;                 // A2 [81][64]
+constexpr int kA3S = 80;                 // A3 [49][64]
+constexpr int kDZS = 48;                 // dz1 [416][32] row stride (tr-read conflict-free, see k_wgrad)
+constexpr int kLdsX = 441 * kXS;         // bf16 elements
+constexpr int kLdsA1 = 400 * kA1S;
+constexpr int kLdsDZ = 416 * kDZS;
+constexpr size_t kTrunkFwdLds = (size_t)(kLdsX + kLdsA1) * 2;   // A2, A3 alias X (dead after conv1)
+constexpr size_t kConv1WgradLds = (size_t)(kLdsX + kLdsDZ) * 2;
+constexpr int kFrameChunks = 4 * 441;    // 16-byte s2d blocks per sample
+constexpr int kPf = (kFrameChunks + kTrunkThreads - 1) / kTrunkThreads;
+
+// 16 u8 -> 16 bf16 (exact) as two 16-byte halves
+__device__ __forceinline__ void u8x16_to_bf16(uint4 v, uint4& lo, uint4& hi) {
+  lo.x = u8pair_bf16(v.x, 0);
+  lo.y = u8pair_bf16(v.x, 16);
+  lo.z = u8pair_bf16(v.y, 0);
+  lo.w = u8pair_bf16(v.y, 16);
+  hi.x = u8pair_bf16(v.z, 0);
+  hi.y = u8pair_bf16(v.z, 16);
+  hi.z = u8pair_bf16(v.w, 0);
+  hi.w = u8pair_bf16(v.w, 16);
+}
+
+// register prefetch of one sample's frames: chunk c = slot * 441 + pos (nullptr frame = zeros)
+__device__ __forceinline__ void frames_prefetch(const uint8_t* const* table, int b, int B, uint4 (&pf)[kPf]) {
+#pragma unroll
+  for (int u = 0; u < kPf; ++u) {
+    const int c = threadIdx.x + u * kTrunkThreads;
+    pf[u] = uint4{0, 0, 0, 0};
+    if (b < B && c < kFrameChunks) {
+      const int slot = c / 441, pos = c - slot * 441;
+      const uint8_t* f = table[b * 4 + slot];
+      if (f) pf[u] = *reinterpret_cast<const uint4*>(f + pos * 16);
+    }
+  }
+}
+
+__device__ __forceinline__ void frames_stage(bf16* X, const uint4 (&pf)[kPf]) {
+#pragma unroll
+  for (int u = 0; u < kPf; ++u) {
+    const int c = threadIdx.x + u * kTrunkThreads;
+    if (c < kFrameChunks) {
+      const int slot = c / 441, pos = c - slot * 441;
+      uint4 lo, hi;
+      u8x16_to_bf16(pf[u], lo, hi);
+      uint4* d = reinterpret_cast<uint4*>(X + pos * kXS + slot * 16);
+      d[0] = lo;
+      d[1] = hi;
+    }
+  }
+}
+
+// LDS rows [rows][stride] -> global contiguous [rows][cols] with 16-byte chunks
+template <int ROWS, int COLS, int STRIDE>
+__device__ __forceinline__ void lds_copy_out(const bf16* src, bf16* dst) {
+  constexpr int CPR = COLS / 8;
+  for (int c = threadIdx.x; c < ROWS * CPR; c += kTrunkThreads) {
+    const int row = c / CPR, col = (c - row * CPR) * 8;
+    *reinterpret_cast<uint4*>(dst + row * COLS + col) = *reinterpret_cast<const uint4*>(src + row * STRIDE + col);
+  }
+}
+
+__device__ __forceinline__ bf16x8 lds8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ bf16 relu_bf16(float v) { return (bf16)(v > 0.0f ? v : 0.0f); }
+
+// One wave's share of a per-sample conv GEMM in the D^T = W X^T orientation: the lane's weight registers
+// w[s] (row = output channel lane & 15 of the wave's 16-channel slice, k = 8 (lane >> 4) + j) are the A
+// operand, the activation rows (column = output position lane & 15) the B operand, so each lane ends with
+// 4 consecutive channels 4 (lane >> 4) + e of one position: one 8-byte LDS store per tile.  The B-fragment
+// LDS reads run D deep ahead of their MFMAs across tile boundaries (ring slot s % D), so a tile's epilogue
+// overlaps the next tile's reads.  addr(t, s) -> LDS pointer of k-step s of tile t for this lane.
+template <int KS, int D, class Addr, class Epi>
+__device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 (&w)[KS], Addr addr, Epi epi) {
+  static_assert(KS % D == 0, "ring depth must divide the k-steps");
+  if (t0 >= nt) return;
+  bf16x8 a[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) a[d] = lds8(addr(t0, d));
+  for (int t = t0; t < nt; t += dt) {
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const bool more = t + dt < nt;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[s], a[s % D], acc, 0, 0, 0);
+      if (s + D < KS) a[s % D] = lds8(addr(t, s + D));
+      else if (more) a[s % D] = lds8(addr(t + dt, s + D - KS));
+    }
+    epi(t, acc);
+  }
+}
+
+__device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
+
+// a1 [B][400][32], a2 [B][81][64] (written when STORE12), a3 [B][49][64] (always)
+template <bool STORE12>
+__global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* const* __restrict__ table, int B,
+                                                                const bf16* __restrict__ wf0, const bf16* __restrict__ wf1,
+                                                                const bf16* __restrict__ wf2, const float* __restrict__ bias0,
+                                                                const float* __restrict__ bias1,
+                                                                const float* __restrict__ bias2, bf16* __restrict__ a1,
+                                                                bf16* __restrict__ a2, bf16* __restrict__ a3) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* X = lds;
+  bf16* A1 = lds + kLdsX;
+  bf16* A2 = lds;               // aliases X
+  bf16* A3 = lds + 81 * kA2S;   // aliases X, after A2
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int c1 = (wave & 1) * 16, c2 = (wave & 3) * 16;   // the wave's output-channel slice, conv1 / conv2+3
+  bf16x8 w1[8], w2[16], w3[18];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) w1[s] = ld8(wf0 + (c1 + r) * 256 + 32 * s + 8 * g);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) w2[s] = ld8(wf1 + (c2 + r) * 512 + 32 * s + 8 * g);
+#pragma unroll
+  for (int s = 0; s < 18; ++s) w3[s] = ld8(wf2 + (c2 + r) * 576 + 32 * s + 8 * g);
+  // biases are re-read (L1 hits) in the epilogues: 12 resident VGPRs would spill the weight fragments
+  auto bias_relu4 = [](const float* bias, f32x4 acc) {
+    const float4 bv = *reinterpret_cast<const float4*>(bias);
+    return pack4_bf16(relu(acc[0] + bv.x), relu(acc[1] + bv.y), relu(acc[2] + bv.z), relu(acc[3] + bv.w));
+  };
+  uint4 pf[kPf];
+  frames_prefetch(table, blockIdx.x, B, pf);
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    __syncthreads();   // previous sample's A2/A3 copy-out is done
+    frames_stage(X, pf);
+    __syncthreads();
+    frames_prefetch(table, b + gridDim.x, B, pf);
+    // conv1: M = 400 (25 tiles of 16), N = 32, K = 256: k-step s covers tap (i, j) = (s >> 2, (s >> 1) & 1)
+    conv_tiles<8, 4>(
+        wave >> 1, 4, 25, w1,
+        [&](int t, int s) {
+          const int m = t * 16 + r, ox = m / 20, oy = m - ox * 20;
+          return X + ((ox + (s >> 2)) * 21 + oy + ((s >> 1) & 1)) * kXS + 32 * (s & 1) + 8 * g;
+        },
+        [&](int t, f32x4 acc) {
+          *reinterpret_cast<uint2*>(A1 + (t * 16 + r) * kA1S + c1 + 4 * g) = bias_relu4(bias0 + c1 + 4 * g, acc);
+        });
+    __syncthreads();
+    if (STORE12) lds_copy_out<400, 32, kA1S>(A1, a1 + (size_t)b * 12800);
+    // conv2: 4x4 stride 2 over A1 [20][20][32]; M = 81 (6 tiles), k-step s = tap (kh, kw) = (s >> 2, s & 3)
+    conv_tiles<16, 4>(
+        wave >> 2, 2, 6, w2,
+        [&](int t, int s) {
+          const int m = min(t * 16 + r, 80), p = m / 9, q = m - p * 9;
+          return A1 + ((2 * p + (s >> 2)) * 20 + 2 * q + (s & 3)) * kA1S + 8 * g;
+        },
+        [&](int t, f32x4 acc) {
+          const int m = t * 16 + r;
+          if (m < 81)
+            *reinterpret_cast<uint2*>(A2 + m * kA2S + c2 + 4 * g) = bias_relu4(bias1 + c2 + 4 * g, acc);
+        });
+    __syncthreads();
+    if (STORE12) lds_copy_out<81, 64, kA2S>(A2, a2 + (size_t)b * 5184);
+    // conv3: 3x3 stride 1 over A2 [9][9][64]; M = 49 (4 tiles), k-step s: tap s >> 1, channel half s & 1
+    conv_tiles<18, 3>(
+        wave >> 2, 2, 4, w3,
+        [&](int t, int s) {
+          const int m = min(t * 16 + r, 48), p = m / 7, q = m - p * 7;
+          const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
+          return A2 + ((p + kh) * 9 + q + kw) * kA2S + 32 * (s & 1) + 8 * g;
+        },
+        [&](int t, f32x4 acc) {
+          const int m = t * 16 + r;
+          if (m < 49)
+            *reinterpret_cast<uint2*>(A3 + m * kA3S + c2 + 4 * g) = bias_relu4(bias2 + c2 + 4 * g, acc);
+        });
+    __syncthreads();
+    lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)b * 3136);
+  }
+}
+
+// conv1 weight gradient: per block fp32 partial dW[256 (s2d k)][32] into slab[blockIdx.x] and the bias
+// partial db[32] into bias_slab[blockIdx.x]; reduced over blocks in fixed order by k_slab_reduce.
+// Wave w owns k tiles 2w, 2w+1 (one s2d tap (i, j) = ((w >> 1) >> 1, (w >> 1) & 1), 32 channels) x both
+// 16-column n tiles.  m-steps of 32 im2col rows (13 per sample, rows 400..415 have dz = 0).
+__global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t* const* __restrict__ table,
+                                                                  const bf16* __restrict__ dz1, int B, float* slab,
+                                                                  float* bias_slab) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* X = lds;
+  bf16* DZ = lds + kLdsX;
+  __shared__ float bred[16][32];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int ij = wave >> 1, ti = ij >> 1, tj = ij & 1;
+  const int col0 = (wave & 1) * 32 + 4 * p;   // channel of this lane's first k tile (second: +16)
+  for (int i = tid; i < 16 * kDZS / 8; i += kTrunkThreads)
+    *reinterpret_cast<uint4*>(DZ + 400 * kDZS + i * 8) = uint4{0, 0, 0, 0};
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float bsum = 0.0f;
+  const int bn = tid & 31, brg = tid >> 5;   // bias: column bn, rows brg + 16 i
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto tr = [](const bf16* pp) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pp)); };
+  uint4 pf[kPf];
+  frames_prefetch(table, blockIdx.x, B, pf);
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    // dz1 sample block [400][32] -> registers (1600 chunks)
+    uint4 dv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      dv[u] = c < 1600 ? *reinterpret_cast<const uint4*>(dz1 + (size_t)b * 12800 + c * 8) : uint4{0, 0, 0, 0};
+    }
+    __syncthreads();   // previous sample's readers are done
+    frames_stage(X, pf);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      if (c < 1600) *reinterpret_cast<uint4*>(DZ + (c >> 2) * kDZS + (c & 3) * 8) = dv[u];
+    }
+    __syncthreads();
+    frames_prefetch(table, b + gridDim.x, B, pf);
+    for (int ms = 0; ms < 13; ++ms) {
+      const int m0 = ms * 32;
+      // rows of this lane's tr reads: m0 + 4g + q and m0 + 16 + 4g + q
+      int mA = min(m0 + 4 * g + q, 399), mB = min(m0 + 16 + 4 * g + q, 399);
+      const int oxA = mA / 20, oyA = mA - oxA * 20, oxB = mB / 20, oyB = mB - oxB * 20;
+      const bf16* xa = X + ((oxA + ti) * 21 + oyA + tj) * kXS + col0;
+      const bf16* xb = X + ((oxB + ti) * 21 + oyB + tj) * kXS + col0;
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      bf16x8 af[2], bf[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const s16x4 v0 = tr(xa + 16 * a), v1 = tr(xb + 16 * a);
+        af[a] = __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const s16x4 v0 = tr(DZ + (m0 + 4 * g + q) * kDZS + c * 16 + 4 * p);
+        const s16x4 v1 = tr(DZ + (m0 + 16 + 4 * g + q) * kDZS + c * 16 + 4 * p);
+        bf[c] = __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf[c], acc[a][c], 0, 0, 0);
+    }
+    for (int m = brg; m < 400; m += 16) bsum += (float)DZ[m * kDZS + bn];
+  }
+  // D tile (a, c): row k = ij * 64 + (wave & 1) * 32 + a * 16 + 4g + e, col n = c * 16 + li
+  float* out = slab + (size_t)blockIdx.x * 8192;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(ij * 64 + (wave & 1) * 32 + a * 16 + 4 * g + e) * 32 + c * 16 + li] = acc[a][c][e];
+  bred[brg][bn] = bsum;
+  __syncthreads();
+  if (tid < 32) {
+    float s = 0.0f;
+    for (int i = 0; i < 16; ++i) s += bred[i][tid];
+    bias_slab[blockIdx.x * 32 + tid] = s;
+  }
+}
+
+// Backward data through conv3 and conv2, fused per sample:
+//   dz2 = convT(dz3, W2) * (a2 > 0)        M = 81 rows (ih, iw), N = 64, K = 576 = (kh*3+kw)*64 + oc
+//   dz1 = convT(dz2, W1) * (a1 > 0)        by output parity class p = (ih & 1, iw & 1): rows (i, j) of
+//                                          10 x 10, N = 128 = p*32 + c, K = 256 = (th*2+tw)*64 + oc
+// dz3 is staged into a zero-bordered [11][11] LDS image (interior at +2) and dz2 into another (interior
+// at +1), so every transposed-conv gather is an unconditional 16-byte LDS read.  W2^T (72 VGPRs) and the
+// parity-packed W1^T (32 VGPRs) are this lane's B fragments for the block's lifetime.
+constexpr int kPadS = 80;                  // padded image row stride (bf16)
+constexpr int kLdsPad = 121 * kPadS;       // [11][11][64 (+8)]
+constexpr int kLdsA2M = 81 * 72;           // staged a2 (ReLU mask of dz2), row stride 72
+constexpr size_t kTrunkBwdLds = (size_t)(2 * kLdsPad + kLdsA2M + kLdsA1) * 2;
+
+__global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16* __restrict__ dz3, const bf16* __restrict__ a2,
+                                                                     const bf16* __restrict__ a1, int B,
+                                                                     const bf16* __restrict__ wb2, const bf16* __restrict__ wb1,
+                                                                     bf16* __restrict__ dz2, bf16* __restrict__ dz1) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* P3 = lds;                   // dz3, interior (oh + 2, ow + 2)
+  bf16* P2 = lds + kLdsPad;         // dz2 (masked), interior (oh + 1, ow + 1)
+  bf16* M2 = lds + 2 * kLdsPad;     // a2
+  bf16* D1 = M2 + kLdsA2M;          // dz1 parity rows before masking: [400][32] in natural (ih, iw) order
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 15, g = lane >> 4;
+  for (int i = tid; i < 2 * kLdsPad / 8; i += kTrunkThreads) *reinterpret_cast<uint4*>(lds + i * 8) = uint4{0, 0, 0, 0};
+  const int n3 = (wave & 3) * 16 + r;   // phase A: output channel c of dz2
+  const int n2 = wave * 16 + r;         // phase B: p*32 + c
+  bf16x8 w3[18], w2[8];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) w3[s] = ld8(wb2 + n3 * 576 + 32 * s + 8 * g);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) w2[s] = ld8(wb1 + n2 * 256 + 32 * s + 8 * g);
+  // prefetch: dz3 392 chunks + a2 648 chunks = 1040 -> 3 per thread
+  constexpr int kC3 = 392, kCA = 648, kCT = kC3 + kCA, kPB = (kCT + kTrunkThreads - 1) / kTrunkThreads;
+  uint4 pf[kPB];
+  auto prefetch = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < kPB; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      pf[u] = uint4{0, 0, 0, 0};
+      if (b < B && c < kCT)
+        pf[u] = c < kC3 ? *reinterpret_cast<const uint4*>(dz3 + (size_t)b * 3136 + c * 8)
+                        : *reinterpret_cast<const uint4*>(a2 + (size_t)b * 5184 + (c - kC3) * 8);
+    }
+  };
+  prefetch(blockIdx.x);
+  __syncthreads();   // borders zeroed
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    __syncthreads();   // previous sample's readers are done
+#pragma unroll
+    for (int u = 0; u < kPB; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      if (c < kC3) {
+        const int row = c >> 3, col = (c & 7) * 8, oh = row / 7, ow = row - oh * 7;
+        *reinterpret_cast<uint4*>(P3 + ((oh + 2) * 11 + ow + 2) * kPadS + col) = pf[u];
+      } else if (c < kCT) {
+        const int cc = c - kC3, row = cc >> 3, col = (cc & 7) * 8;
+        *reinterpret_cast<uint4*>(M2 + row * 72 + col) = pf[u];
+      }
+    }
+    __syncthreads();
+    prefetch(b + gridDim.x);
+    // phase A: dz2
+    for (int t = wave >> 2; t < 6; t += 2) {
+      const int m = min(t * 16 + r, 80), ih = m / 9, iw = m - ih * 9;
+      const bf16* ar = P3 + ((ih + 2) * 11 + iw + 2) * kPadS + 8 * g;
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < 18; ++s) {
+        const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(ar - (kh * 11 + kw) * kPadS + 32 * (s & 1)), w3[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int mm = t * 16 + 4 * g + e;
+        if (mm < 81) {
+          const int oh = mm / 9, ow = mm - oh * 9;
+          const float v = (float)M2[mm * 72 + n3] > 0.0f ? acc[e] : 0.0f;
+          P2[((oh + 1) * 11 + ow + 1) * kPadS + n3] = (bf16)v;
+        }
+      }
+    }
+    __syncthreads();
+    // dz2 -> global (81 x 64)
+    for (int c = tid; c < 648; c += kTrunkThreads) {
+      const int row = c >> 3, col = (c & 7) * 8, oh = row / 9, ow = row - oh * 9;
+      *reinterpret_cast<uint4*>(dz2 + (size_t)b * 5184 + row * 64 + col) =
+          *reinterpret_cast<const uint4*>(P2 + ((oh + 1) * 11 + ow + 1) * kPadS + col);
+    }
+    // phase B: dz1 parity classes; wave = n tile (p = wave >> 1, c = (wave & 1) * 16 + r)
+    {
+      const int p = wave >> 1, ph = p >> 1, pw = p & 1, c = (wave & 1) * 16 + r;
+      for (int t = 0; t < 7; ++t) {
+        const int m = min(t * 16 + r, 99), i = m / 10, j = m - i * 10;
+        const bf16* ar = P2 + ((i + 1) * 11 + j + 1) * kPadS + 8 * g;
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int tp = s >> 1, th = tp >> 1, tw = tp & 1;
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(ar - (th * 11 + tw) * kPadS + 32 * (s & 1)), w2[s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int mm = t * 16 + 4 * g + e;
+          if (mm < 100) {
+            const int ii = mm / 10, jj = mm - ii * 10;
+            D1[((2 * ii + ph) * 20 + 2 * jj + pw) * kA1S + c] = (bf16)acc[e];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // dz1 = D1 * (a1 > 0) -> global, coalesced
+    for (int c = tid; c < 1600; c += kTrunkThreads) {
+      const int row = c >> 2, col = (c & 3) * 8;
+      const bf16x8 act = ld8(a1 + (size_t)b * 12800 + row * 32 + col);
+      bf16x8 v = lds8(D1 + row * kA1S + col);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (float)act[e] > 0.0f ? v[e] : (bf16)0.0f;
+      *reinterpret_cast<bf16x8*>(dz1 + (size_t)b * 12800 + row * 32 + col) = v;
+    }
+  }
+}
+
+}  // namespace qn
+}  // namespace qlx

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Hardware-counter passes (one counter group per rocprofv3 run; no trace domains with --pmc) over a short
+# bench run, restricted to the update-path kernels.  Output: gpurun_out/pmc/<pass>/*_counter_collection.csv
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out/pmc
+RE="${QLX_PMC_REGEX:-k_trunk|k_conv1_wgrad|k_igemm|k_wgrad|k_adam|k_slab}"
+ARGS="--steps 2 --warmup 12 --cpu-sample 0 --profile-steps 1"
+run() {
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --kernel-include-regex "$RE" --pmc "$@" --output-format csv -d gpurun_out/pmc/$name -o c -- \
+    python3 bench.py $ARGS > gpurun_out/pmc/$name.json 2> gpurun_out/pmc/$name.err
+}
+run sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE || exit 1
+run mix SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE || exit 1
+run fetch FETCH_SIZE || exit 1
+run write WRITE_SIZE || exit 1
+exit 0

@@ -64,7 +64,7 @@ def test_init_weights_bit_identical():
         assert not m.get(v, 1).any() and not m.get(v, 2).any()
 
 
-@pytest.mark.parametrize("B,kind", [(1, "env"), (32, "rand"), (100, "sparse"), (256, "env")])
+@pytest.mark.parametrize("B,kind", [(1, "env"), (32, "rand"), (100, "sparse"), (256, "env"), (520, "sparse")])
 def test_forward_parity(B, kind):
     m = _qlx().DeepQLearningModel(seed=2)
     ref = O.QNet(seed=2)
@@ -94,7 +94,7 @@ def test_batch_max_q_and_predict_action():
     assert a in (0, 1, 2)
 
 
-@pytest.mark.parametrize("B", [32, 256])
+@pytest.mark.parametrize("B", [32, 256, 320])
 def test_train_step_parity(B):
     m = _qlx().DeepQLearningModel(seed=7)
     ref = O.QNet(seed=7)
