@@ -1,15 +1,21 @@
 // LDS-tiled bf16 GEMM for the dense layer fc1 (3136 <-> 512) on gfx950.
 //
 //   C[m][n] = sum_k A(m, k) B(n, k), fp32 accumulation with v_mfma_f32_32x32x16_bf16.
-//   NT (TN = false): A stored [M][lda] and B stored [N][ldb], k contiguous   (fc1 forward, fc1 dgrad)
-//   TN (TN = true) : A stored [K][lda] and B stored [K][ldb], m / n contiguous (fc1 wgrad: k = batch)
+//   Operand layouts (per operand): row-major  [rows][ld], k contiguous   (AK / BK = false)
+//                                  k-major    [K][ld], rows contiguous  (AK / BK = true)
+//   fc1 forward  : A = a3 [B][3136]           B = W3 [3136][512] k-major (the Keras [in][out] layout)
+//   fc1 dgrad    : A = dz4 [B][512]           B = W3 [3136][512] row-major (n = in, k = out)
+//   fc1 wgrad    : A = a3 [B][3136] k-major   B = dz4 [B][512] k-major (k = batch)
 // Block tile 128 x 128 (4 waves as 2 x 2, each 64 x 64 = 2 x 2 MFMA tiles), K stepped by 64 through a
-// double-buffered LDS image (next step's 16-byte global loads in flight in registers during the MFMAs).
-// NT images: [128 rows][64 + 8] (the 8-bf16 pad makes the 32-row ds_read_b128 fragment reads
-// conflict-free); TN images: [64 k][128 + 32], read with ds_read_b64_tr_b16 (4 k-rows x 64 B per 32-lane
-// half land in disjoint bank windows at the 80-dword row stride).  grid = (ceil(M/128), ceil(N/128),
-// splits); blockIdx.z covers k in [z*kps, min(K, (z+1)*kps)).  NT requires K % 64 == 0.
-// TN only: ones_m >= 0 (a multiple of 8) makes A row ones_m an all-ones row, so C row ones_m = sum_k B(n, k)
+// double-buffered LDS image (the next step's 16-byte global loads are in flight in registers during the
+// MFMAs).  Row-major images [128][64 + 8] are read with ds_read_b128 (the 8-bf16 pad makes the 32-row
+// fragment reads conflict-free); k-major images [64][128 + 32] with ds_read_b64_tr_b16 (4 k-rows x 64 B
+// per 32-lane half land in disjoint bank windows at the 80-dword row stride).  Both deliver k in natural
+// order, so the layouts mix freely.  The MFMA computes C^T (B fragment as the A operand): each lane ends
+// with 4 consecutive n of one m, so epilogues move 8 (bf16) or 16 (fp32) bytes per access.
+// grid = (ceil(M/128), ceil(N/128), splits); blockIdx.z covers k in [z*kps, min(K, (z+1)*kps)).
+// Row-major operands need K % 64 == 0 and kps % 64 == 0.
+// ones_m >= 0 (a multiple of 8, k-major A only) makes A row ones_m all ones, so C row ones_m = sum_k B(n, k)
 // (the bias gradient of a dense layer rides along as one extra output row).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -21,68 +27,124 @@
 namespace qlx {
 namespace qn {
 
-template <bool TN>
 struct GemmCfg {
   static constexpr int BM = 128, BN = 128, KT = 64;
-  static constexpr int S = TN ? 128 + 32 : 64 + 8;          // image row stride (bf16)
-  static constexpr int IMG = TN ? KT * S : 128 * S;         // one operand image (bf16 elements)
-  static constexpr size_t LDS = (size_t)2 * 2 * IMG * 2;    // 2 buffers x (A, B) x bf16
-  static constexpr int CH = 128 * KT / 8 / 256;             // 16-byte chunks per thread per operand (4)
+  static constexpr int SR = KT + 8;                 // row-major image row stride (bf16)
+  static constexpr int SK = 128 + 32;               // k-major image row stride (bf16)
+  static constexpr int IMG = KT * SK;               // >= 128 * SR; one operand image (bf16 elements)
+  static constexpr size_t LDS = (size_t)2 * 2 * IMG * 2;
+  static constexpr int CH = 128 * KT / 8 / 256;     // 16-byte chunks per thread per operand (4)
 };
 
-template <bool TN, class Epi>
+template <bool KM>
+struct GemmOperand {
+  // global 16-byte chunk idx of the tile at (row0, k0) -> registers
+  __device__ __forceinline__ static uint4 load(const bf16* p, int ld, int row0, int rows, int k0, int ke, int idx, int ones) {
+    if (!KM) {
+      const int row = idx >> 3, col = (idx & 7) * 8;
+      return row0 + row < rows ? *reinterpret_cast<const uint4*>(p + (size_t)(row0 + row) * ld + k0 + col) : uint4{0, 0, 0, 0};
+    }
+    const int kr = idx >> 4, col = (idx & 15) * 8;
+    uint4 v = {0, 0, 0, 0};
+    if (k0 + kr < ke) {
+      if (row0 + col == ones) v.x = 0x3F80u;   // bf16 1.0 in element 0
+      else if (row0 + col < rows) v = *reinterpret_cast<const uint4*>(p + (size_t)(k0 + kr) * ld + row0 + col);
+    }
+    return v;
+  }
+  __device__ __forceinline__ static void store(bf16* img, int idx, uint4 v) {
+    const int row = KM ? idx >> 4 : idx >> 3, col = KM ? (idx & 15) * 8 : (idx & 7) * 8;
+    *reinterpret_cast<uint4*>(img + row * (KM ? GemmCfg::SK : GemmCfg::SR) + col) = v;
+  }
+  // MFMA fragment: 32 rows (base + lane & 31) x 16 k (k16 + 8 (lane >> 5) + j, natural order)
+  __device__ __forceinline__ static bf16x8 frag(const bf16* img, int base, int k16, int lane) {
+    const int h = lane >> 5;
+    if (!KM) return *reinterpret_cast<const bf16x8*>(img + (base + (lane & 31)) * GemmCfg::SR + k16 + 8 * h);
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const int gh = (lane >> 4) & 1, q = (lane & 15) >> 2, p = lane & 3;
+    const bf16* p0 = img + (k16 + 8 * h + q) * GemmCfg::SK + base + 16 * gh + 4 * p;
+    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * GemmCfg::SK));
+    return __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+  }
+};
+
+// Epilogues: operator()(m, n, v) for C[m][n .. n+3] = v[0..3] (n % 4 == 0, n + 3 < N when n < N)
+struct Epi4Slab {   // split-K partial: slab[z][m][n] (fp32)
+  float* slab;
+  int ldo;
+  size_t zstride;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+    *reinterpret_cast<f32x4*>(slab + blockIdx.z * zstride + (size_t)m * ldo + n) = v;
+  }
+};
+
+struct Epi4StoreF32 {   // out[m][n] = v (fp32)
+  float* out;
+  int ldo;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+    *reinterpret_cast<f32x4*>(out + (size_t)m * ldo + n) = v;
+  }
+};
+
+__device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+  typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+  const bf16x4v v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  return __builtin_bit_cast(uint2, v);
+}
+
+struct Epi4BiasRelu {   // out[m][n] = relu(v + bias[n]) as bf16
+  bf16* out;
+  const float* bias;
+  int ldo;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+    const float4 b = *reinterpret_cast<const float4*>(bias + n);
+    auto r = [](float x) { return x > 0.0f ? x : 0.0f; };
+    *reinterpret_cast<uint2*>(out + (size_t)m * ldo + n) = pack4(r(v[0] + b.x), r(v[1] + b.y), r(v[2] + b.z), r(v[3] + b.w));
+  }
+};
+
+struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16
+  bf16* out;
+  const bf16* act;
+  int ldo;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+    const size_t i = (size_t)m * ldo + n;
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    const bf16x4v a = *reinterpret_cast<const bf16x4v*>(act + i);
+    *reinterpret_cast<uint2*>(out + i) = pack4((float)a[0] > 0.0f ? v[0] : 0.0f, (float)a[1] > 0.0f ? v[1] : 0.0f,
+                                               (float)a[2] > 0.0f ? v[2] : 0.0f, (float)a[3] > 0.0f ? v[3] : 0.0f);
+  }
+};
+
+template <bool AK, bool BK, class Epi>
 __global__ __launch_bounds__(256, 1) void k_gemm(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb,
                                                  int M, int N, int K, int kps, int ones_m, Epi epi) {
-  using C = GemmCfg<TN>;
-  constexpr int KT = C::KT, S = C::S, IMG = C::IMG, CH = C::CH;
+  using C = GemmCfg;
+  constexpr int KT = C::KT, IMG = C::IMG, CH = C::CH;
+  using OA = GemmOperand<AK>;
+  using OB = GemmOperand<BK>;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
   const int kb = blockIdx.z * kps, ke = min(K, kb + kps);
   uint4 ra[CH], rb[CH];
-  // chunk idx -> (row, col) of the 128 x 64 (NT) or 64 x 128 (TN) tile
   auto gload = [&](int k0) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int idx = tid + c * 256;
-      if (!TN) {
-        const int row = idx >> 3, col = (idx & 7) * 8;
-        const int m = m0 + row, n = n0 + row;
-        ra[c] = m < M ? *reinterpret_cast<const uint4*>(A + (size_t)m * lda + k0 + col) : uint4{0, 0, 0, 0};
-        rb[c] = n < N ? *reinterpret_cast<const uint4*>(Bm + (size_t)n * ldb + k0 + col) : uint4{0, 0, 0, 0};
-      } else {
-        const int row = idx >> 4, col = (idx & 15) * 8;
-        const int k = k0 + row;
-        ra[c] = uint4{0, 0, 0, 0};
-        if (k < ke && m0 + col == ones_m) ra[c].x = 0x3F80u;   // bf16 1.0 in element 0
-        else if (k < ke && m0 + col < M) ra[c] = *reinterpret_cast<const uint4*>(A + (size_t)k * lda + m0 + col);
-        rb[c] = (k < ke && n0 + col < N) ? *reinterpret_cast<const uint4*>(Bm + (size_t)k * ldb + n0 + col) : uint4{0, 0, 0, 0};
-      }
+      ra[c] = OA::load(A, lda, m0, M, k0, ke, tid + c * 256, ones_m);
+      rb[c] = OB::load(Bm, ldb, n0, N, k0, ke, tid + c * 256, -1);
     }
   };
   auto sstore = [&](int buf) {
     bf16* la = lds + buf * 2 * IMG;
-    bf16* lb = la + IMG;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int idx = tid + c * 256;
-      const int row = TN ? idx >> 4 : idx >> 3, col = TN ? (idx & 15) * 8 : (idx & 7) * 8;
-      *reinterpret_cast<uint4*>(la + row * S + col) = ra[c];
-      *reinterpret_cast<uint4*>(lb + row * S + col) = rb[c];
+      OA::store(la, tid + c * 256, ra[c]);
+      OB::store(la + IMG, tid + c * 256, rb[c]);
     }
-  };
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  const int h = lane >> 5, r = lane & 31;
-  const int gh = (lane >> 4) & 1, li = lane & 15, q = li >> 2, p = li & 3;
-  // operand fragment (32 rows/cols x 16 k) at tile offset `base` (m or n) and k offset k16
-  auto frag = [&](const bf16* img, int base, int k16) -> bf16x8 {
-    if (!TN) return *reinterpret_cast<const bf16x8*>(img + (base + r) * S + k16 + 8 * h);
-    const bf16* p0 = img + (k16 + 8 * h + q) * S + base + 16 * gh + 4 * p;
-    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * S));
-    return __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -106,34 +168,32 @@ __global__ __launch_bounds__(256, 1) void k_gemm(const bf16* __restrict__ A, int
     for (int ks = 0; ks < KT / 16; ++ks) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) af[t] = frag(la, wm * 64 + t * 32, ks * 16);
+      for (int t = 0; t < 2; ++t) af[t] = OA::frag(la, wm * 64 + t * 32, ks * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = frag(lb, wn * 64 + j * 32, ks * 16);
+      for (int j = 0; j < 2; ++j) bfr[j] = OB::frag(lb, wn * 64 + j * 32, ks * 16, lane);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[t][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bfr[j], acc[t][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[t][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[t], acc[t][j], 0, 0, 0);
     }
     if (it + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
+  // C^T tile: lane = m (lane & 31), reg e = n offset (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+  const int h = lane >> 5;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + wm * 64 + t * 32 + (lane & 31);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wm * 64 + t * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int n = n0 + wn * 64 + j * 32 + r;
-        if (m < M && n < N) epi(m, n, acc[t][j][e]);
+      for (int u = 0; u < 4; ++u) {
+        const int n = n0 + wn * 64 + j * 32 + 8 * u + 4 * h;
+        if (m < M && n < N)
+          epi(m, n, f32x4{acc[t][j][4 * u], acc[t][j][4 * u + 1], acc[t][j][4 * u + 2], acc[t][j][4 * u + 3]});
       }
+    }
 }
-
-struct EpiStoreF32 {   // out[m][n] = v (fp32)
-  float* out;
-  int ldo;
-  __device__ __forceinline__ void operator()(int m, int n, float v) const { out[(size_t)m * ldo + n] = v; }
-};
 
 }  // namespace qn
 }  // namespace qlx

@@ -202,14 +202,7 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
   const uint8_t* bact = L->d_bact + (size_t)u_local * B;
   // online: forward, Huber, backward
   model_forward_trunk(on, tab_s, (int)B, s);
-  Fc2Args oa = fc2_args(on, (int)B);
-  oa.actions = bact;
-  oa.y = L->d_targets + (size_t)u_local * B;
-  oa.gsample = on->w.gs;
-  oa.hsample = on->w.hs;
-  launch_fc2(3, oa, (int)B, s);
-  launch_loss_sum(on->w.hs, (int)B, L->d_losses + u_local, s);
-  model_backward(on, tab_s, (int)B, bact, s);
+  model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s);
   float scale = 1.0f;
   if (L->comm) {
     ProfScope ps(&L->prof, "allreduce", s);

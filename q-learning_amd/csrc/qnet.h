@@ -27,7 +27,6 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float* fc1slab = nullptr;
   float* slab = nullptr;
   float* bslab = nullptr;
-  float* g0_s2d = nullptr;
   float* loss = nullptr;
 };
 
@@ -42,7 +41,7 @@ struct qlx_model {
   float* d_v = nullptr;
   float* d_grads = nullptr;
   // bf16 MFMA operand copies ([n][k], k contiguous)
-  __bf16 *wf0 = nullptr, *wf1 = nullptr, *wb1 = nullptr, *wf2 = nullptr, *wb2 = nullptr, *wf3 = nullptr, *wb3 = nullptr;
+  __bf16 *wf0 = nullptr, *wf1 = nullptr, *wb1 = nullptr, *wf2 = nullptr, *wb2 = nullptr, *wb3 = nullptr;
   int64_t iterations = 0;
   float lr = 0.00025f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, clipnorm = 1.0f;
   int n_ranges = 0;
@@ -69,19 +68,21 @@ struct Fc2Args {
   const uint8_t* dones;    // mode 2
   float gamma;             // mode 2
   float* y_out;            // mode 2
-  const uint8_t* actions;  // mode 3
-  const float* y;          // mode 3
-  float* gsample;          // mode 3: dloss/dq_a per sample
-  float* hsample;          // mode 3: per-sample Huber value
+  const uint8_t* actions;  // training head
+  const float* y;          // training head
+  float* gsample;          // training head: dloss/dq_a per sample
+  float* hsample;          // training head: per-sample Huber value
 };
 Fc2Args fc2_args(qlx_model* m, int B);
 void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s);
-void launch_loss_sum(const float* h, int B, float* out, hipStream_t s);
 void model_workspace(qlx_model* m, int B);
 void model_pack(qlx_model* m);
 // store_acts = false skips writing a1/a2 (only a3 is needed when no backward pass follows)
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts = true);
-void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, hipStream_t s);
+// Huber head + backward after model_forward_trunk: loss -> *loss_dev, raw gradients -> m->d_grads
+void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
+                    hipStream_t s);
+// per-range sums of squares of the (scaled) gradients; k_adam finishes the per-variable norms
 void model_norms(qlx_model* m, hipStream_t s, float scale);
 void model_adam(qlx_model* m, hipStream_t s, float scale);
 }  // namespace qlx

@@ -41,7 +41,7 @@ __device__ __forceinline__ int conv1_s2d_k(int kh, int kw, int c) {
 }
 
 struct PackPtrs {
-  bf16 *wf0, *wf1, *wb1, *wf2, *wb2, *wf3, *wb3;
+  bf16 *wf0, *wf1, *wb1, *wf2, *wb2, *wb3;
 };
 
 // writes the bf16 copies of parameter element idx (global flat index) with value w
@@ -72,11 +72,7 @@ __device__ __forceinline__ void pack_one(const PackPtrs& P, int64_t idx, float w
   }
   idx -= 36864 + 64;
   if (idx < 0) return;
-  if (idx < 3136 * 512) {   // full_layer kernel [3136][512]
-    const int n = idx & 511, k = (int)(idx >> 9);
-    P.wf3[(size_t)n * 3136 + k] = v;
-    P.wb3[idx] = v;
-  }
+  if (idx < 3136 * 512) P.wb3[idx] = v;   // full_layer kernel [3136][512]: the Keras layout serves fwd and dgrad
 }
 
 __global__ void k_pack_all(const float* w, int64_t count, PackPtrs P) {
@@ -108,7 +104,7 @@ __global__ void k_frame_table(const uint8_t* frames, int B, const uint8_t** tabl
 // ------------------------------------------------------------------------------------------
 // dense 512 -> 3 (linear) on VALU, one wave per sample; optional heads:
 //   mode 0: q only; mode 1: argmax actions (predict_action); mode 2: max -> Bellman target
-//   mode 3: Huber loss + dq for train (needs actions, y)
+//   (the training head with Huber + dq lives in k_fc2_train)
 
 
 template <int MODE>
@@ -144,35 +140,63 @@ __global__ __launch_bounds__(256) void k_fc2(Fc2Args A) {
     const float mx = fmaxf(fmaxf(q0, q1), q2);
     const float r = A.rewards[b];
     A.y_out[b] = A.dones[b] ? r : r + mx * A.gamma;
-  } else if (MODE == 3) {   // Huber(delta=1) of e = q_a - y, mean over batch
-    const int a = A.actions[b];
-    const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
-    const float e = qa - A.y[b];
-    const float ae = fabsf(e);
-    A.hsample[b] = ae <= 1.0f ? 0.5f * e * e : ae - 0.5f;
-    const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
-    A.gsample[b] = ge / (float)A.B;
   }
 }
 
-// dz4[b][k] = g_b * W4[k][a_b] * (a4[b][k] > 0)
-__global__ void k_fc2_bwd_data(const bf16* a4, const float* w4, const uint8_t* actions, const float* gs, int B, bf16* dz4) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * 512) return;
-  const int b = i >> 9, k = i & 511;
-  const float v = (float)a4[i] > 0.0f ? gs[b] * w4[k * 3 + actions[b]] : 0.0f;
-  dz4[i] = (bf16)v;
+// Training head, one wave per sample: q = a4 W4 + b4, Huber(delta=1) of e = q_a - y (per-sample value and
+// dloss/dq_a = clip(e, -1, 1) / B), and the backward into the dense-512 layer in the same wave:
+// dz4[b][k] = g_b * W4[k][a_b] * (a4[b][k] > 0).  The xor butterfly leaves the full dot products in every
+// lane, so each lane finishes its own 8 k.
+__global__ __launch_bounds__(256) void k_fc2_train(Fc2Args A, bf16* dz4) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= A.B) return;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+  const bf16x8 v = ld8(A.a4 + (size_t)b * 512 + lane * 8);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = (float)v[e];
+    const float* w = A.w4 + (lane * 8 + e) * 3;
+    s0 += x * w[0];
+    s1 += x * w[1];
+    s2 += x * w[2];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  const float q0 = s0 + A.b4[0], q1 = s1 + A.b4[1], q2 = s2 + A.b4[2];
+  const int a = A.actions[b];
+  const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
+  const float e = qa - A.y[b];
+  const float ae = fabsf(e);
+  const float g = (ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f)) / (float)A.B;
+  if (lane == 0) {
+    A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2;
+    A.hsample[b] = ae <= 1.0f ? 0.5f * e * e : ae - 0.5f;
+    A.gsample[b] = g;
+  }
+  bf16x8 d;
+#pragma unroll
+  for (int e8 = 0; e8 < 8; ++e8) d[e8] = (bf16)((float)v[e8] > 0.0f ? g * A.w4[(lane * 8 + e8) * 3 + a] : 0.0f);
+  *reinterpret_cast<bf16x8*>(dz4 + (size_t)b * 512 + lane * 8) = d;
 }
 
-// dW4[k][a] = sum_b a4[b][k] g_b [a_b == a]; db4[a] = sum_b g_b [a_b == a]   (block per k, k = 512 -> bias)
-__global__ __launch_bounds__(256) void k_fc2_wgrad(const bf16* a4, const uint8_t* actions, const float* gs, int B,
-                                                   float* g_w4, float* g_b4) {
+// dW4[k][a] = sum_b a4[b][k] g_b [a_b == a] (block k < 512); db4[a] = sum_b g_b [a_b == a] (block 512);
+// loss = sum_b h_b / B (block 513).  Fixed strided + tree order: deterministic.
+__global__ __launch_bounds__(256) void k_fc2_wgrad(const bf16* a4, const uint8_t* actions, const float* gs, const float* hs,
+                                                   int B, float* g_w4, float* g_b4, float* loss) {
   __shared__ float red[3][256];
   const int k = blockIdx.x;
   float s[3] = {0.0f, 0.0f, 0.0f};
-  for (int b = threadIdx.x; b < B; b += 256) {
-    const float x = k < 512 ? (float)a4[(size_t)b * 512 + k] : 1.0f;
-    s[actions[b]] += x * gs[b];
+  if (k == 513) {
+    for (int b = threadIdx.x; b < B; b += 256) s[0] += hs[b];
+  } else {
+    for (int b = threadIdx.x; b < B; b += 256) {
+      const float x = k < 512 ? (float)a4[(size_t)b * 512 + k] : 1.0f;
+      s[actions[b]] += x * gs[b];
+    }
   }
   for (int j = 0; j < 3; ++j) red[j][threadIdx.x] = s[j];
   __syncthreads();
@@ -183,7 +207,8 @@ __global__ __launch_bounds__(256) void k_fc2_wgrad(const bf16* a4, const uint8_t
   }
   if (threadIdx.x < 3) {
     if (k < 512) g_w4[k * 3 + threadIdx.x] = red[threadIdx.x][0];
-    else g_b4[threadIdx.x] = red[threadIdx.x][0];
+    else if (k == 512) g_b4[threadIdx.x] = red[threadIdx.x][0];
+    else if (threadIdx.x == 0) *loss = red[0][0] / (float)B;
   }
 }
 
@@ -192,39 +217,18 @@ void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s) {
   switch (mode) {
     case 0: hipLaunchKernelGGL(k_fc2<0>, g, blk, 0, s, a); break;
     case 1: hipLaunchKernelGGL(k_fc2<1>, g, blk, 0, s, a); break;
-    case 2: hipLaunchKernelGGL(k_fc2<2>, g, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL(k_fc2<3>, g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_fc2<2>, g, blk, 0, s, a); break;
   }
   QLX_HIP(hipGetLastError());
-}
-
-// loss = sum_b h_b / B in fixed order (one block)
-__global__ void k_loss_sum(const float* h, int B, float* loss) {  // loss = sum_b h_b / B
-  __shared__ float red[256];
-  float s = 0.0f;
-  for (int b = threadIdx.x; b < B; b += 256) s += h[b];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *loss = red[0] / (float)B;
-}
-
-// conv1 weight gradient from s2d k order [256][32] into HWIO [8][8][4][32]
-__global__ void k_conv1_grad_unpermute(const float* g_s2d, float* g_hwio) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 8192) return;
-  const int oc = idx & 31, c = (idx >> 5) & 3, kw = (idx >> 7) & 7, kh = idx >> 10;
-  g_hwio[idx] = g_s2d[conv1_s2d_k(kh, kw, c) * 32 + oc];
 }
 
 // ------------------------------------------------------------------------------------------
 // clip_by_norm per variable + ResourceApplyAdam
 
-__global__ __launch_bounds__(256) void k_sumsq(const float* g, const int64_t* range_begin, const int64_t* range_end,
-                                               float scale, float* partial) {
+// Per-range sums of squares: block r sums gradient range r (<= 2048 elements of one variable).  The norms
+// themselves are finished by every k_adam block from these partials (fixed order, no extra launch).
+__global__ __launch_bounds__(256) void k_sumsq(const float* g, const int64_t* range_begin, const int64_t* range_end, float scale,
+                                               float* partial) {
   __shared__ float red[256];
   const int64_t b = range_begin[blockIdx.x], e = range_end[blockIdx.x];
   float s = 0.0f;
@@ -241,30 +245,14 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* g, const int64_t* ra
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-// one block per variable; fixed strided + tree order -> deterministic
-__global__ __launch_bounds__(256) void k_norms(const float* partial, const int* var_first, float* norms) {
-  __shared__ float red[256];
-  const int v = blockIdx.x;
-  float s = 0.0f;
-  for (int r = var_first[v] + threadIdx.x; r < var_first[v + 1]; r += 256) s += partial[r];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const float t = red[0];
-    norms[v] = t > 0.0f ? sqrtf(t) : t;   // tf.clip_by_norm: safe sqrt via where(l2sum > 0)
-  }
-}
-
 struct AdamArgs {
   float* w;
   float* m;
   float* v;
   const float* g;
-  const float* norms;
+  const float* partial;    // k_sumsq output
+  const int* var_first;    // partial range of variable v: [var_first[v], var_first[v + 1])
+  float* norms;            // written by block 0 (for the ABI)
   int64_t count;
   float scale;     // 1/world for data-parallel mean
   float alpha;     // lr * sqrt(1 - b2^t) / (1 - b1^t)
@@ -272,18 +260,32 @@ struct AdamArgs {
   PackPtrs pack;
 };
 
+// tf.clip_by_norm per variable + ResourceApplyAdam.  Every block first finishes the per-variable norms
+// from the k_sumsq partials (wave w reduces variables w, w+4, w+8: lane-strided sums + xor tree, the
+// same fixed order in every block).
 __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
   __shared__ int64_t offs[kNumVars + 1];
+  __shared__ float nrm[kNumVars];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (threadIdx.x == 0) {
     int64_t o = 0;
     for (int i = 0; i < kNumVars; ++i) { offs[i] = o; o += kVarSize[i]; }
     offs[kNumVars] = o;
   }
+  for (int v = wave; v < kNumVars; v += 4) {
+    float t = 0.0f;
+    for (int r = A.var_first[v] + lane; r < A.var_first[v + 1]; r += 64) t += A.partial[r];
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    if (lane == 0) {
+      nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
+      if (blockIdx.x == 0) A.norms[v] = nrm[v];
+    }
+  }
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.count; i += (int64_t)gridDim.x * blockDim.x) {
     int var = 0;
     while (i >= offs[var + 1]) ++var;
-    const float denom = fmaxf(A.norms[var], A.clipnorm);
+    const float denom = fmaxf(nrm[var], A.clipnorm);
     const float gc = (A.g[i] * A.scale * A.clipnorm) / denom;
     float m = A.m[i], v = A.v[i], w = A.w[i];
     m += (gc - m) * (1.0f - A.beta1);
@@ -320,7 +322,6 @@ void model_workspace(qlx_model* m, int B) {
   const size_t o_fc1slab = take((size_t)kFc1Split * B * 512 * 4);
   const size_t o_slab = take(kWgradSlabFloats * 4);
   const size_t o_bslab = take(kBiasSlabFloats * 4);
-  const size_t o_g0 = take(8192 * 4);
   const size_t o_loss = take(64);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
@@ -335,14 +336,13 @@ void model_workspace(qlx_model* m, int B) {
   w.fc1slab = (float*)(base + o_fc1slab);
   w.slab = (float*)(base + o_slab);
   w.bslab = (float*)(base + o_bslab);
-  w.g0_s2d = (float*)(base + o_g0);
   w.loss = (float*)(base + o_loss);
   m->ws_batch = B;
 }
 
 static PackPtrs pack_ptrs(qlx_model* m) {
   PackPtrs P;
-  P.wf0 = m->wf0; P.wf1 = m->wf1; P.wb1 = m->wb1; P.wf2 = m->wf2; P.wb2 = m->wb2; P.wf3 = m->wf3; P.wb3 = m->wb3;
+  P.wf0 = m->wf0; P.wf1 = m->wf1; P.wb1 = m->wb1; P.wf2 = m->wf2; P.wb2 = m->wb2; P.wb3 = m->wb3;
   return P;
 }
 
@@ -351,24 +351,6 @@ void model_pack(qlx_model* m) {
   QLX_HIP(hipGetLastError());
 }
 
-// k_igemm2 launch: persistent blocks (as many as LDS lets reside, <= 4 per CU on 256 CUs) over M tiles
-template <int BN, int WMT, int K, class LoadA, class Epi>
-static void launch_igemm2(LoadA la, const bf16* Bt, int M, int N, Epi epi, hipStream_t s) {
-  constexpr int BM = 4 * WMT * 32;
-  constexpr size_t lds = (size_t)BN * (K + 8) * sizeof(bf16);
-  static bool attr = false;
-  if (!attr) {
-    QLX_HIP(hipFuncSetAttribute((const void*)k_igemm2<BN, WMT, K, LoadA, Epi>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-    attr = true;
-  }
-  const int n_mtiles = (M + BM - 1) / BM;
-  const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / lds)));
-  const int grid_x = std::min(n_mtiles, 256 * per_cu);
-  hipLaunchKernelGGL((k_igemm2<BN, WMT, K, LoadA, Epi>), dim3(grid_x, N / BN), dim3(256), lds, s, la, Bt, M, n_mtiles, epi);
-}
-
-// forward through fc1 (a1..a4 in the workspace); `table` = [B][4] frame pointers
 // one block per CU (LDS-limited), persistent over samples
 static int trunk_grid(int B) { return std::max(1, std::min(B, 256)); }
 
@@ -377,18 +359,19 @@ static void set_lds_attr(Kern k, size_t bytes) {
   QLX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
 }
 
-template <bool TN, class Epi>
+template <bool AK, bool BK, class Epi>
 static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K, int splits, Epi epi, hipStream_t s,
                         int ones_m = -1) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_gemm<TN, Epi>, GemmCfg<TN>::LDS);
+    set_lds_attr(k_gemm<AK, BK, Epi>, GemmCfg::LDS);
     attr = true;
   }
   const int kps = (K + splits - 1) / splits;
-  QLX_CHECK(TN || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID, "k_gemm NT needs K and K/splits multiples of 64");
+  QLX_CHECK((AK && BK) || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID,
+            "k_gemm: row-major operands need K and K/splits multiples of 64");
   const dim3 grid((M + 127) / 128, (N + 127) / 128, splits);
-  hipLaunchKernelGGL((k_gemm<TN, Epi>), grid, dim3(256), GemmCfg<TN>::LDS, s, A, lda, Bm, ldb, M, N, K, kps, ones_m, epi);
+  hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), grid, dim3(256), GemmCfg::LDS, s, A, lda, Bm, ldb, M, N, K, kps, ones_m, epi);
 }
 
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts) {
@@ -411,9 +394,9 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
      // ReLU in fixed order) to fill the chip; from 64 M tiles on (B >= 8192) one pass with the epilogue fused
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
     if (B >= 64 * 128) {
-      launch_gemm<false>(w.a3, 3136, m->wf3, 3136, B, 512, 3136, 1, EpiBiasRelu{w.a4, p + var_offset(7), 512}, s);
+      launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, 1, Epi4BiasRelu{w.a4, p + var_offset(7), 512}, s);
     } else {
-      launch_gemm<false>(w.a3, 3136, m->wf3, 3136, B, 512, 3136, kFc1Split, EpiSlab{w.fc1slab, 512, (size_t)B * 512}, s);
+      launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, kFc1Split, Epi4Slab{w.fc1slab, 512, (size_t)B * 512}, s);
       hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, s, w.fc1slab,
                          (size_t)B * 512, kFc1Split, B, 512, p + var_offset(7), w.a4);
     }
@@ -431,44 +414,33 @@ Fc2Args fc2_args(qlx_model* m, int B) {
   return a;
 }
 
-// grads (raw, unclipped) of the Huber loss into m->d_grads; gs = per-sample dloss/dq_a, actions in ws
-void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, hipStream_t s) {
+// Huber loss (mean over the batch -> *loss_dev) and its raw, unclipped gradients into m->d_grads, after
+// model_forward_trunk on the same batch; actions / y are device arrays [B]
+void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
+                    hipStream_t s) {
   ModelWs& w = m->w;
   float* G = m->d_grads;
-  // fc2
-  {
-    ProfScope ps(m->prof, "fc2_bwd", s);
-    hipLaunchKernelGGL(k_fc2_bwd_data, dim3((B * 512 + 255) / 256), dim3(256), 0, s, w.a4, m->d_params + var_offset(8),
-                       actions, w.gs, B, w.dz4);
-    hipLaunchKernelGGL(k_fc2_wgrad, dim3(513), dim3(256), 0, s, w.a4, actions, w.gs, B, G + var_offset(8), G + var_offset(9));
+  {  // head: q, Huber, dz4 (one wave per sample); dW4, db4 and the loss (fixed-order block reductions)
+    ProfScope ps(m->prof, "fc2_head", s);
+    Fc2Args a = fc2_args(m, B);
+    a.actions = actions;
+    a.y = y;
+    a.gsample = w.gs;
+    a.hsample = w.hs;
+    hipLaunchKernelGGL(k_fc2_train, dim3((B + 3) / 4), dim3(256), 0, s, a, w.dz4);
+    hipLaunchKernelGGL(k_fc2_wgrad, dim3(514), dim3(256), 0, s, w.a4, actions, w.gs, w.hs, B, G + var_offset(8),
+                       G + var_offset(9), loss_dev);
   }
   // fc1: dW3 = a3^T dz4 (one chunk), db3; dz3 = (dz4 W3^T) * (a3 > 0)
   {
     ProfScope ps(m->prof, "fc1_wgrad", s, 2.0 * B * 512 * 3136);
     // row 3136 of the output = the all-ones row = db3, which follows dW3 [3136][512] in the flat gradient
-    launch_gemm<true>(w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, EpiStoreF32{G + var_offset(6), 512}, s, 3136);
+    launch_gemm<true, true>(w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, s, 3136);
   }
   {
     ProfScope ps(m->prof, "fc1_dgrad", s, 2.0 * B * 512 * 3136);
-    launch_gemm<false>(w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, EpiReluMask{w.dz3, w.a3, 3136}, s);
+    launch_gemm<false, false>(w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136}, s);
   }
-  // conv weight gradients: k_wgrad2 over m-chunks into fp32 slabs, then the fixed-order slab reduction
-  auto wgrad_conv = [&](const char* name, auto lx, const bf16* dz, int M, int KIN, int N, int target_chunks, float* gW, float* gb,
-                        auto kwt_tag, auto nb_tag) {
-    ProfScope ps(m->prof, name, s, 2.0 * M * KIN * N);
-    constexpr int KWT = decltype(kwt_tag)::value, NB = decltype(nb_tag)::value, KT = 64 * KWT;
-    int m_chunk = (int)align_up((M + target_chunks - 1) / target_chunks, 64);
-    if (m_chunk < 256) m_chunk = 256;
-    const int chunks = (M + m_chunk - 1) / m_chunk;
-    hipLaunchKernelGGL((k_wgrad2<KWT, NB, decltype(lx)>), dim3(KIN / KT, N / NB, chunks), dim3(256), 0, s, lx, dz, M, N,
-                       m_chunk, w.slab, N, (size_t)KIN * N, w.bslab);
-    hipLaunchKernelGGL(k_slab_reduce, dim3((KIN * N + 63) / 64), dim3(256), 0, s, w.slab, (size_t)KIN * N, chunks,
-                       (size_t)KIN * N, gW);
-    hipLaunchKernelGGL(k_slab_reduce, dim3((N + 63) / 64), dim3(256), 0, s, w.bslab, (size_t)N, chunks, (size_t)N, gb);
-  };
-  using I3 = std::integral_constant<int, 3>;
-  using I4 = std::integral_constant<int, 4>;
-  using I64 = std::integral_constant<int, 64>;
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
     ProfScope ps(m->prof, "trunk_bwd_data", s, 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512));
@@ -481,10 +453,29 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
                        m->wb1, w.dz2, w.dz1);
   }
   // conv3: dW2 = im2col(a2)^T dz3;  conv2: dW1 = im2col(a1)^T dz2
-  wgrad_conv("conv3_wgrad", LoadIm2col<9, 9, 64, 3, 1, 7, 7>{w.a2, B * 49}, w.dz3, B * 49, 576, 64, 96, G + var_offset(4),
-             G + var_offset(5), I3{}, I64{});
-  wgrad_conv("conv2_wgrad", LoadIm2col<20, 20, 32, 4, 2, 9, 9>{w.a1, B * 81}, w.dz2, B * 81, 512, 64, 128, G + var_offset(2),
-             G + var_offset(3), I4{}, I64{});
+  // conv3 (3 tap groups of 3 taps) and conv2 (2 groups of 8 taps): per-sample LDS-staged partials, then
+  // one fixed-order reduction of [dW | db] rows straight into the flat gradient (b follows W)
+  auto conv_wgrad = [&](const char* name, auto kern, size_t lds, int groups, const bf16* in, const bf16* dzp, size_t zs,
+                        double flops, float* gW) {
+    ProfScope ps(m->prof, name, s, flops);
+    static bool attr[2] = {false, false};
+    bool& a = attr[groups == 3 ? 0 : 1];
+    if (!a) {
+      set_lds_attr(kern, lds);
+      a = true;
+    }
+    const int chunks = std::max(1, std::min(B, 256 / groups));
+    const int per = (B + chunks - 1) / chunks;
+    const int used = (B + per - 1) / per;
+    hipLaunchKernelGGL(kern, dim3(used, groups), dim3(kTrunkThreads), lds, s, in, dzp, B, per, w.slab);
+    hipLaunchKernelGGL(k_slab_reduce<false>, dim3((unsigned)((zs + 63) / 64)), dim3(256), 0, s, w.slab, zs, used, zs, gW);
+  };
+  using CW3 = ConvWgradCfg<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>;
+  using CW2 = ConvWgradCfg<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>;
+  conv_wgrad("conv3_wgrad", k_conv_wgrad<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>, CW3::LDS, 3, w.a2, w.dz3, CW3::ZS,
+             2.0 * B * 49 * 576 * 64, G + var_offset(4));
+  conv_wgrad("conv2_wgrad", k_conv_wgrad<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>, CW2::LDS, 2, w.a1, w.dz2, CW2::ZS,
+             2.0 * B * 81 * 512 * 64, G + var_offset(2));
   // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames (s2d k order -> HWIO)
   {
     ProfScope ps(m->prof, "conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
@@ -494,23 +485,18 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
       attr = true;
     }
     const int grid = trunk_grid(B);
-    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B, w.slab, w.bslab);
-    hipLaunchKernelGGL(k_slab_reduce, dim3(8192 / 64), dim3(256), 0, s, w.slab, (size_t)8192, grid, (size_t)8192, w.g0_s2d);
-    hipLaunchKernelGGL(k_slab_reduce, dim3(1), dim3(256), 0, s, w.bslab, (size_t)32, grid, (size_t)32, G + var_offset(1));
+    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B, w.slab);
+    // s2d-ordered partials -> HWIO kernel gradient (var 0) and bias (var 1) in one pass
+    hipLaunchKernelGGL(k_slab_reduce<true>, dim3((kConv1SlabStride + 63) / 64), dim3(256), 0, s, w.slab,
+                       (size_t)kConv1SlabStride, grid, (size_t)kConv1SlabStride, G);
   }
-  hipLaunchKernelGGL(k_conv1_grad_unpermute, dim3(32), dim3(256), 0, s, w.g0_s2d, G);
   QLX_HIP(hipGetLastError());
 }
 
-void launch_loss_sum(const float* h, int B, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, h, B, out);
-  QLX_HIP(hipGetLastError());
-}
 
 void model_norms(qlx_model* m, hipStream_t s, float scale) {
   ProfScope ps(m->prof, "norms", s);
   hipLaunchKernelGGL(k_sumsq, dim3(m->n_ranges), dim3(256), 0, s, m->d_grads, m->d_rbeg, m->d_rend, scale, m->d_partial);
-  hipLaunchKernelGGL(k_norms, dim3(kNumVars), dim3(256), 0, s, m->d_partial, m->d_var_first, m->d_norms);
   QLX_HIP(hipGetLastError());
 }
 
@@ -520,6 +506,7 @@ void model_adam(qlx_model* m, hipStream_t s, float scale) {
   const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
   AdamArgs a;
   a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.norms = m->d_norms;
+  a.partial = m->d_partial; a.var_first = m->d_var_first;
   a.count = kNumParams; a.scale = scale;
   a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
@@ -585,7 +572,6 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     QLX_HIP(hipMalloc(&m->wb1, 32 * 1024 * 2));
     QLX_HIP(hipMalloc(&m->wf2, 64 * 576 * 2));
     QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
-    QLX_HIP(hipMalloc(&m->wf3, 512 * 3136 * 2));
     QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
     // norm ranges: chunks of <= 2048 elements (~830 blocks) that never cross a variable
     std::vector<int64_t> rb, re;
@@ -626,7 +612,7 @@ int32_t qlx_model_destroy(qlx_model* m) {
     if (!m) return;
     (void)hipSetDevice(m->device);
     (void)hipStreamSynchronize(m->stream);
-    void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wf3, m->wb3,
+    void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wb3,
                     m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->ws};
     for (void* p : ptrs) (void)hipFree(p);
     if (m->own_stream) (void)hipStreamDestroy(m->stream);
@@ -713,11 +699,7 @@ int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions
     QLX_HIP(hipMemcpyAsync(m->w.act, actions, B, hipMemcpyHostToDevice, s));
     QLX_HIP(hipMemcpyAsync(m->w.y, y, B * 4, hipMemcpyHostToDevice, s));
     model_forward_trunk(m, m->w.table, (int)B, s);
-    Fc2Args a = fc2_args(m, (int)B);
-    a.actions = m->w.act; a.y = m->w.y; a.gsample = m->w.gs; a.hsample = m->w.hs;
-    hipLaunchKernelGGL(k_fc2<3>, dim3((B + 3) / 4), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, m->w.hs, (int)B, m->w.loss);
-    model_backward(m, m->w.table, (int)B, m->w.act, s);
+    model_backward(m, m->w.table, (int)B, m->w.act, m->w.y, m->w.loss, s);
     if (grads_out) QLX_HIP(hipMemcpyAsync(grads_out, m->d_grads, kNumParams * 4, hipMemcpyDeviceToHost, s));
     model_norms(m, s, 1.0f);
     model_adam(m, s, 1.0f);

@@ -32,7 +32,10 @@ constexpr int kDZS = 48;                 // dz1 [416][32] row stride (tr-read co
 constexpr int kLdsX = 441 * kXS;         // bf16 elements
 constexpr int kLdsA1 = 400 * kA1S;
 constexpr int kLdsDZ = 416 * kDZS;
-constexpr size_t kTrunkFwdLds = (size_t)(kLdsX + kLdsA1) * 2;   // A2, A3 alias X (dead after conv1)
+constexpr int kLdsA3 = 49 * kA3S;
+// A2 aliases X (dead after conv1); A3 has its own region because its copy-out is deferred past the next
+// sample's staging (see k_trunk_fwd)
+constexpr size_t kTrunkFwdLds = (size_t)(kLdsX + kLdsA1 + kLdsA3) * 2;
 constexpr size_t kConv1WgradLds = (size_t)(kLdsX + kLdsDZ) * 2;
 constexpr int kFrameChunks = 4 * 441;    // 16-byte s2d blocks per sample
 constexpr int kPf = (kFrameChunks + kTrunkThreads - 1) / kTrunkThreads;
@@ -58,7 +61,10 @@ __device__ __forceinline__ void frames_prefetch(const uint8_t* const* table, int
     if (b < B && c < kFrameChunks) {
       const int slot = c / 441, pos = c - slot * 441;
       const uint8_t* f = table[b * 4 + slot];
-      if (f) pf[u] = *reinterpret_cast<const uint4*>(f + pos * 16);
+      // global (not flat) load: a flat load also counts on lgkmcnt, so every LDS wait in the conv phases
+      // would wait for this prefetch too
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      if (f) pf[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(f + pos * 16));
     }
   }
 }
@@ -111,15 +117,19 @@ __device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[s], a[s % D], acc, 0, 0, 0);
+      // unconditional refill (the last tile re-reads its own rows): equal LDS-read counts on every path let
+      // the compiler wait with lgkmcnt(D - 1) instead of draining the queue before each MFMA
       if (s + D < KS) a[s % D] = lds8(addr(t, s + D));
-      else if (more) a[s % D] = lds8(addr(t + dt, s + D - KS));
+      else a[s % D] = lds8(addr(more ? t + dt : t, s + D - KS));
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // keep the order: this MFMA, then its refill read
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     epi(t, acc);
   }
 }
 
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) {
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   const bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
   return __builtin_bit_cast(uint2, v);
 }
@@ -138,8 +148,8 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   bf16* X = lds;
   bf16* A1 = lds + kLdsX;
   bf16* A2 = lds;               // aliases X
-  bf16* A3 = lds + 81 * kA2S;   // aliases X, after A2
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  bf16* A3 = lds + kLdsX + kLdsA1;
+  const int wave = wave_id(), lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   const int c1 = (wave & 1) * 16, c2 = (wave & 3) * 16;   // the wave's output-channel slice, conv1 / conv2+3
   bf16x8 w1[8], w2[16], w3[18];
@@ -149,17 +159,25 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   for (int s = 0; s < 16; ++s) w2[s] = ld8(wf1 + (c2 + r) * 512 + 32 * s + 8 * g);
 #pragma unroll
   for (int s = 0; s < 18; ++s) w3[s] = ld8(wf2 + (c2 + r) * 576 + 32 * s + 8 * g);
-  // biases are re-read (L1 hits) in the epilogues: 12 resident VGPRs would spill the weight fragments
+  // biases staged in LDS (12 resident VGPRs would spill the weight fragments; a global load in the epilogue
+  // would make the compiler drain vmcnt, i.e. wait for the next sample's frame prefetch)
+  __shared__ __attribute__((aligned(16))) float sbias[160];
+  if (threadIdx.x < 160)
+    sbias[threadIdx.x] = threadIdx.x < 32 ? bias0[threadIdx.x] : (threadIdx.x < 96 ? bias1[threadIdx.x - 32] : bias2[threadIdx.x - 96]);
   auto bias_relu4 = [](const float* bias, f32x4 acc) {
     const float4 bv = *reinterpret_cast<const float4*>(bias);
     return pack4_bf16(relu(acc[0] + bv.x), relu(acc[1] + bv.y), relu(acc[2] + bv.z), relu(acc[3] + bv.w));
   };
+  // Loads and stores share vmcnt: waiting for a prefetch also waits for every store issued before the wait.
+  // Each sample's frames are therefore staged BEFORE the previous sample's a3 copy-out is issued, so the wait
+  // never covers fresh stores (a1 / a2 go out during the conv2 / conv3 phases, long before).
   uint4 pf[kPf];
   frames_prefetch(table, blockIdx.x, B, pf);
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    __syncthreads();   // previous sample's A2/A3 copy-out is done
+    lds_barrier();   // previous sample's conv phases are done with X / A2
     frames_stage(X, pf);
-    __syncthreads();
+    if (b != (int)blockIdx.x) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)(b - gridDim.x) * 3136);
+    lds_barrier();
     frames_prefetch(table, b + gridDim.x, B, pf);
     // conv1: M = 400 (25 tiles of 16), N = 32, K = 256: k-step s covers tap (i, j) = (s >> 2, (s >> 1) & 1)
     conv_tiles<8, 4>(
@@ -169,9 +187,9 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
           return X + ((ox + (s >> 2)) * 21 + oy + ((s >> 1) & 1)) * kXS + 32 * (s & 1) + 8 * g;
         },
         [&](int t, f32x4 acc) {
-          *reinterpret_cast<uint2*>(A1 + (t * 16 + r) * kA1S + c1 + 4 * g) = bias_relu4(bias0 + c1 + 4 * g, acc);
+          *reinterpret_cast<uint2*>(A1 + (t * 16 + r) * kA1S + c1 + 4 * g) = bias_relu4(sbias + c1 + 4 * g, acc);
         });
-    __syncthreads();
+    lds_barrier();
     if (STORE12) lds_copy_out<400, 32, kA1S>(A1, a1 + (size_t)b * 12800);
     // conv2: 4x4 stride 2 over A1 [20][20][32]; M = 81 (6 tiles), k-step s = tap (kh, kw) = (s >> 2, s & 3)
     conv_tiles<16, 4>(
@@ -183,9 +201,9 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
         [&](int t, f32x4 acc) {
           const int m = t * 16 + r;
           if (m < 81)
-            *reinterpret_cast<uint2*>(A2 + m * kA2S + c2 + 4 * g) = bias_relu4(bias1 + c2 + 4 * g, acc);
+            *reinterpret_cast<uint2*>(A2 + m * kA2S + c2 + 4 * g) = bias_relu4(sbias + 32 + c2 + 4 * g, acc);
         });
-    __syncthreads();
+    lds_barrier();
     if (STORE12) lds_copy_out<81, 64, kA2S>(A2, a2 + (size_t)b * 5184);
     // conv3: 3x3 stride 1 over A2 [9][9][64]; M = 49 (4 tiles), k-step s: tap s >> 1, channel half s & 1
     conv_tiles<18, 3>(
@@ -198,25 +216,26 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
         [&](int t, f32x4 acc) {
           const int m = t * 16 + r;
           if (m < 49)
-            *reinterpret_cast<uint2*>(A3 + m * kA3S + c2 + 4 * g) = bias_relu4(bias2 + c2 + 4 * g, acc);
+            *reinterpret_cast<uint2*>(A3 + m * kA3S + c2 + 4 * g) = bias_relu4(sbias + 96 + c2 + 4 * g, acc);
         });
-    __syncthreads();
-    lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)b * 3136);
   }
+  lds_barrier();
+  const int last = (int)blockIdx.x + ((B - 1 - (int)blockIdx.x) / (int)gridDim.x) * (int)gridDim.x;
+  if ((int)blockIdx.x < B) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)last * 3136);
 }
 
-// conv1 weight gradient: per block fp32 partial dW[256 (s2d k)][32] into slab[blockIdx.x] and the bias
-// partial db[32] into bias_slab[blockIdx.x]; reduced over blocks in fixed order by k_slab_reduce.
+// conv1 weight gradient: per block fp32 partial dW[256 (s2d k)][32] followed by the bias partial db[32] in
+// slab[blockIdx.x] (stride kConv1SlabStride); reduced over blocks in fixed order by k_slab_reduce<true>.
+constexpr int kConv1SlabStride = 8192 + 32;
 // Wave w owns k tiles 2w, 2w+1 (one s2d tap (i, j) = ((w >> 1) >> 1, (w >> 1) & 1), 32 channels) x both
 // 16-column n tiles.  m-steps of 32 im2col rows (13 per sample, rows 400..415 have dz = 0).
 __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t* const* __restrict__ table,
-                                                                  const bf16* __restrict__ dz1, int B, float* slab,
-                                                                  float* bias_slab) {
+                                                                  const bf16* __restrict__ dz1, int B, float* slab) {
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   bf16* X = lds;
   bf16* DZ = lds + kLdsX;
   __shared__ float bred[16][32];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int ij = wave >> 1, ti = ij >> 1, tj = ij & 1;
   const int col0 = (wave & 1) * 32 + 4 * p;   // channel of this lane's first k tile (second: +16)
@@ -231,25 +250,31 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
   const int bn = tid & 31, brg = tid >> 5;   // bias: column bn, rows brg + 16 i
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   auto tr = [](const bf16* pp) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pp)); };
-  uint4 pf[kPf];
-  frames_prefetch(table, blockIdx.x, B, pf);
-  for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    // dz1 sample block [400][32] -> registers (1600 chunks)
-    uint4 dv[4];
+  uint4 pf[kPf], dv[4];
+  // dz1 sample block [400][32] -> registers (1600 chunks), one sample ahead like the frames
+  auto dz_prefetch = [&](int b) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + u * kTrunkThreads;
-      dv[u] = c < 1600 ? *reinterpret_cast<const uint4*>(dz1 + (size_t)b * 12800 + c * 8) : uint4{0, 0, 0, 0};
+      dv[u] = uint4{0, 0, 0, 0};
+      if (b < B && c < 1600)
+        dv[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(dz1 + (size_t)b * 12800 + c * 8));
     }
-    __syncthreads();   // previous sample's readers are done
+  };
+  frames_prefetch(table, blockIdx.x, B, pf);
+  dz_prefetch(blockIdx.x);
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    lds_barrier();   // previous sample's readers are done
     frames_stage(X, pf);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + u * kTrunkThreads;
       if (c < 1600) *reinterpret_cast<uint4*>(DZ + (c >> 2) * kDZS + (c & 3) * 8) = dv[u];
     }
-    __syncthreads();
+    lds_barrier();
     frames_prefetch(table, b + gridDim.x, B, pf);
+    dz_prefetch(b + gridDim.x);
     for (int ms = 0; ms < 13; ++ms) {
       const int m0 = ms * 32;
       // rows of this lane's tr reads: m0 + 4g + q and m0 + 16 + 4g + q
@@ -278,7 +303,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
     for (int m = brg; m < 400; m += 16) bsum += (float)DZ[m * kDZS + bn];
   }
   // D tile (a, c): row k = ij * 64 + (wave & 1) * 32 + a * 16 + 4g + e, col n = c * 16 + li
-  float* out = slab + (size_t)blockIdx.x * 8192;
+  float* out = slab + (size_t)blockIdx.x * kConv1SlabStride;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -286,11 +311,11 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
 #pragma unroll
       for (int e = 0; e < 4; ++e) out[(ij * 64 + (wave & 1) * 32 + a * 16 + 4 * g + e) * 32 + c * 16 + li] = acc[a][c][e];
   bred[brg][bn] = bsum;
-  __syncthreads();
+  lds_barrier();
   if (tid < 32) {
     float s = 0.0f;
     for (int i = 0; i < 16; ++i) s += bred[i][tid];
-    bias_slab[blockIdx.x * 32 + tid] = s;
+    out[8192 + tid] = s;
   }
 }
 
@@ -315,33 +340,61 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
   bf16* P2 = lds + kLdsPad;         // dz2 (masked), interior (oh + 1, ow + 1)
   bf16* M2 = lds + 2 * kLdsPad;     // a2
   bf16* D1 = M2 + kLdsA2M;          // dz1 parity rows before masking: [400][32] in natural (ih, iw) order
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int r = lane & 15, g = lane >> 4;
   for (int i = tid; i < 2 * kLdsPad / 8; i += kTrunkThreads) *reinterpret_cast<uint4*>(lds + i * 8) = uint4{0, 0, 0, 0};
-  const int n3 = (wave & 3) * 16 + r;   // phase A: output channel c of dz2
-  const int n2 = wave * 16 + r;         // phase B: p*32 + c
-  bf16x8 w3[18], w2[8];
+  const int c3 = (wave & 3) * 16;       // phase A: the wave's 16 channels of dz2
+  bf16x8 w3[18], w2[8];                 // A operands (row = lane & 15 of the wave's channel slice)
 #pragma unroll
-  for (int s = 0; s < 18; ++s) w3[s] = ld8(wb2 + n3 * 576 + 32 * s + 8 * g);
+  for (int s = 0; s < 18; ++s) w3[s] = ld8(wb2 + (c3 + r) * 576 + 32 * s + 8 * g);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) w2[s] = ld8(wb1 + n2 * 256 + 32 * s + 8 * g);
-  // prefetch: dz3 392 chunks + a2 648 chunks = 1040 -> 3 per thread
+  for (int s = 0; s < 8; ++s) w2[s] = ld8(wb1 + (wave * 16 + r) * 256 + 32 * s + 8 * g);
+  // prefetch: dz3 392 chunks + a2 648 chunks = 1040 -> 3 per thread (staged to LDS); the sample's a1 (the
+  // dz1 ReLU mask, 1600 chunks -> 4 per thread) stays in registers in the mapping of the dz1 copy-out.
+  // Loads and stores share vmcnt, so a sample's dz1 copy-out is deferred until after the next sample's
+  // staging wait: no fresh stores are outstanding when a prefetch is awaited.
   constexpr int kC3 = 392, kCA = 648, kCT = kC3 + kCA, kPB = (kCT + kTrunkThreads - 1) / kTrunkThreads;
-  uint4 pf[kPB];
+  constexpr int kPA = (1600 + kTrunkThreads - 1) / kTrunkThreads;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) u32x4 gvec;
+  uint4 pf[kPB], pa[kPA];
   auto prefetch = [&](int b) {
 #pragma unroll
     for (int u = 0; u < kPB; ++u) {
       const int c = tid + u * kTrunkThreads;
       pf[u] = uint4{0, 0, 0, 0};
       if (b < B && c < kCT)
-        pf[u] = c < kC3 ? *reinterpret_cast<const uint4*>(dz3 + (size_t)b * 3136 + c * 8)
-                        : *reinterpret_cast<const uint4*>(a2 + (size_t)b * 5184 + (c - kC3) * 8);
+        pf[u] = __builtin_bit_cast(uint4, c < kC3 ? *(gvec*)(dz3 + (size_t)b * 3136 + c * 8)
+                                                  : *(gvec*)(a2 + (size_t)b * 5184 + (c - kC3) * 8));
+    }
+  };
+  auto prefetch_mask = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < kPA; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      pa[u] = uint4{0, 0, 0, 0};
+      if (b < B && c < 1600) pa[u] = __builtin_bit_cast(uint4, *(gvec*)(a1 + (size_t)b * 12800 + c * 8));
+    }
+  };
+  // dz1 = D1 * (a1 > 0) -> global, coalesced (D1 and pa hold sample b)
+  auto dz1_out = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < kPA; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      if (c < 1600) {
+        const int row = c >> 2, col = (c & 3) * 8;
+        const bf16x8 act = __builtin_bit_cast(bf16x8, pa[u]);
+        bf16x8 v = lds8(D1 + row * kA1S + col);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (float)act[e] > 0.0f ? v[e] : (bf16)0.0f;
+        *reinterpret_cast<bf16x8*>(dz1 + (size_t)b * 12800 + row * 32 + col) = v;
+      }
     }
   };
   prefetch(blockIdx.x);
-  __syncthreads();   // borders zeroed
+  lds_barrier();   // borders zeroed
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    __syncthreads();   // previous sample's readers are done
+    lds_barrier();   // previous sample's readers are done
 #pragma unroll
     for (int u = 0; u < kPB; ++u) {
       const int c = tid + u * kTrunkThreads;
@@ -353,66 +406,193 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
         *reinterpret_cast<uint4*>(M2 + row * 72 + col) = pf[u];
       }
     }
-    __syncthreads();
+    if (b != (int)blockIdx.x) dz1_out(b - gridDim.x);
+    lds_barrier();
     prefetch(b + gridDim.x);
-    // phase A: dz2
-    for (int t = wave >> 2; t < 6; t += 2) {
-      const int m = min(t * 16 + r, 80), ih = m / 9, iw = m - ih * 9;
-      const bf16* ar = P3 + ((ih + 2) * 11 + iw + 2) * kPadS + 8 * g;
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(ar - (kh * 11 + kw) * kPadS + 32 * (s & 1)), w3[s], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int mm = t * 16 + 4 * g + e;
-        if (mm < 81) {
-          const int oh = mm / 9, ow = mm - oh * 9;
-          const float v = (float)M2[mm * 72 + n3] > 0.0f ? acc[e] : 0.0f;
-          P2[((oh + 1) * 11 + ow + 1) * kPadS + n3] = (bf16)v;
-        }
-      }
-    }
-    __syncthreads();
+    prefetch_mask(b);
+    // phase A: dz2 (wave: channel slice c3, tiles wave >> 2, +2, ...)
+    conv_tiles<18, 3>(
+        wave >> 2, 2, 6, w3,
+        [&](int t, int s) {
+          const int m = min(t * 16 + r, 80), ih = m / 9, iw = m - ih * 9;
+          const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
+          return P3 + ((ih + 2 - kh) * 11 + iw + 2 - kw) * kPadS + 32 * (s & 1) + 8 * g;
+        },
+        [&](int t, f32x4 acc) {
+          const int m = t * 16 + r;
+          if (m < 81) {
+            const int oh = m / 9, ow = m - oh * 9;
+            const bf16x4 act = *reinterpret_cast<const bf16x4*>(M2 + m * 72 + c3 + 4 * g);
+            *reinterpret_cast<uint2*>(P2 + ((oh + 1) * 11 + ow + 1) * kPadS + c3 + 4 * g) =
+                pack4_bf16((float)act[0] > 0.0f ? acc[0] : 0.0f, (float)act[1] > 0.0f ? acc[1] : 0.0f,
+                           (float)act[2] > 0.0f ? acc[2] : 0.0f, (float)act[3] > 0.0f ? acc[3] : 0.0f);
+          }
+        });
+    lds_barrier();
     // dz2 -> global (81 x 64)
     for (int c = tid; c < 648; c += kTrunkThreads) {
       const int row = c >> 3, col = (c & 7) * 8, oh = row / 9, ow = row - oh * 9;
       *reinterpret_cast<uint4*>(dz2 + (size_t)b * 5184 + row * 64 + col) =
           *reinterpret_cast<const uint4*>(P2 + ((oh + 1) * 11 + ow + 1) * kPadS + col);
     }
-    // phase B: dz1 parity classes; wave = n tile (p = wave >> 1, c = (wave & 1) * 16 + r)
+    // phase B: dz1 parity classes; wave = 16-column slice of N = p*32 + c (p = wave >> 1)
     {
-      const int p = wave >> 1, ph = p >> 1, pw = p & 1, c = (wave & 1) * 16 + r;
-      for (int t = 0; t < 7; ++t) {
-        const int m = min(t * 16 + r, 99), i = m / 10, j = m - i * 10;
-        const bf16* ar = P2 + ((i + 1) * 11 + j + 1) * kPadS + 8 * g;
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      const int p = wave >> 1, ph = p >> 1, pw = p & 1, c0 = (wave & 1) * 16;
+      conv_tiles<8, 4>(
+          0, 1, 7, w2,
+          [&](int t, int s) {
+            const int m = min(t * 16 + r, 99), i = m / 10, j = m - i * 10;
+            const int tp = s >> 1, th = tp >> 1, tw = tp & 1;
+            return P2 + ((i + 1 - th) * 11 + j + 1 - tw) * kPadS + 32 * (s & 1) + 8 * g;
+          },
+          [&](int t, f32x4 acc) {
+            const int m = t * 16 + r;
+            if (m < 100) {
+              const int i = m / 10, j = m - i * 10;
+              *reinterpret_cast<uint2*>(D1 + ((2 * i + ph) * 20 + 2 * j + pw) * kA1S + c0 + 4 * g) =
+                  pack4_bf16(acc[0], acc[1], acc[2], acc[3]);
+            }
+          });
+    }
+    lds_barrier();
+  }
+  lds_barrier();
+  const int last = (int)blockIdx.x + ((B - 1 - (int)blockIdx.x) / (int)gridDim.x) * (int)gridDim.x;
+  if ((int)blockIdx.x < B) dz1_out(last);
+}
+
+}  // namespace qn
+}  // namespace qlx
+
+namespace qlx {
+namespace qn {
+
+// Weight gradient of conv2 / conv3, per sample from LDS:
+//   dW[(kh*KS + kw)*C + c][n] = sum_samples sum_(oh,ow) in[oh*S + kh][ow*S + kw][c] * dz[oh][ow][n]
+//   db[n] = sum dz[..][n]
+// Block (8 waves) = one group of TG taps (TG*C rows of dW) x one chunk of samples; per sample the input
+// activation [IH*IW][C] and dz [OH*OW][64] are staged into LDS once (prefetched one sample ahead), and
+// the m-reduction (output positions, 32 per MFMA) reads both operands with ds_read_b64_tr_b16: each lane
+// supplies the LDS row of its own im2col position, so the im2col is never materialised.  Wave w owns
+// KTW k-tiles (16 rows of dW each) x NTW of the four 16-column n-tiles.
+// Output: slab[chunk][TAPS*C*64 + 64] rows of [dW partial | db partial] (db from tap group 0 only).
+template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW>
+struct ConvWgradCfg {
+  static constexpr int M = OH * OW, MP = (M + 31) / 32 * 32;   // positions, padded to the 32-row m-step
+  static constexpr int XS = C + (C == 32 ? 8 : 16);            // input row stride (bf16): 20 / 40 dwords
+  static constexpr int DS = 64 + 16;                            // dz row stride: 40 dwords
+  static constexpr int LX = IH * IW * XS, LD = MP * DS;
+  static constexpr size_t LDS = (size_t)(LX + LD) * 2;
+  static constexpr int KTILES = TG * C / 16;                    // 16-row k tiles per block
+  static_assert(4 % NTW == 0 && (KTILES / KTW) * (4 / NTW) == 8 && KTILES % KTW == 0,
+                "KTW k tiles x NTW n tiles per wave must cover the block's KTILES x 4 tiles with 8 waves");
+  static constexpr int CHX = IH * IW * C / 8, CHD = M * 64 / 8;  // 16-byte chunks per sample
+  static constexpr int PF = (CHX + CHD + kTrunkThreads - 1) / kTrunkThreads;
+  static constexpr int TAPS = KS * KS;
+  static constexpr size_t ZS = (size_t)TAPS * C * 64 + 64;      // slab row
+};
+
+template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW>
+__global__ __launch_bounds__(kTrunkThreads, 1) void k_conv_wgrad(const bf16* __restrict__ in, const bf16* __restrict__ dz,
+                                                                 int B, int per_chunk, float* slab) {
+  using Cf = ConvWgradCfg<IH, IW, C, KS, S, OH, OW, TG, KTW, NTW>;
+  constexpr int M = Cf::M, MP = Cf::MP, XS = Cf::XS, DS = Cf::DS;
+  constexpr int CHX = Cf::CHX, CHD = Cf::CHD, PF = Cf::PF;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* X = lds;
+  bf16* DZ = lds + Cf::LX;
+  const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int tg = blockIdx.y;                       // tap group
+  const int b0 = blockIdx.x * per_chunk, b1 = min(B, b0 + per_chunk);
+  // wave's tiles: k tiles kt0 .. kt0+KTW-1, n tiles nt0 .. nt0+NTW-1
+  constexpr int NGROUPS = 4 / NTW;                  // waves sharing a k-tile set
+  const int kt0 = (wave / NGROUPS) * KTW, nt0 = (wave % NGROUPS) * NTW;
+  for (int i = tid; i < (MP - M) * DS / 8; i += kTrunkThreads)   // zero dz pad rows once
+    *reinterpret_cast<uint4*>(DZ + M * DS + i * 8) = uint4{0, 0, 0, 0};
+  f32x4 acc[KTW][NTW];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int tp = s >> 1, th = tp >> 1, tw = tp & 1;
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(ar - (th * 11 + tw) * kPadS + 32 * (s & 1)), w2[s], acc, 0, 0, 0);
-        }
+  for (int a = 0; a < KTW; ++a)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int mm = t * 16 + 4 * g + e;
-          if (mm < 100) {
-            const int ii = mm / 10, jj = mm - ii * 10;
-            D1[((2 * ii + ph) * 20 + 2 * jj + pw) * kA1S + c] = (bf16)acc[e];
-          }
-        }
+    for (int c = 0; c < NTW; ++c) acc[a][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float bsum = 0.0f;
+  const int bn = tid & 63, brg = tid >> 6;          // bias: column bn, rows brg + 8 i
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) u32x4 gvec;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  uint4 pf[PF];
+  auto prefetch = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      pf[u] = uint4{0, 0, 0, 0};
+      if (b < b1 && c < CHX + CHD)
+        pf[u] = __builtin_bit_cast(uint4, c < CHX ? *(gvec*)(in + (size_t)b * (IH * IW * C) + c * 8)
+                                                  : *(gvec*)(dz + (size_t)b * (M * 64) + (c - CHX) * 8));
+    }
+  };
+  auto tr = [](const bf16* pp) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pp)); };
+  prefetch(b0);
+  for (int b = b0; b < b1; ++b) {
+    lds_barrier();   // previous sample's readers are done
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      if (c < CHX) {
+        const int row = c / (C / 8), col = (c - row * (C / 8)) * 8;
+        *reinterpret_cast<uint4*>(X + row * XS + col) = pf[u];
+      } else if (c < CHX + CHD) {
+        const int cc = c - CHX, row = cc >> 3, col = (cc & 7) * 8;
+        *reinterpret_cast<uint4*>(DZ + row * DS + col) = pf[u];
       }
     }
-    __syncthreads();
-    // dz1 = D1 * (a1 > 0) -> global, coalesced
-    for (int c = tid; c < 1600; c += kTrunkThreads) {
-      const int row = c >> 2, col = (c & 3) * 8;
-      const bf16x8 act = ld8(a1 + (size_t)b * 12800 + row * 32 + col);
-      bf16x8 v = lds8(D1 + row * kA1S + col);
+    lds_barrier();
+    prefetch(b + 1);
+#pragma unroll 1
+    for (int m0 = 0; m0 < MP; m0 += 32) {
+      // this lane's two tr-read rows: m0 + 4g + q and m0 + 16 + 4g + q (clamped; their dz rows are zero)
+      const int mA = min(m0 + 4 * g + q, M - 1), mB = min(m0 + 16 + 4 * g + q, M - 1);
+      const int ohA = mA / OW, owA = mA - ohA * OW, ohB = mB / OW, owB = mB - ohB * OW;
+      bf16x8 bf[NTW];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (float)act[e] > 0.0f ? v[e] : (bf16)0.0f;
-      *reinterpret_cast<bf16x8*>(dz1 + (size_t)b * 12800 + row * 32 + col) = v;
+      for (int c = 0; c < NTW; ++c) {
+        const s16x4 v0 = tr(DZ + (m0 + 4 * g + q) * DS + (nt0 + c) * 16 + 4 * p);
+        const s16x4 v1 = tr(DZ + (m0 + 16 + 4 * g + q) * DS + (nt0 + c) * 16 + 4 * p);
+        bf[c] = __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+      }
+#pragma unroll
+      for (int a = 0; a < KTW; ++a) {
+        const int kr = (tg * Cf::KTILES + kt0 + a) * 16;   // first dW row of this k tile
+        const int tap = kr / C, c0 = kr - tap * C, kh = tap / KS, kw = tap - kh * KS;
+        const bf16* xa = X + ((ohA * S + kh) * IW + owA * S + kw) * XS + c0 + 4 * p;
+        const bf16* xb = X + ((ohB * S + kh) * IW + owB * S + kw) * XS + c0 + 4 * p;
+        const s16x4 v0 = tr(xa), v1 = tr(xb);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+#pragma unroll
+        for (int c = 0; c < NTW; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[c], acc[a][c], 0, 0, 0);
+      }
+    }
+    if (tg == 0)
+      for (int m = brg; m < M; m += 8) bsum += (float)DZ[m * DS + bn];
+  }
+  // D tile (a, c): row k = (tg * KTILES + kt0 + a) * 16 + 4g + e, col n = (nt0 + c) * 16 + li
+  float* out = slab + (size_t)blockIdx.x * Cf::ZS;
+#pragma unroll
+  for (int a = 0; a < KTW; ++a)
+#pragma unroll
+    for (int c = 0; c < NTW; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        out[(size_t)((tg * Cf::KTILES + kt0 + a) * 16 + 4 * g + e) * 64 + (nt0 + c) * 16 + li] = acc[a][c][e];
+  if (tg == 0) {
+    __shared__ float bred[8][64];
+    bred[brg][bn] = bsum;
+    lds_barrier();
+    if (tid < 64) {
+      float sb = 0.0f;
+      for (int i = 0; i < 8; ++i) sb += bred[i][tid];
+      out[(size_t)Cf::TAPS * C * 64 + tid] = sb;
     }
   }
 }
