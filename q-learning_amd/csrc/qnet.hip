@@ -44,30 +44,31 @@ struct PackPtrs {
   bf16 *wf0, *wf1, *wb1, *wf2, *wb2, *wb3;
 };
 
-// writes the bf16 copies of parameter element idx (global flat index) with value w
+// writes the bf16 copies of parameter element idx (global flat index) with value w; the conv operand copies
+// are MFMA-fragment-major (frag_index), the dense one keeps the Keras [3136][512] layout
 __device__ __forceinline__ void pack_one(const PackPtrs& P, int64_t idx, float w) {
   const bf16 v = (bf16)w;
   if (idx < 8192) {   // conv1 kernel [8][8][4][32]
     const int oc = idx & 31, c = (idx >> 5) & 3, kw = (idx >> 7) & 7, kh = (int)(idx >> 10);
-    P.wf0[oc * 256 + conv1_s2d_k(kh, kw, c)] = v;
+    P.wf0[frag_index(oc, conv1_s2d_k(kh, kw, c), 256)] = v;
     return;
   }
   idx -= 8192 + 32;
   if (idx < 0) return;
   if (idx < 32768) {   // conv2 kernel [4][4][32][64]
     const int oc = idx & 63, c = (idx >> 6) & 31, tap = (int)(idx >> 11);   // tap = kh*4 + kw
-    P.wf1[oc * 512 + tap * 32 + c] = v;
+    P.wf1[frag_index(oc, tap * 32 + c, 512)] = v;
     // backward data by parity class p = (kh&1)*2 + (kw&1): [p*32 + c][(kh>>1)*2 + (kw>>1)][oc]
     const int kh = tap >> 2, kw = tap & 3, p = (kh & 1) * 2 + (kw & 1);
-    P.wb1[(p * 32 + c) * 256 + ((kh >> 1) * 2 + (kw >> 1)) * 64 + oc] = v;
+    P.wb1[frag_index(p * 32 + c, ((kh >> 1) * 2 + (kw >> 1)) * 64 + oc, 256)] = v;
     return;
   }
   idx -= 32768 + 64;
   if (idx < 0) return;
   if (idx < 36864) {   // conv3 kernel [3][3][64][64]
     const int oc = idx & 63, c = (idx >> 6) & 63, tap = (int)(idx >> 12);  // tap = kh*3 + kw
-    P.wf2[oc * 576 + tap * 64 + c] = v;
-    P.wb2[c * 576 + tap * 64 + oc] = v;
+    P.wf2[frag_index(oc, tap * 64 + c, 576)] = v;
+    P.wb2[frag_index(c, tap * 64 + oc, 576)] = v;
     return;
   }
   idx -= 36864 + 64;
@@ -431,13 +432,19 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     hipLaunchKernelGGL(k_fc2_wgrad, dim3(514), dim3(256), 0, s, w.a4, actions, w.gs, w.hs, B, G + var_offset(8),
                        G + var_offset(9), loss_dev);
   }
-  // fc1: dW3 = a3^T dz4 (one chunk), db3; dz3 = (dz4 W3^T) * (a3 > 0)
-  {
-    ProfScope ps(m->prof, "fc1_wgrad", s, 2.0 * B * 512 * 3136);
-    // row 3136 of the output = the all-ones row = db3, which follows dW3 [3136][512] in the flat gradient
-    launch_gemm<true, true>(w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, s, 3136);
+  // Branches (all only read the forward activations / dz chain and write disjoint gradient ranges):
+  //   main  : fc1 dgrad -> backward data (dz2, dz1) -> conv1 wgrad
+  //   side 0: fc1 wgrad (100 blocks: fills the CUs the dgrad chain leaves idle) -> conv3 wgrad
+  //   side 1: conv2 wgrad
+  // joined on the main stream before returning (norms + Adam follow on it).
+  hipStream_t s2 = m->side[0], s3 = m->side[1];
+  QLX_HIP(hipEventRecord(m->ev[0], s));
+  QLX_HIP(hipStreamWaitEvent(s2, m->ev[0], 0));
+  {  // fc1: dW3 = a3^T dz4 and db3 (row 3136 = the all-ones row; db3 follows dW3 [3136][512] in the flat gradient)
+    ProfScope ps(m->prof, "fc1_wgrad", s2, 2.0 * B * 512 * 3136);
+    launch_gemm<true, true>(w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, s2, 3136);
   }
-  {
+  {  // dz3 = (dz4 W3^T) * (a3 > 0)
     ProfScope ps(m->prof, "fc1_dgrad", s, 2.0 * B * 512 * 3136);
     launch_gemm<false, false>(w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136}, s);
   }
@@ -452,12 +459,14 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     hipLaunchKernelGGL(k_trunk_bwd_data, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkBwdLds, s, w.dz3, w.a2, w.a1, B, m->wb2,
                        m->wb1, w.dz2, w.dz1);
   }
-  // conv3: dW2 = im2col(a2)^T dz3;  conv2: dW1 = im2col(a1)^T dz2
+  QLX_HIP(hipEventRecord(m->ev[1], s));
+  QLX_HIP(hipStreamWaitEvent(s2, m->ev[1], 0));
+  QLX_HIP(hipStreamWaitEvent(s3, m->ev[1], 0));
   // conv3 (3 tap groups of 3 taps) and conv2 (2 groups of 8 taps): per-sample LDS-staged partials, then
   // one fixed-order reduction of [dW | db] rows straight into the flat gradient (b follows W)
   auto conv_wgrad = [&](const char* name, auto kern, size_t lds, int groups, const bf16* in, const bf16* dzp, size_t zs,
-                        double flops, float* gW) {
-    ProfScope ps(m->prof, name, s, flops);
+                        double flops, float* gW, float* slab, hipStream_t st) {
+    ProfScope ps(m->prof, name, st, flops);
     static bool attr[2] = {false, false};
     bool& a = attr[groups == 3 ? 0 : 1];
     if (!a) {
@@ -467,15 +476,18 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     const int chunks = std::max(1, std::min(B, 256 / groups));
     const int per = (B + chunks - 1) / chunks;
     const int used = (B + per - 1) / per;
-    hipLaunchKernelGGL(kern, dim3(used, groups), dim3(kTrunkThreads), lds, s, in, dzp, B, per, w.slab);
-    hipLaunchKernelGGL(k_slab_reduce<false>, dim3((unsigned)((zs + 63) / 64)), dim3(256), 0, s, w.slab, zs, used, zs, gW);
+    hipLaunchKernelGGL(kern, dim3(used, groups), dim3(kTrunkThreads), lds, st, in, dzp, B, per, slab);
+    hipLaunchKernelGGL(k_slab_reduce<false>, dim3((unsigned)((zs + 63) / 64)), dim3(256), 0, st, slab, zs, used, zs, gW);
   };
   using CW3 = ConvWgradCfg<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>;
   using CW2 = ConvWgradCfg<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>;
+  static_assert(85 * CW3::ZS <= kSlabConv2 && kSlabConv2 + 128 * CW2::ZS <= kSlabConv1 &&
+                    kSlabConv1 + 256 * (size_t)kConv1SlabStride <= kWgradSlabFloats,
+                "slab regions overlap");
   conv_wgrad("conv3_wgrad", k_conv_wgrad<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>, CW3::LDS, 3, w.a2, w.dz3, CW3::ZS,
-             2.0 * B * 49 * 576 * 64, G + var_offset(4));
+             2.0 * B * 49 * 576 * 64, G + var_offset(4), w.slab + kSlabConv3, s2);
   conv_wgrad("conv2_wgrad", k_conv_wgrad<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>, CW2::LDS, 2, w.a1, w.dz2, CW2::ZS,
-             2.0 * B * 81 * 512 * 64, G + var_offset(2));
+             2.0 * B * 81 * 512 * 64, G + var_offset(2), w.slab + kSlabConv2, s3);
   // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames (s2d k order -> HWIO)
   {
     ProfScope ps(m->prof, "conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
@@ -485,11 +497,16 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
       attr = true;
     }
     const int grid = trunk_grid(B);
-    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B, w.slab);
+    float* slab = w.slab + kSlabConv1;
+    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B, slab);
     // s2d-ordered partials -> HWIO kernel gradient (var 0) and bias (var 1) in one pass
-    hipLaunchKernelGGL(k_slab_reduce<true>, dim3((kConv1SlabStride + 63) / 64), dim3(256), 0, s, w.slab,
+    hipLaunchKernelGGL(k_slab_reduce<true>, dim3((kConv1SlabStride + 63) / 64), dim3(256), 0, s, slab,
                        (size_t)kConv1SlabStride, grid, (size_t)kConv1SlabStride, G);
   }
+  QLX_HIP(hipEventRecord(m->ev[2], s2));
+  QLX_HIP(hipEventRecord(m->ev[3], s3));
+  QLX_HIP(hipStreamWaitEvent(s, m->ev[2], 0));
+  QLX_HIP(hipStreamWaitEvent(s, m->ev[3], 0));
   QLX_HIP(hipGetLastError());
 }
 
@@ -562,6 +579,8 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     auto* m = new qlx_model;
     m->device = device;
     QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+    for (auto& st : m->side) QLX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (auto& e : m->ev) QLX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const size_t pb = kNumParams * sizeof(float);
     QLX_HIP(hipMalloc(&m->d_params, pb));
     QLX_HIP(hipMalloc(&m->d_m, pb));
@@ -616,6 +635,10 @@ int32_t qlx_model_destroy(qlx_model* m) {
                     m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->ws};
     for (void* p : ptrs) (void)hipFree(p);
     if (m->own_stream) (void)hipStreamDestroy(m->stream);
+    for (auto& st : m->side)
+      if (st) (void)hipStreamDestroy(st);
+    for (auto& e : m->ev)
+      if (e) (void)hipEventDestroy(e);
     delete m;
   });
 }

@@ -30,11 +30,21 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// MFMA-fragment-major layout of a bf16 [rows][K] operand: element (row, k) of 16-row slice row >> 4 and
+// 32-wide k step k >> 5 sits at lane (k >> 3 & 3) * 16 + (row & 15), element k & 7, so one wave's fragment
+// (16 rows x 32 k) is 1 KB contiguous: ld8(base + frag_offset(slice, s, K) + lane * 8).
+__host__ __device__ constexpr int frag_index(int row, int k, int K) {
+  return (((row >> 4) * (K / 32) + (k >> 5)) * 64 + ((k >> 3) & 3) * 16 + (row & 15)) * 8 + (k & 7);
+}
+
 __device__ __forceinline__ bf16x8 zero8() {
   const uint4 z = {0, 0, 0, 0};
   return __builtin_bit_cast(bf16x8, z);
 }
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p)); }
+__device__ __forceinline__ bf16x8 ldfrag(const bf16* base, int slice, int s, int K, int lane) {
+  return ld8(base + ((slice * (K / 32) + s) * 64 + lane) * 8);
+}
 
 // u8 pixel -> bf16 is exact (integers <= 256 have <= 8 significant bits): the f32's top half.
 __device__ __forceinline__ uint32_t u8pair_bf16(uint32_t w, int s) {

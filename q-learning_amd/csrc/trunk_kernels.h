@@ -153,12 +153,13 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   const int r = lane & 15, g = lane >> 4;
   const int c1 = (wave & 1) * 16, c2 = (wave & 3) * 16;   // the wave's output-channel slice, conv1 / conv2+3
   bf16x8 w1[8], w2[16], w3[18];
+  // fragment-major weight copies (frag_index): each fragment load is 1 KB contiguous per wave
 #pragma unroll
-  for (int s = 0; s < 8; ++s) w1[s] = ld8(wf0 + (c1 + r) * 256 + 32 * s + 8 * g);
+  for (int s = 0; s < 8; ++s) w1[s] = ldfrag(wf0, c1 >> 4, s, 256, lane);
 #pragma unroll
-  for (int s = 0; s < 16; ++s) w2[s] = ld8(wf1 + (c2 + r) * 512 + 32 * s + 8 * g);
+  for (int s = 0; s < 16; ++s) w2[s] = ldfrag(wf1, c2 >> 4, s, 512, lane);
 #pragma unroll
-  for (int s = 0; s < 18; ++s) w3[s] = ld8(wf2 + (c2 + r) * 576 + 32 * s + 8 * g);
+  for (int s = 0; s < 18; ++s) w3[s] = ldfrag(wf2, c2 >> 4, s, 576, lane);
   // biases staged in LDS (12 resident VGPRs would spill the weight fragments; a global load in the epilogue
   // would make the compiler drain vmcnt, i.e. wait for the next sample's frame prefetch)
   __shared__ __attribute__((aligned(16))) float sbias[160];
@@ -346,9 +347,9 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
   const int c3 = (wave & 3) * 16;       // phase A: the wave's 16 channels of dz2
   bf16x8 w3[18], w2[8];                 // A operands (row = lane & 15 of the wave's channel slice)
 #pragma unroll
-  for (int s = 0; s < 18; ++s) w3[s] = ld8(wb2 + (c3 + r) * 576 + 32 * s + 8 * g);
+  for (int s = 0; s < 18; ++s) w3[s] = ldfrag(wb2, c3 >> 4, s, 576, lane);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) w2[s] = ld8(wb1 + (wave * 16 + r) * 256 + 32 * s + 8 * g);
+  for (int s = 0; s < 8; ++s) w2[s] = ldfrag(wb1, wave, s, 256, lane);
   // prefetch: dz3 392 chunks + a2 648 chunks = 1040 -> 3 per thread (staged to LDS); the sample's a1 (the
   // dz1 ReLU mask, 1600 chunks -> 4 per thread) stays in registers in the mapping of the dz1 copy-out.
   // Loads and stores share vmcnt, so a sample's dz1 copy-out is deferred until after the next sample's
