@@ -25,8 +25,10 @@ sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0         # HBM3E spec
-GEMM_SCOPES = ("conv1_fwd", "conv2_fwd", "conv3_fwd", "fc1_fwd", "fc1_wgrad", "fc1_dgrad", "conv3_wgrad",
-               "conv3_dgrad", "conv2_wgrad", "conv2_dgrad", "conv1_wgrad")
+GEMM_SCOPES = ("trunk_fwd", "trunk_fwd_nostore", "trunk_bwd_data", "fc1_fwd", "fc1_bwd", "conv23_wgrad", "conv1_wgrad")
+# profiler scope -> the rocprofv3 kernel symbol it launches (for the committed PMC traffic lookup)
+SCOPE_KERNEL = {"trunk_fwd": "k_trunk_fwdILb1E", "trunk_fwd_nostore": "k_trunk_fwdILb0E", "trunk_bwd_data": "k_trunk_bwd_data",
+                "conv1_wgrad": "k_conv1_wgrad", "conv23_wgrad": "k_conv23_wgrad", "fc1_bwd": "k_gemm_pair"}
 HBM_SCOPES = ("adam", "env_step", "replay_push")
 
 
@@ -92,6 +94,21 @@ def cpu_baseline(sample_steps):
             "grad_updates_per_sec": round(r["updates_per_sec"], 3)}
 
 
+def pmc_traffic(scope):
+    """HBM bytes per launch of the scope's kernel from the newest committed PMC pass (profiles/*/pmc_traffic.json,
+    written by scripts/pmc.sh + scripts/pmc_traffic.py on the same build), or None."""
+    import glob
+    key = SCOPE_KERNEL.get(scope)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    if not key or not files:
+        return None, None
+    data = json.load(open(files[-1]))["kernels"]
+    hits = [v for k, v in data.items() if key in k]
+    if len(hits) != 1:
+        return None, None
+    return hits[0]["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse()
     ctl = Control()
@@ -146,6 +163,7 @@ def main():
         return
     avg_us = us / max(launches, 1)
     achieved = work / us / 1e6 if us > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(dominant)
     line = {
         "metric": METRIC,
         "value": round(env_steps / dt, 1),
@@ -169,7 +187,8 @@ def main():
         "grad_updates_per_sec": round(updates / dt, 2),
         "samples_per_sec": round(updates * B * ctl.world / dt, 1),
         "roofline": {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "avg_us": round(avg_us, 2), "launches": launches,
                      "flops_per_launch": round(work / max(launches, 1))},
         "components": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}

@@ -13,7 +13,8 @@
 // per 32-lane half land in disjoint bank windows at the 80-dword row stride).  Both deliver k in natural
 // order, so the layouts mix freely.  The MFMA computes C^T (B fragment as the A operand): each lane ends
 // with 4 consecutive n of one m, so epilogues move 8 (bf16) or 16 (fp32) bytes per access.
-// grid = (ceil(M/128), ceil(N/128), splits); blockIdx.z covers k in [z*kps, min(K, (z+1)*kps)).
+// A problem has ceil(M/128) x ceil(N/128) x splits tiles (one block each); split z covers k in
+// [z*kps, min(K, (z+1)*kps)).
 // Row-major operands need K % 64 == 0 and kps % 64 == 0.
 // ones_m >= 0 (a multiple of 8, k-major A only) makes A row ones_m all ones, so C row ones_m = sum_k B(n, k)
 // (the bias gradient of a dense layer rides along as one extra output row).
@@ -70,20 +71,20 @@ struct GemmOperand {
   }
 };
 
-// Epilogues: operator()(m, n, v) for C[m][n .. n+3] = v[0..3] (n % 4 == 0, n + 3 < N when n < N)
+// Epilogues: operator()(m, n, v, z) for C[m][n .. n+3] = v[0..3] of k split z (n % 4 == 0, n + 3 < N when n < N)
 struct Epi4Slab {   // split-K partial: slab[z][m][n] (fp32)
   float* slab;
   int ldo;
   size_t zstride;
-  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
-    *reinterpret_cast<f32x4*>(slab + blockIdx.z * zstride + (size_t)m * ldo + n) = v;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int z) const {
+    *reinterpret_cast<f32x4*>(slab + z * zstride + (size_t)m * ldo + n) = v;
   }
 };
 
 struct Epi4StoreF32 {   // out[m][n] = v (fp32)
   float* out;
   int ldo;
-  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int) const {
     *reinterpret_cast<f32x4*>(out + (size_t)m * ldo + n) = v;
   }
 };
@@ -98,7 +99,7 @@ struct Epi4BiasRelu {   // out[m][n] = relu(v + bias[n]) as bf16
   bf16* out;
   const float* bias;
   int ldo;
-  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int) const {
     const float4 b = *reinterpret_cast<const float4*>(bias + n);
     auto r = [](float x) { return x > 0.0f ? x : 0.0f; };
     *reinterpret_cast<uint2*>(out + (size_t)m * ldo + n) = pack4(r(v[0] + b.x), r(v[1] + b.y), r(v[2] + b.z), r(v[3] + b.w));
@@ -109,7 +110,7 @@ struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16
   bf16* out;
   const bf16* act;
   int ldo;
-  __device__ __forceinline__ void operator()(int m, int n, f32x4 v) const {
+  __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int) const {
     const size_t i = (size_t)m * ldo + n;
     typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
     const bf16x4v a = *reinterpret_cast<const bf16x4v*>(act + i);
@@ -118,9 +119,26 @@ struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16
   }
 };
 
+// One problem C[M][N] (+ split z of K); a launch covers ceil(M/128) x ceil(N/128) x splits tiles.
+template <class Epi>
+struct GemmProblem {
+  const bf16* A;
+  int lda;
+  const bf16* B;
+  int ldb;
+  int M, N, K, kps, ones_m;
+  int tiles_m, tiles_n, splits;
+  Epi epi;
+  __host__ __device__ int tiles() const { return tiles_m * tiles_n * splits; }
+};
+
 template <bool AK, bool BK, class Epi>
-__global__ __launch_bounds__(256, 1) void k_gemm(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb,
-                                                 int M, int N, int K, int kps, int ones_m, Epi epi) {
+__device__ __forceinline__ void gemm_tile(const GemmProblem<Epi>& P, int tile) {
+  const bf16* __restrict__ A = P.A;
+  const bf16* __restrict__ Bm = P.B;
+  const int lda = P.lda, ldb = P.ldb, M = P.M, N = P.N, K = P.K, kps = P.kps, ones_m = P.ones_m;
+  const Epi& epi = P.epi;
+  const int bx = tile % P.tiles_m, by = (tile / P.tiles_m) % P.tiles_n, bz = tile / (P.tiles_m * P.tiles_n);
   using C = GemmCfg;
   constexpr int KT = C::KT, IMG = C::IMG, CH = C::CH;
   using OA = GemmOperand<AK>;
@@ -128,8 +146,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm(const bf16* __restrict__ A, int
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
-  const int kb = blockIdx.z * kps, ke = min(K, kb + kps);
+  const int m0 = bx * C::BM, n0 = by * C::BN;
+  const int kb = bz * kps, ke = min(K, kb + kps);
   uint4 ra[CH], rb[CH];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -190,9 +208,24 @@ __global__ __launch_bounds__(256, 1) void k_gemm(const bf16* __restrict__ A, int
       for (int u = 0; u < 4; ++u) {
         const int n = n0 + wn * 64 + j * 32 + 8 * u + 4 * h;
         if (m < M && n < N)
-          epi(m, n, f32x4{acc[t][j][4 * u], acc[t][j][4 * u + 1], acc[t][j][4 * u + 2], acc[t][j][4 * u + 3]});
+          epi(m, n, f32x4{acc[t][j][4 * u], acc[t][j][4 * u + 1], acc[t][j][4 * u + 2], acc[t][j][4 * u + 3]}, bz);
       }
     }
+}
+
+// single problem: one block per tile
+template <bool AK, bool BK, class Epi>
+__global__ __launch_bounds__(256, 1) void k_gemm(GemmProblem<Epi> P) {
+  gemm_tile<AK, BK>(P, blockIdx.x);
+}
+
+// two independent problems in one launch (blocks [0, P1.tiles()) -> P1, the rest -> P2): concurrency without
+// cross-stream events, whose dependency latency costs more than a small kernel
+template <bool AK1, bool BK1, class E1, bool AK2, bool BK2, class E2>
+__global__ __launch_bounds__(256, 1) void k_gemm_pair(GemmProblem<E1> P1, GemmProblem<E2> P2) {
+  const int t = blockIdx.x;
+  if (t < P1.tiles()) gemm_tile<AK1, BK1>(P1, t);
+  else gemm_tile<AK2, BK2>(P2, t - P1.tiles());
 }
 
 }  // namespace qn

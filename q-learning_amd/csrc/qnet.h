@@ -12,7 +12,7 @@ namespace qlx {
 constexpr int kNumVars = 10;
 constexpr int64_t kNumParams = 1685667;   // sum of the 10 Keras variables (variables.index shapes)
 constexpr int kFc1Split = 7;              // split-K of the 3136-deep dense layer (14 MFMA k-steps each)
-// conv weight-gradient partial slabs; conv3 / conv2 / conv1 run concurrently, each in its own region
+// conv weight-gradient partial slabs, one region per layer (conv3 and conv2 share a launch)
 constexpr size_t kSlabConv3 = 0, kSlabConv2 = (size_t)3200 * 1024, kSlabConv1 = (size_t)7424 * 1024;
 constexpr size_t kWgradSlabFloats = (size_t)9600 * 1024;
 constexpr size_t kBiasSlabFloats = 256 * 512;
@@ -38,8 +38,6 @@ struct qlx_model {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = true;
-  hipStream_t side[2] = {nullptr, nullptr};   // concurrent weight-gradient branches of model_backward
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float* d_params = nullptr;   // fp32 master weights, Keras layouts, variables concatenated
   float* d_m = nullptr;
   float* d_v = nullptr;

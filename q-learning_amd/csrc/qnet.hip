@@ -360,6 +360,15 @@ static void set_lds_attr(Kern k, size_t bytes) {
   QLX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
 }
 
+template <class Epi>
+static GemmProblem<Epi> gemm_problem(bool row_major_operand, const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K,
+                                     int splits, Epi epi, int ones_m = -1) {
+  const int kps = (K + splits - 1) / splits;
+  QLX_CHECK(!row_major_operand || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID,
+            "k_gemm: row-major operands need K and K/splits multiples of 64");
+  return GemmProblem<Epi>{A, lda, Bm, ldb, M, N, K, kps, ones_m, (M + 127) / 128, (N + 127) / 128, splits, epi};
+}
+
 template <bool AK, bool BK, class Epi>
 static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K, int splits, Epi epi, hipStream_t s,
                         int ones_m = -1) {
@@ -368,11 +377,8 @@ static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, 
     set_lds_attr(k_gemm<AK, BK, Epi>, GemmCfg::LDS);
     attr = true;
   }
-  const int kps = (K + splits - 1) / splits;
-  QLX_CHECK((AK && BK) || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID,
-            "k_gemm: row-major operands need K and K/splits multiples of 64");
-  const dim3 grid((M + 127) / 128, (N + 127) / 128, splits);
-  hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), grid, dim3(256), GemmCfg::LDS, s, A, lda, Bm, ldb, M, N, K, kps, ones_m, epi);
+  const GemmProblem<Epi> P = gemm_problem(!(AK && BK), A, lda, Bm, ldb, M, N, K, splits, epi, ones_m);
+  hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), dim3(P.tiles()), dim3(256), GemmCfg::LDS, s, P);
 }
 
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts) {
@@ -380,7 +386,9 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
   m->last_batch = B;
   const float* p = m->d_params;
   {  // conv1 -> conv2 -> conv3 fused per sample (trunk_kernels.h)
-    ProfScope ps(m->prof, "trunk_fwd", s, 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576));
+    // scope per role so each maps to one kernel instantiation (trunk_fwd = online pass with stored activations)
+    ProfScope ps(m->prof, store_acts ? "trunk_fwd" : "trunk_fwd_nostore", s,
+                 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576));
     static bool attr = false;
     if (!attr) {
       set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
@@ -432,21 +440,20 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     hipLaunchKernelGGL(k_fc2_wgrad, dim3(514), dim3(256), 0, s, w.a4, actions, w.gs, w.hs, B, G + var_offset(8),
                        G + var_offset(9), loss_dev);
   }
-  // Branches (all only read the forward activations / dz chain and write disjoint gradient ranges):
-  //   main  : fc1 dgrad -> backward data (dz2, dz1) -> conv1 wgrad
-  //   side 0: fc1 wgrad (100 blocks: fills the CUs the dgrad chain leaves idle) -> conv3 wgrad
-  //   side 1: conv2 wgrad
-  // joined on the main stream before returning (norms + Adam follow on it).
-  hipStream_t s2 = m->side[0], s3 = m->side[1];
-  QLX_HIP(hipEventRecord(m->ev[0], s));
-  QLX_HIP(hipStreamWaitEvent(s2, m->ev[0], 0));
-  {  // fc1: dW3 = a3^T dz4 and db3 (row 3136 = the all-ones row; db3 follows dW3 [3136][512] in the flat gradient)
-    ProfScope ps(m->prof, "fc1_wgrad", s2, 2.0 * B * 512 * 3136);
-    launch_gemm<true, true>(w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, s2, 3136);
-  }
-  {  // dz3 = (dz4 W3^T) * (a3 > 0)
-    ProfScope ps(m->prof, "fc1_dgrad", s, 2.0 * B * 512 * 3136);
-    launch_gemm<false, false>(w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136}, s);
+  // fc1 in one launch of two independent GEMMs (both only read dz4 / a3):
+  //   dW3 = a3^T dz4 and db3 (row 3136 = the all-ones row; db3 follows dW3 [3136][512] in the flat gradient)
+  //   dz3 = (dz4 W3^T) * (a3 > 0)
+  {
+    ProfScope ps(m->prof, "fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
+    const auto Pw = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, 3136);
+    const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
+    auto kern = k_gemm_pair<true, true, Epi4StoreF32, false, false, Epi4ReluMask>;
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(kern, GemmCfg::LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(Pw.tiles() + Pd.tiles()), dim3(256), GemmCfg::LDS, s, Pw, Pd);
   }
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
@@ -459,54 +466,61 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     hipLaunchKernelGGL(k_trunk_bwd_data, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkBwdLds, s, w.dz3, w.a2, w.a1, B, m->wb2,
                        m->wb1, w.dz2, w.dz1);
   }
-  QLX_HIP(hipEventRecord(m->ev[1], s));
-  QLX_HIP(hipStreamWaitEvent(s2, m->ev[1], 0));
-  QLX_HIP(hipStreamWaitEvent(s3, m->ev[1], 0));
-  // conv3 (3 tap groups of 3 taps) and conv2 (2 groups of 8 taps): per-sample LDS-staged partials, then
-  // one fixed-order reduction of [dW | db] rows straight into the flat gradient (b follows W)
-  auto conv_wgrad = [&](const char* name, auto kern, size_t lds, int groups, const bf16* in, const bf16* dzp, size_t zs,
-                        double flops, float* gW, float* slab, hipStream_t st) {
-    ProfScope ps(m->prof, name, st, flops);
-    static bool attr[2] = {false, false};
-    bool& a = attr[groups == 3 ? 0 : 1];
-    if (!a) {
-      set_lds_attr(kern, lds);
-      a = true;
-    }
-    const int chunks = std::max(1, std::min(B, 256 / groups));
-    const int per = (B + chunks - 1) / chunks;
-    const int used = (B + per - 1) / per;
-    hipLaunchKernelGGL(kern, dim3(used, groups), dim3(kTrunkThreads), lds, st, in, dzp, B, per, slab);
-    hipLaunchKernelGGL(k_slab_reduce<false>, dim3((unsigned)((zs + 63) / 64)), dim3(256), 0, st, slab, zs, used, zs, gW);
-  };
+  // conv3 (3 tap groups of 3 taps) + conv2 (2 groups of 8 taps) weight gradients in one launch, then
+  // conv1's; per-block fp32 partials of [dW | db] rows, reduced in fixed order by one grouped launch
+  // straight into the flat gradient (each layer's b follows its W; conv1 goes s2d -> HWIO)
   using CW3 = ConvWgradCfg<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>;
   using CW2 = ConvWgradCfg<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>;
   static_assert(85 * CW3::ZS <= kSlabConv2 && kSlabConv2 + 128 * CW2::ZS <= kSlabConv1 &&
                     kSlabConv1 + 256 * (size_t)kConv1SlabStride <= kWgradSlabFloats,
                 "slab regions overlap");
-  conv_wgrad("conv3_wgrad", k_conv_wgrad<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>, CW3::LDS, 3, w.a2, w.dz3, CW3::ZS,
-             2.0 * B * 49 * 576 * 64, G + var_offset(4), w.slab + kSlabConv3, s2);
-  conv_wgrad("conv2_wgrad", k_conv_wgrad<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>, CW2::LDS, 2, w.a1, w.dz2, CW2::ZS,
-             2.0 * B * 81 * 512 * 64, G + var_offset(2), w.slab + kSlabConv2, s3);
-  // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames (s2d k order -> HWIO)
+  auto chunking = [&](int groups, int& per) {
+    const int chunks = std::max(1, std::min(B, 256 / groups));
+    per = (B + chunks - 1) / chunks;
+    return (B + per - 1) / per;
+  };
+  int per3 = 0, per2 = 0;
+  const int used3 = chunking(3, per3), used2 = chunking(2, per2);
   {
+    ProfScope ps(m->prof, "conv23_wgrad", s, 2.0 * B * (49.0 * 576 * 64 + 81.0 * 512 * 64));
+    constexpr size_t lds = std::max(CW3::LDS, CW2::LDS);
+    auto kern = k_conv23_wgrad;
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(kern, lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(used3 * 3 + used2 * 2), dim3(kTrunkThreads), lds, s, w.a2, w.dz3, per3, used3,
+                       w.slab + kSlabConv3, w.a1, w.dz2, per2, used2, w.slab + kSlabConv2, B);
+  }
+  const int grid1 = trunk_grid(B);
+  {  // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames
     ProfScope ps(m->prof, "conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
     static bool attr = false;
     if (!attr) {
       set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
       attr = true;
     }
-    const int grid = trunk_grid(B);
-    float* slab = w.slab + kSlabConv1;
-    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B, slab);
-    // s2d-ordered partials -> HWIO kernel gradient (var 0) and bias (var 1) in one pass
-    hipLaunchKernelGGL(k_slab_reduce<true>, dim3((kConv1SlabStride + 63) / 64), dim3(256), 0, s, slab,
-                       (size_t)kConv1SlabStride, grid, (size_t)kConv1SlabStride, G);
+    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid1), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B,
+                       w.slab + kSlabConv1);
   }
-  QLX_HIP(hipEventRecord(m->ev[2], s2));
-  QLX_HIP(hipEventRecord(m->ev[3], s3));
-  QLX_HIP(hipStreamWaitEvent(s, m->ev[2], 0));
-  QLX_HIP(hipStreamWaitEvent(s, m->ev[3], 0));
+  {
+    ProfScope ps(m->prof, "wgrad_reduce", s);
+    SlabSeg segs[3] = {
+        {w.slab + kSlabConv3, CW3::ZS, used3, CW3::ZS, G + var_offset(4), 0},
+        {w.slab + kSlabConv2, CW2::ZS, used2, CW2::ZS, G + var_offset(2), 0},
+        {w.slab + kSlabConv1, (size_t)kConv1SlabStride, grid1, (size_t)kConv1SlabStride, G, 1},
+    };
+    SlabSegs3 a;
+    int blocks = 0;
+    for (int i = 0; i < 3; ++i) {
+      a.seg[i] = segs[i];
+      a.first_block[i] = blocks;
+      blocks += (int)((segs[i].count + 63) / 64);
+    }
+    a.first_block[3] = blocks;
+    hipLaunchKernelGGL(k_slab_reduce3, dim3(blocks), dim3(256), 0, s, a);
+  }
   QLX_HIP(hipGetLastError());
 }
 
@@ -579,8 +593,6 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     auto* m = new qlx_model;
     m->device = device;
     QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
-    for (auto& st : m->side) QLX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    for (auto& e : m->ev) QLX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const size_t pb = kNumParams * sizeof(float);
     QLX_HIP(hipMalloc(&m->d_params, pb));
     QLX_HIP(hipMalloc(&m->d_m, pb));
@@ -635,10 +647,6 @@ int32_t qlx_model_destroy(qlx_model* m) {
                     m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->ws};
     for (void* p : ptrs) (void)hipFree(p);
     if (m->own_stream) (void)hipStreamDestroy(m->stream);
-    for (auto& st : m->side)
-      if (st) (void)hipStreamDestroy(st);
-    for (auto& e : m->ev)
-      if (e) (void)hipEventDestroy(e);
     delete m;
   });
 }

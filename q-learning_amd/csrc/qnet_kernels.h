@@ -74,12 +74,11 @@ __device__ __forceinline__ int conv1_hwio_from_s2d(int i) {   // i = k * 32 + oc
   return (((4 * ii + dx) * 8 + 4 * j + dy) * 4 + c) * 32 + oc;
 }
 
-template <bool CONV1 = false>
-__global__ __launch_bounds__(256) void k_slab_reduce(const float* slab, size_t zstride, int chunks, size_t count,
-                                                     float* out) {
+__device__ __forceinline__ void slab_reduce_block(const float* slab, size_t zstride, int chunks, size_t count, float* out,
+                                                  bool conv1, int blk) {
   __shared__ float part[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t i = (size_t)blockIdx.x * 64 + lane;
+  const size_t i = (size_t)blk * 64 + lane;
   const int q = (chunks + 3) / 4, c0 = wave * q, c1 = min(chunks, c0 + q);
   float s = 0.0f;
   if (i < count) {
@@ -96,9 +95,35 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* slab, size_t z
   part[wave][lane] = s;
   __syncthreads();
   if (wave == 0 && i < count) {
-    const size_t d = CONV1 && i < 8192 ? (size_t)conv1_hwio_from_s2d((int)i) : i;
+    const size_t d = conv1 && i < 8192 ? (size_t)conv1_hwio_from_s2d((int)i) : i;
     out[d] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
   }
+}
+
+template <bool CONV1 = false>
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* slab, size_t zstride, int chunks, size_t count,
+                                                     float* out) {
+  slab_reduce_block(slab, zstride, chunks, count, out, CONV1, blockIdx.x);
+}
+
+// three independent slab reductions in one launch (segment i owns blocks [first_block[i], first_block[i+1]))
+struct SlabSeg {
+  const float* slab;
+  size_t zstride;
+  int chunks;
+  size_t count;
+  float* out;
+  int conv1;
+};
+struct SlabSegs3 {
+  SlabSeg seg[3];
+  int first_block[4];
+};
+__global__ __launch_bounds__(256) void k_slab_reduce3(SlabSegs3 a) {
+  const int b = blockIdx.x;
+  const int i = b < a.first_block[1] ? 0 : (b < a.first_block[2] ? 1 : 2);
+  const SlabSeg& g = a.seg[i];
+  slab_reduce_block(g.slab, g.zstride, g.chunks, g.count, g.out, g.conv1 != 0, b - a.first_block[i]);
 }
 
 __global__ void k_slab_reduce_bias_relu(const float* slab, size_t zstride, int chunks, int M, int N,

@@ -477,6 +477,7 @@ namespace qn {
 // supplies the LDS row of its own im2col position, so the im2col is never materialised.  Wave w owns
 // KTW k-tiles (16 rows of dW each) x NTW of the four 16-column n-tiles.
 // Output: slab[chunk][TAPS*C*64 + 64] rows of [dW partial | db partial] (db from tap group 0 only).
+// Launched as k_conv23_wgrad (conv3 and conv2 blocks in one grid).
 template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW>
 struct ConvWgradCfg {
   static constexpr int M = OH * OW, MP = (M + 31) / 32 * 32;   // positions, padded to the 32-row m-step
@@ -494,8 +495,8 @@ struct ConvWgradCfg {
 };
 
 template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW>
-__global__ __launch_bounds__(kTrunkThreads, 1) void k_conv_wgrad(const bf16* __restrict__ in, const bf16* __restrict__ dz,
-                                                                 int B, int per_chunk, float* slab) {
+__device__ __forceinline__ void conv_wgrad_body(const bf16* __restrict__ in, const bf16* __restrict__ dz, int B, int per_chunk,
+                                                float* slab, int chunk, int tg) {
   using Cf = ConvWgradCfg<IH, IW, C, KS, S, OH, OW, TG, KTW, NTW>;
   constexpr int M = Cf::M, MP = Cf::MP, XS = Cf::XS, DS = Cf::DS;
   constexpr int CHX = Cf::CHX, CHD = Cf::CHD, PF = Cf::PF;
@@ -504,8 +505,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv_wgrad(const bf16* __r
   bf16* DZ = lds + Cf::LX;
   const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int tg = blockIdx.y;                       // tap group
-  const int b0 = blockIdx.x * per_chunk, b1 = min(B, b0 + per_chunk);
+  const int b0 = chunk * per_chunk, b1 = min(B, b0 + per_chunk);
   // wave's tiles: k tiles kt0 .. kt0+KTW-1, n tiles nt0 .. nt0+NTW-1
   constexpr int NGROUPS = 4 / NTW;                  // waves sharing a k-tile set
   const int kt0 = (wave / NGROUPS) * KTW, nt0 = (wave % NGROUPS) * NTW;
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv_wgrad(const bf16* __r
       for (int m = brg; m < M; m += 8) bsum += (float)DZ[m * DS + bn];
   }
   // D tile (a, c): row k = (tg * KTILES + kt0 + a) * 16 + 4g + e, col n = (nt0 + c) * 16 + li
-  float* out = slab + (size_t)blockIdx.x * Cf::ZS;
+  float* out = slab + (size_t)chunk * Cf::ZS;
 #pragma unroll
   for (int a = 0; a < KTW; ++a)
 #pragma unroll
@@ -595,6 +595,20 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv_wgrad(const bf16* __r
       for (int i = 0; i < 8; ++i) sb += bred[i][tid];
       out[(size_t)Cf::TAPS * C * 64 + tid] = sb;
     }
+  }
+}
+
+// conv3 (blocks [0, 3*used3): chunk t % used3, tap group t / used3) and conv2 (the rest) in one launch
+__global__ __launch_bounds__(kTrunkThreads, 1) void k_conv23_wgrad(const bf16* __restrict__ a2, const bf16* __restrict__ dz3,
+                                                                   int per3, int used3, float* slab3, const bf16* __restrict__ a1,
+                                                                   const bf16* __restrict__ dz2, int per2, int used2,
+                                                                   float* slab2, int B) {
+  int t = blockIdx.x;
+  if (t < 3 * used3) {
+    conv_wgrad_body<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>(a2, dz3, B, per3, slab3, t % used3, t / used3);
+  } else {
+    t -= 3 * used3;
+    conv_wgrad_body<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>(a1, dz2, B, per2, slab2, t % used2, t / used2);
   }
 }
 

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-RE="${QLX_PMC_REGEX:-k_trunk|k_conv1_wgrad|k_igemm|k_wgrad|k_adam|k_slab}"
+RE="${QLX_PMC_REGEX:-k_trunk|k_conv|k_gemm|k_adam|k_slab|k_replay|k_env}"
 ARGS="--steps 2 --warmup 12 --cpu-sample 0 --profile-steps 1"
 run() {
   local name=$1; shift
@@ -16,4 +16,5 @@ run sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST
 run mix SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE || exit 1
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
+python3 scripts/pmc_traffic.py gpurun_out/pmc > gpurun_out/pmc/traffic.log 2>&1
 exit 0
