@@ -64,12 +64,15 @@ struct Book {
 };
 
 // One wave, envs in order: ep_reward += r; an env whose episode ended (done, or max_steps_per_episode
-// steps) pushes its reward into the FIFO of episode rewards, refreshes running_reward once
-// episode_count >= hist cap (sequential f32 sum, oldest first), counts the episode and is marked for reset.
+// steps) pushes its reward into the FIFO of episode rewards, counts the episode and is marked for reset.
+// running_reward is refreshed (sequential f32 sum, oldest first) by every ending with episode_count >= hist
+// cap; only the last such refresh of the step survives and it sums the final FIFO, so it runs once.
 __global__ __launch_bounds__(64) void k_episode_book(uint32_t n, const float* rewards, const uint8_t* dones,
                                                      const uint32_t* ep_steps, uint64_t max_steps, float* ep_reward,
                                                      float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask) {
   const int lane = threadIdx.x;
+  Book b = *book;
+  bool refresh = false;
   for (uint32_t base = 0; base < n; base += 64) {
     const uint32_t e = base + lane;
     bool end = false;
@@ -81,28 +84,28 @@ __global__ __launch_bounds__(64) void k_episode_book(uint32_t n, const float* re
       reset_mask[e] = end ? 1 : 0;
     }
     unsigned long long bal = __ballot(end);
-    while (bal) {
+    while (bal) {   // uniform loop: every lane tracks the same Book
       const int l = __builtin_ctzll(bal);
       bal &= bal - 1;
       const float v = __shfl(er, l);
-      if (lane == 0) {
-        Book b = *book;
-        if (b.hist_len < hist_cap) {
-          hist[(b.hist_head + b.hist_len) % hist_cap] = v;
-          b.hist_len += 1;
-        } else {
-          hist[b.hist_head] = v;
-          b.hist_head = (b.hist_head + 1) % hist_cap;
-        }
-        if (b.episode_count >= hist_cap) {
-          float s = 0.0f;
-          for (uint32_t i = 0; i < b.hist_len; ++i) s += hist[(b.hist_head + i) % hist_cap];
-          b.running_reward = s / (float)b.hist_len;
-        }
-        b.episode_count += 1;
-        *book = b;
+      if (b.hist_len < hist_cap) {
+        if (lane == 0) hist[(b.hist_head + b.hist_len) % hist_cap] = v;
+        b.hist_len += 1;
+      } else {
+        if (lane == 0) hist[b.hist_head] = v;
+        b.hist_head = (b.hist_head + 1) % hist_cap;
       }
+      refresh = refresh || b.episode_count >= hist_cap;
+      b.episode_count += 1;
     }
+  }
+  if (lane == 0) {
+    if (refresh) {
+      float s = 0.0f;
+      for (uint32_t i = 0; i < b.hist_len; ++i) s += hist[(b.hist_head + i) % hist_cap];
+      b.running_reward = s / (float)b.hist_len;
+    }
+    *book = b;
   }
 }
 

@@ -27,6 +27,7 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float *gs = nullptr, *hs = nullptr, *y = nullptr, *rew = nullptr;
   uint8_t *act = nullptr, *argmax = nullptr, *done = nullptr;
   float* fc1slab = nullptr;
+  int a4_splits = 0;                  // > 0: a4 still pending as that many split-K fc1 partials in fc1slab
   float* slab = nullptr;
   float* bslab = nullptr;
   float* loss = nullptr;
@@ -61,6 +62,13 @@ struct qlx_model {
 namespace qlx {
 struct Fc2Args {
   const __bf16* a4;          // [B][512]
+  // pending split-K fc1 partials (splits > 0): the head finishes a4 = relu(sum_z slab[z] + b3) in fixed z order
+  // and writes it to a4_out, so no separate reduction launch runs
+  const float* slab;
+  size_t zstride;
+  int splits;
+  const float* b3;
+  __bf16* a4_out;
   const float* w4;         // [512][3] master
   const float* b4;         // [3]
   int B;
@@ -75,6 +83,8 @@ struct Fc2Args {
   float* gsample;          // training head: dloss/dq_a per sample
   float* hsample;          // training head: per-sample Huber value
 };
+// fc2 kernel arguments for the model's last forward; consumes pending fc1 partials (the fc2 launch that
+// follows materialises a4)
 Fc2Args fc2_args(qlx_model* m, int B);
 void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s);
 void model_workspace(qlx_model* m, int B);

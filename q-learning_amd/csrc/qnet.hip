@@ -108,13 +108,35 @@ __global__ void k_frame_table(const uint8_t* frames, int B, const uint8_t** tabl
 //   (the training head with Huber + dq lives in k_fc2_train)
 
 
+// this lane's 8 a4 values of sample b (k = 8 lane + e): straight from a4, or finished from the fc1 split-K
+// partials (sum over z in order, + b3, ReLU, bf16 - the values k_slab_reduce_bias_relu would store)
+__device__ __forceinline__ bf16x8 fc2_load_a4(const Fc2Args& A, int b, int lane) {
+  if (A.splits == 0) return ld8(A.a4 + (size_t)b * 512 + lane * 8);
+  const size_t i = (size_t)b * 512 + lane * 8;
+  float4 s0 = {0.0f, 0.0f, 0.0f, 0.0f}, s1 = s0;
+  for (int z = 0; z < A.splits; ++z) {
+    const float4 u0 = *reinterpret_cast<const float4*>(A.slab + z * A.zstride + i);
+    const float4 u1 = *reinterpret_cast<const float4*>(A.slab + z * A.zstride + i + 4);
+    s0.x += u0.x; s0.y += u0.y; s0.z += u0.z; s0.w += u0.w;
+    s1.x += u1.x; s1.y += u1.y; s1.z += u1.z; s1.w += u1.w;
+  }
+  const float4 c0 = *reinterpret_cast<const float4*>(A.b3 + lane * 8);
+  const float4 c1 = *reinterpret_cast<const float4*>(A.b3 + lane * 8 + 4);
+  const float t[8] = {s0.x + c0.x, s0.y + c0.y, s0.z + c0.z, s0.w + c0.w, s1.x + c1.x, s1.y + c1.y, s1.z + c1.z, s1.w + c1.w};
+  bf16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (bf16)(t[e] > 0.0f ? t[e] : 0.0f);
+  *reinterpret_cast<bf16x8*>(A.a4_out + i) = v;
+  return v;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_fc2(Fc2Args A) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= A.B) return;
   float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-  const bf16x8 v = ld8(A.a4 + (size_t)b * 512 + lane * 8);
+  const bf16x8 v = fc2_load_a4(A, b, lane);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float x = (float)v[e];
@@ -153,7 +175,7 @@ __global__ __launch_bounds__(256) void k_fc2_train(Fc2Args A, bf16* dz4) {
   const int lane = threadIdx.x & 63;
   if (b >= A.B) return;
   float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-  const bf16x8 v = ld8(A.a4 + (size_t)b * 512 + lane * 8);
+  const bf16x8 v = fc2_load_a4(A, b, lane);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float x = (float)v[e];
@@ -184,32 +206,79 @@ __global__ __launch_bounds__(256) void k_fc2_train(Fc2Args A, bf16* dz4) {
   *reinterpret_cast<bf16x8*>(dz4 + (size_t)b * 512 + lane * 8) = d;
 }
 
-// dW4[k][a] = sum_b a4[b][k] g_b [a_b == a] (block k < 512); db4[a] = sum_b g_b [a_b == a] (block 512);
-// loss = sum_b h_b / B (block 513).  Fixed strided + tree order: deterministic.
-__global__ __launch_bounds__(256) void k_fc2_wgrad(const bf16* a4, const uint8_t* actions, const float* gs, const float* hs,
-                                                   int B, float* g_w4, float* g_b4, float* loss) {
-  __shared__ float red[3][256];
-  const int k = blockIdx.x;
-  float s[3] = {0.0f, 0.0f, 0.0f};
-  if (k == 513) {
-    for (int b = threadIdx.x; b < B; b += 256) s[0] += hs[b];
+// dW4[k][a] = sum_b a4[b][k] g_b [a_b == a]: block j < 64 owns k = 8j .. 8j+7 and reads those 16 bytes of every
+// a4 row once; block 64 sums db4[a] = sum_b g_b [a_b == a] and the loss = sum_b h_b / B.  Per-thread strided
+// sums, an xor butterfly per wave, then the 4 wave sums in order: deterministic.  Runs as trailing blocks of
+// the fc1 backward launch (k_fc1_bwd), overlapping its GEMM tiles.
+struct Fc2WgradArgs {
+  const bf16* a4;
+  const uint8_t* actions;
+  const float* gs;
+  const float* hs;
+  int B;
+  float* g_w4;
+  float* g_b4;
+  float* loss;
+};
+constexpr int kFc2WgradBlocks = 65;
+
+__device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, float* red /* LDS [4][24] */) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float s[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) s[i] = 0.0f;
+  if (j == 64) {
+    for (int b = tid; b < A.B; b += 256) {
+      const int a = A.actions[b];
+      const float g = A.gs[b];
+      s[0] += a == 0 ? g : 0.0f;
+      s[1] += a == 1 ? g : 0.0f;
+      s[2] += a == 2 ? g : 0.0f;
+      s[3] += A.hs[b];
+    }
   } else {
-    for (int b = threadIdx.x; b < B; b += 256) {
-      const float x = k < 512 ? (float)a4[(size_t)b * 512 + k] : 1.0f;
-      s[actions[b]] += x * gs[b];
+    const int k0 = j * 8;
+    for (int b = tid; b < A.B; b += 256) {
+      const bf16x8 x = ld8(A.a4 + (size_t)b * 512 + k0);
+      const int a = A.actions[b];
+      const float g = A.gs[b];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = (float)x[e] * g;
+        s[e * 3 + 0] += a == 0 ? v : 0.0f;
+        s[e * 3 + 1] += a == 1 ? v : 0.0f;
+        s[e * 3 + 2] += a == 2 ? v : 0.0f;
+      }
     }
   }
-  for (int j = 0; j < 3; ++j) red[j][threadIdx.x] = s[j];
+#pragma unroll
+  for (int i = 0; i < 24; ++i)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s[i] += __shfl_xor(s[i], off);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 24; ++i) red[wave * 24 + i] = s[i];
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w)
-      for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + w];
-    __syncthreads();
+  if (tid < 24) {
+    const float t = ((red[tid] + red[24 + tid]) + red[48 + tid]) + red[72 + tid];
+    if (j == 64) {
+      if (tid < 3) A.g_b4[tid] = t;
+      else if (tid == 3) *A.loss = t / (float)A.B;
+    } else {
+      A.g_w4[j * 24 + tid] = t;   // [k][a] with k = 8 j + tid / 3
+    }
   }
-  if (threadIdx.x < 3) {
-    if (k < 512) g_w4[k * 3 + threadIdx.x] = red[threadIdx.x][0];
-    else if (k == 512) g_b4[threadIdx.x] = red[threadIdx.x][0];
-    else if (threadIdx.x == 0) *loss = red[0][0] / (float)B;
+}
+
+// fc1 backward (dW3 + db3 tiles, then dz3 tiles) and the dense-3 weight gradient in one launch
+template <class E1, class E2>
+__global__ __launch_bounds__(256, 2) void k_fc1_bwd(GemmProblem<E1> Pw, GemmProblem<E2> Pd, Fc2WgradArgs F) {
+  const int t = blockIdx.x, tg = Pw.tiles() + Pd.tiles();
+  if (t < tg) {
+    gemm_pair_block<true, true, E1, false, false, E2>(Pw, Pd, t);
+  } else {
+    extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+    fc2_wgrad_block(F, t - tg, reinterpret_cast<float*>(lds));
   }
 }
 
@@ -283,6 +352,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     }
   }
   __syncthreads();
+  // one parameter per thread and grid-stride step (measured faster than 16-byte groups on this kernel)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.count; i += (int64_t)gridDim.x * blockDim.x) {
     int var = 0;
     while (i >= offs[var + 1]) ++var;
@@ -362,23 +432,24 @@ static void set_lds_attr(Kern k, size_t bytes) {
 
 template <class Epi>
 static GemmProblem<Epi> gemm_problem(bool row_major_operand, const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K,
-                                     int splits, Epi epi, int ones_m = -1) {
+                                     int splits, Epi epi, int ones_m = -1, bool n_fastest = false, bool remap = false) {
   const int kps = (K + splits - 1) / splits;
   QLX_CHECK(!row_major_operand || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID,
             "k_gemm: row-major operands need K and K/splits multiples of 64");
-  return GemmProblem<Epi>{A, lda, Bm, ldb, M, N, K, kps, ones_m, (M + 127) / 128, (N + 127) / 128, splits, epi};
+  return GemmProblem<Epi>{A, lda, Bm, ldb, M, N, K, kps, ones_m, (M + 127) / 128, (N + 127) / 128, splits, n_fastest ? 1 : 0,
+                          remap ? 1 : 0, epi};
 }
 
 template <bool AK, bool BK, class Epi>
 static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K, int splits, Epi epi, hipStream_t s,
-                        int ones_m = -1) {
+                        int ones_m = -1, bool remap = false) {
   static bool attr = false;
   if (!attr) {
     set_lds_attr(k_gemm<AK, BK, Epi>, GemmCfg::LDS);
     attr = true;
   }
-  const GemmProblem<Epi> P = gemm_problem(!(AK && BK), A, lda, Bm, ldb, M, N, K, splits, epi, ones_m);
-  hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), dim3(P.tiles()), dim3(256), GemmCfg::LDS, s, P);
+  const GemmProblem<Epi> P = gemm_problem(!(AK && BK), A, lda, Bm, ldb, M, N, K, splits, epi, ones_m, false, remap);
+  hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), dim3(xcd_grid(P.tiles())), dim3(256), GemmCfg::LDS, s, P);
 }
 
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts) {
@@ -404,10 +475,12 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
     if (B >= 64 * 128) {
       launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, 1, Epi4BiasRelu{w.a4, p + var_offset(7), 512}, s);
+      w.a4_splits = 0;
     } else {
-      launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, kFc1Split, Epi4Slab{w.fc1slab, 512, (size_t)B * 512}, s);
-      hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, s, w.fc1slab,
-                         (size_t)B * 512, kFc1Split, B, 512, p + var_offset(7), w.a4);
+      // XCD-grouped order: each XCD works on one k split (its a3 / W3 slices land in that XCD's L2 once)
+      launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, kFc1Split, Epi4Slab{w.fc1slab, 512, (size_t)B * 512}, s, -1,
+                               true);
+      w.a4_splits = kFc1Split;   // bias + ReLU + the fixed-order sum happen in the fc2 head that follows
     }
   }
   QLX_HIP(hipGetLastError());
@@ -420,6 +493,12 @@ Fc2Args fc2_args(qlx_model* m, int B) {
   a.b4 = m->d_params + var_offset(9);
   a.B = B;
   a.q = m->w.q;
+  a.slab = m->w.fc1slab;
+  a.zstride = (size_t)B * 512;
+  a.splits = m->w.a4_splits;
+  a.b3 = m->d_params + var_offset(7);
+  a.a4_out = m->w.a4;
+  m->w.a4_splits = 0;
   return a;
 }
 
@@ -429,7 +508,7 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
                     hipStream_t s) {
   ModelWs& w = m->w;
   float* G = m->d_grads;
-  {  // head: q, Huber, dz4 (one wave per sample); dW4, db4 and the loss (fixed-order block reductions)
+  {  // head: q, Huber, dz4 (one wave per sample)
     ProfScope ps(m->prof, "fc2_head", s);
     Fc2Args a = fc2_args(m, B);
     a.actions = actions;
@@ -437,23 +516,22 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     a.gsample = w.gs;
     a.hsample = w.hs;
     hipLaunchKernelGGL(k_fc2_train, dim3((B + 3) / 4), dim3(256), 0, s, a, w.dz4);
-    hipLaunchKernelGGL(k_fc2_wgrad, dim3(514), dim3(256), 0, s, w.a4, actions, w.gs, w.hs, B, G + var_offset(8),
-                       G + var_offset(9), loss_dev);
   }
-  // fc1 in one launch of two independent GEMMs (both only read dz4 / a3):
+  // fc1 in one launch of two independent GEMMs (both only read dz4 / a3), plus dW4 / db4 / loss:
   //   dW3 = a3^T dz4 and db3 (row 3136 = the all-ones row; db3 follows dW3 [3136][512] in the flat gradient)
   //   dz3 = (dz4 W3^T) * (a3 > 0)
   {
     ProfScope ps(m->prof, "fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
     const auto Pw = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, 3136);
     const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
-    auto kern = k_gemm_pair<true, true, Epi4StoreF32, false, false, Epi4ReluMask>;
+    const Fc2WgradArgs F{w.a4, actions, w.gs, w.hs, B, G + var_offset(8), G + var_offset(9), loss_dev};
+    auto kern = k_fc1_bwd<Epi4StoreF32, Epi4ReluMask>;
     static bool attr = false;
     if (!attr) {
       set_lds_attr(kern, GemmCfg::LDS);
       attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3(Pw.tiles() + Pd.tiles()), dim3(256), GemmCfg::LDS, s, Pw, Pd);
+    hipLaunchKernelGGL(kern, dim3(Pw.tiles() + Pd.tiles() + kFc2WgradBlocks), dim3(256), GemmCfg::LDS, s, Pw, Pd, F);
   }
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
@@ -743,6 +821,14 @@ int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions
 int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
   return guard([&] {
     QLX_CHECK(m && out && layer >= 1 && layer <= 4 && m->ws_batch > 0, QLX_E_INVALID, "bad argument");
+    QLX_HIP(hipSetDevice(m->device));
+    if (layer == 4 && m->w.a4_splits > 0) {   // forward without a head yet: finish a4 from the fc1 partials
+      const int B = m->last_batch;
+      hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, m->stream,
+                         m->w.fc1slab, (size_t)B * 512, m->w.a4_splits, B, 512, m->d_params + var_offset(7), m->w.a4);
+      QLX_HIP(hipGetLastError());
+      m->w.a4_splits = 0;
+    }
     QLX_HIP(hipStreamSynchronize(m->stream));
     const size_t per[5] = {0, 12800, 5184, 3136, 512};
     const bf16* src = layer == 1 ? m->w.a1 : layer == 2 ? m->w.a2 : layer == 3 ? m->w.a3 : m->w.a4;

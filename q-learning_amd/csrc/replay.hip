@@ -41,55 +41,61 @@ __device__ __forceinline__ uint64_t umulhi64(uint64_t a, uint64_t b, uint64_t* l
   return (uint64_t)(m >> 64);
 }
 
-// generate_distinct_random_ids, one wave per update.  64 consecutive u64 draws are evaluated in
-// parallel per round; a draw is kept iff it passes the zone test, is not in the LDS hash set of
-// earlier keeps and no earlier lane of the round drew the same value — the sequential loop's result.
-__global__ __launch_bounds__(64) void k_sample_distinct(uint64_t seed, uint32_t first_update, uint32_t rank,
-                                                        uint64_t len, uint32_t B, uint32_t log2_table,
-                                                        uint64_t* out) {
-  extern __shared__ unsigned long long table[];
-  const uint32_t u = first_update + blockIdx.x;
-  const int lane = threadIdx.x;
+// generate_distinct_random_ids, one 256-thread block per update.  256 consecutive u64 draws are evaluated in
+// parallel per round; a draw is kept iff it passes the zone test and no earlier draw (an earlier round's keep,
+// or an earlier draw of this round) has the same value - the sequential loop's result.  Every accepted draw
+// claims its value's slot of an LDS hash set (keys u32: values < len < 2^32 - 1) and atomicMin's its draw
+// index into the slot's owner word; after a barrier a draw is kept iff it owns its slot (an earlier round's
+// keep owns it with a smaller index).  Kept draws are compacted in draw order by a block prefix count.
+constexpr int kSampleThreads = 256;
+__global__ __launch_bounds__(kSampleThreads) void k_sample_distinct(uint64_t seed, uint32_t first_update, uint32_t rank,
+                                                                    uint64_t len, uint32_t B, uint32_t log2_table,
+                                                                    uint64_t* out) {
+  extern __shared__ uint32_t sh[];
   const uint32_t tsize = 1u << log2_table;
-  const unsigned long long EMPTY = ~0ull;
-  for (uint32_t i = lane; i < tsize; i += 64) table[i] = EMPTY;
+  uint32_t* keys = sh;
+  uint32_t* owner = sh + tsize;
+  __shared__ uint32_t wave_cnt[kSampleThreads / 64];
+  const uint32_t u = first_update + blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t EMPTY = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < tsize; i += kSampleThreads) { keys[i] = EMPTY; owner[i] = EMPTY; }
   __syncthreads();
   const uint64_t zone = ~0ull - ((~0ull - len + 1) % len);
   uint64_t* dst = out + (size_t)blockIdx.x * B;
   uint32_t count = 0;
   for (uint64_t round = 0; count < B; ++round) {
-    const uint64_t d = round * 64 + lane;
+    const uint64_t d = round * kSampleThreads + tid;
     RngStream rs(seed, u, rank, P_SAMPLE, 2 * d);
     const uint64_t v = rs.u64();
     uint64_t lo;
-    const uint64_t hi = umulhi64(v, len, &lo);
+    const uint32_t hi = (uint32_t)umulhi64(v, len, &lo);
     const bool acc = lo <= zone;
-    bool inset = false;
+    uint32_t h = 0;
     if (acc) {
-      uint32_t h = (uint32_t)((hi * 0x9E3779B97F4A7C15ull) >> (64 - log2_table));
+      h = (uint32_t)(((uint64_t)hi * 0x9E3779B97F4A7C15ull) >> (64 - log2_table));
       for (;;) {
-        const unsigned long long t = table[h];
-        if (t == EMPTY) break;
-        if (t == hi) { inset = true; break; }
+        const uint32_t t = atomicCAS(&keys[h], EMPTY, hi);
+        if (t == EMPTY || t == hi) break;
         h = (h + 1) & (tsize - 1);
       }
+      atomicMin(&owner[h], (uint32_t)d);
     }
-    bool dup = false;
-    for (int j = 0; j < 63; ++j) {
-      const uint64_t vj = __shfl(hi, j);
-      const int aj = __shfl((int)acc, j);
-      if (j < lane && aj && vj == hi) dup = true;
-    }
-    const bool ok = acc && !inset && !dup;
-    const unsigned long long bal = __ballot(ok);
-    const uint32_t pos = count + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    if (ok && pos < B) {
-      dst[pos] = hi;
-      uint32_t h = (uint32_t)((hi * 0x9E3779B97F4A7C15ull) >> (64 - log2_table));
-      while (atomicCAS(&table[h], EMPTY, (unsigned long long)hi) != EMPTY) h = (h + 1) & (tsize - 1);
-    }
-    count = min(B, count + (uint32_t)__popcll(bal));
     __syncthreads();
+    const bool ok = acc && owner[h] == (uint32_t)d;
+    const unsigned long long bal = __ballot(ok);
+    if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kSampleThreads / 64; ++w) {
+      before += w < wave ? wave_cnt[w] : 0u;
+      total += wave_cnt[w];
+    }
+    const uint32_t pos = count + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (ok && pos < B) dst[pos] = hi;
+    count = min(B, count + total);
+    __syncthreads();   // wave_cnt / owner reads done before the next round writes them
   }
 }
 
@@ -136,16 +142,23 @@ void replay_launch_push(qlx_replay* rb, qlx_env* env, hipStream_t s, const uint8
   rb->total += env->n;
 }
 
+// the set holds at most B + 255 keys (the last round may claim slots past B): keep it at most half full
 static uint32_t table_log2(uint32_t batch) {
-  uint32_t l = 6;
-  while ((1u << l) < 4 * batch) ++l;
+  uint32_t l = 8;
+  while ((1u << l) < 2 * (batch + kSampleThreads)) ++l;
   return l;
 }
 
 void replay_launch_sample(qlx_replay* rb, hipStream_t s, uint64_t seed, uint32_t first_update, uint32_t n_updates,
                           uint32_t rank, uint32_t batch, uint64_t* d_out) {
   const uint32_t l2 = table_log2(batch);
-  hipLaunchKernelGGL(k_sample_distinct, dim3(n_updates), dim3(64), (size_t)8 << l2, s, seed, first_update, rank,
+  QLX_CHECK(rb->len() < 0xFFFFFFFFull, QLX_E_INVALID, "replay sampling keys are 32-bit: len must be < 2^32 - 1");
+  static bool attr = false;
+  if (!attr) {   // up to 128 KB of hash set at B = 4096
+    QLX_HIP(hipFuncSetAttribute((const void*)k_sample_distinct, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_sample_distinct, dim3(n_updates), dim3(kSampleThreads), (size_t)8 << l2, s, seed, first_update, rank,
                      (uint64_t)rb->len(), batch, l2, d_out);
   QLX_HIP(hipGetLastError());
 }
