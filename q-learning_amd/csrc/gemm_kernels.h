@@ -82,7 +82,10 @@ struct GemmOperand {
 };
 
 // Epilogues: operator()(m, n, v, z) for C[m][n .. n+3] = v[0..3] of k split z (n % 4 == 0, n + 3 < N when n < N)
+// kSq: the epilogue also yields this tile's sum of squares of the stored values (split by the ones_m row),
+// the clip_by_norm partials of a weight gradient written straight to its final place (see gemm_tile)
 struct Epi4Slab {   // split-K partial: slab[z][m][n] (fp32)
+  static constexpr bool kSq = false;
   float* slab;
   int ldo;
   size_t zstride;
@@ -91,9 +94,11 @@ struct Epi4Slab {   // split-K partial: slab[z][m][n] (fp32)
   }
 };
 
-struct Epi4StoreF32 {   // out[m][n] = v (fp32)
+struct Epi4StoreF32 {   // out[m][n] = v (fp32); sq (optional): [tiles] partials of rows != ones_m, then [tiles] of row ones_m
+  static constexpr bool kSq = true;
   float* out;
   int ldo;
+  float* sq;
   __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int) const {
     *reinterpret_cast<f32x4*>(out + (size_t)m * ldo + n) = v;
   }
@@ -106,6 +111,7 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 }
 
 struct Epi4BiasRelu {   // out[m][n] = relu(v + bias[n]) as bf16
+  static constexpr bool kSq = false;
   bf16* out;
   const float* bias;
   int ldo;
@@ -117,6 +123,7 @@ struct Epi4BiasRelu {   // out[m][n] = relu(v + bias[n]) as bf16
 };
 
 struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16
+  static constexpr bool kSq = false;
   bf16* out;
   const bf16* act;
   int ldo;
@@ -277,6 +284,7 @@ __device__ __forceinline__ void gemm_tile(const GemmProblem<Epi>& P, int tile) {
   }
   // C^T tile: lane = m (lane & 31), reg e = n offset (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
   const int h = lane >> 5;
+  float sq_main = 0.0f, sq_ones = 0.0f;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -285,10 +293,33 @@ __device__ __forceinline__ void gemm_tile(const GemmProblem<Epi>& P, int tile) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int n = n0 + wn * 64 + j * 32 + 8 * u + 4 * h;
-        if (m < M && n < N)
-          epi(m, n, f32x4{acc[t][j][4 * u], acc[t][j][4 * u + 1], acc[t][j][4 * u + 2], acc[t][j][4 * u + 3]}, bz);
+        if (m < M && n < N) {
+          const f32x4 v = {acc[t][j][4 * u], acc[t][j][4 * u + 1], acc[t][j][4 * u + 2], acc[t][j][4 * u + 3]};
+          epi(m, n, v, bz);
+          if constexpr (Epi::kSq) {
+            const float q = ((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]) + v[3] * v[3];
+            if (m == ones_m) sq_ones += q;
+            else sq_main += q;
+          }
+        }
       }
     }
+  if constexpr (Epi::kSq) {
+    if (epi.sq) {   // fixed-order block reduction: xor butterfly per wave, then the 4 waves in order
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        sq_main += __shfl_xor(sq_main, off);
+        sq_ones += __shfl_xor(sq_ones, off);
+      }
+      float* red = reinterpret_cast<float*>(lds);   // the k loop ended on a barrier: LDS is free
+      if (lane == 0) { red[2 * wave] = sq_main; red[2 * wave + 1] = sq_ones; }
+      __syncthreads();
+      if (tid == 0) {
+        epi.sq[tile] = ((red[0] + red[2]) + red[4]) + red[6];
+        epi.sq[P.tiles() + tile] = ((red[1] + red[3]) + red[5]) + red[7];
+      }
+    }
+  }
 }
 
 constexpr int kGemmStages = 2;

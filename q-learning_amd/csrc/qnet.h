@@ -51,6 +51,11 @@ struct qlx_model {
   int64_t *d_rbeg = nullptr, *d_rend = nullptr;
   float* d_partial = nullptr;
   int* d_var_first = nullptr;
+  // clip_by_norm partials written by the gradient producers themselves (fc1 wgrad tiles, conv slab reduction
+  // blocks, fc2 wgrad blocks): when no all-reduce sits between backward and Adam the k_sumsq pass is skipped
+  float* d_sqf = nullptr;
+  int* d_sqf_first = nullptr;
+  bool norms_fused = false;   // set by model_norms: Adam reads d_sqf / d_sqf_first instead
   float* d_norms = nullptr;
   void* ws = nullptr;
   int ws_batch = 0;
@@ -94,7 +99,8 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
 // Huber head + backward after model_forward_trunk: loss -> *loss_dev, raw gradients -> m->d_grads
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
                     hipStream_t s);
-// per-range sums of squares of the (scaled) gradients; k_adam finishes the per-variable norms
+// per-variable norm partials for Adam: with scale == 1 (no all-reduce since the backward) the producers'
+// fused partials are used as they are; otherwise per-range sums of squares of the scaled gradients
 void model_norms(qlx_model* m, hipStream_t s, float scale);
 void model_adam(qlx_model* m, hipStream_t s, float scale);
 }  // namespace qlx

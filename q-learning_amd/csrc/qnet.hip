@@ -32,6 +32,16 @@ static int64_t var_offset(int v) {
   return o;
 }
 
+// fused clip_by_norm partial slots per variable: conv W/b from the slab reduction blocks (64 outputs each),
+// W3/b3 from the 25 x 4 fc1 wgrad tiles (each writes one W3 and one b3 slot), W4 from the 64 dW4 blocks
+constexpr int kFc1WgradTiles = 25 * 4;
+static const int kSqSlots[kNumVars] = {128, 1, 512, 1, 576, 1, kFc1WgradTiles, kFc1WgradTiles, 64, 1};
+static int sq_first(int v) {
+  int o = 0;
+  for (int i = 0; i < v; ++i) o += kSqSlots[i];
+  return o;
+}
+
 // ------------------------------------------------------------------------------------------
 // weight packing: fp32 master (Keras layouts) -> bf16 MFMA operand layouts
 
@@ -219,6 +229,8 @@ struct Fc2WgradArgs {
   float* g_w4;
   float* g_b4;
   float* loss;
+  float* sq_w4;   // [64] square sums of each block's 24 dW4 values
+  float* sq_b4;   // [1]
 };
 constexpr int kFc2WgradBlocks = 65;
 
@@ -259,14 +271,23 @@ __device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, fl
 #pragma unroll
     for (int i = 0; i < 24; ++i) red[wave * 24 + i] = s[i];
   __syncthreads();
+  float t = 0.0f;
   if (tid < 24) {
-    const float t = ((red[tid] + red[24 + tid]) + red[48 + tid]) + red[72 + tid];
+    t = ((red[tid] + red[24 + tid]) + red[48 + tid]) + red[72 + tid];
     if (j == 64) {
       if (tid < 3) A.g_b4[tid] = t;
       else if (tid == 3) *A.loss = t / (float)A.B;
     } else {
       A.g_w4[j * 24 + tid] = t;   // [k][a] with k = 8 j + tid / 3
     }
+    red[96 + tid] = (j < 64 || tid < 3) ? t * t : 0.0f;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float q = 0.0f;
+    for (int i = 0; i < 24; ++i) q += red[96 + i];
+    if (j < 64) A.sq_w4[j] = q;
+    else A.sq_b4[0] = q;
   }
 }
 
@@ -522,9 +543,12 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
   //   dz3 = (dz4 W3^T) * (a3 > 0)
   {
     ProfScope ps(m->prof, "fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
-    const auto Pw = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, 3136);
+    const auto Pw =
+        gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136);
+    QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
     const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
-    const Fc2WgradArgs F{w.a4, actions, w.gs, w.hs, B, G + var_offset(8), G + var_offset(9), loss_dev};
+    const Fc2WgradArgs F{w.a4, actions, w.gs, w.hs, B, G + var_offset(8), G + var_offset(9), loss_dev,
+                         m->d_sqf + sq_first(8), m->d_sqf + sq_first(9)};
     auto kern = k_fc1_bwd<Epi4StoreF32, Epi4ReluMask>;
     static bool attr = false;
     if (!attr) {
@@ -584,10 +608,12 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
   }
   {
     ProfScope ps(m->prof, "wgrad_reduce", s);
+    // slot ranges: each layer's weight blocks then its one bias block (sq_first(W) + blocks == sq_first(b))
+    static_assert(CW3::ZS == 576 * 64 + 64 && CW2::ZS == 512 * 64 + 64 && kConv1SlabStride == 128 * 64 + 32, "slab blocks");
     SlabSeg segs[3] = {
-        {w.slab + kSlabConv3, CW3::ZS, used3, CW3::ZS, G + var_offset(4), 0},
-        {w.slab + kSlabConv2, CW2::ZS, used2, CW2::ZS, G + var_offset(2), 0},
-        {w.slab + kSlabConv1, (size_t)kConv1SlabStride, grid1, (size_t)kConv1SlabStride, G, 1},
+        {w.slab + kSlabConv3, CW3::ZS, used3, CW3::ZS, G + var_offset(4), 0, m->d_sqf + sq_first(4)},
+        {w.slab + kSlabConv2, CW2::ZS, used2, CW2::ZS, G + var_offset(2), 0, m->d_sqf + sq_first(2)},
+        {w.slab + kSlabConv1, (size_t)kConv1SlabStride, grid1, (size_t)kConv1SlabStride, G, 1, m->d_sqf + sq_first(0)},
     };
     SlabSegs3 a;
     int blocks = 0;
@@ -604,6 +630,8 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
 
 
 void model_norms(qlx_model* m, hipStream_t s, float scale) {
+  m->norms_fused = scale == 1.0f;   // the gradients are exactly what model_backward produced
+  if (m->norms_fused) return;
   ProfScope ps(m->prof, "norms", s);
   hipLaunchKernelGGL(k_sumsq, dim3(m->n_ranges), dim3(256), 0, s, m->d_grads, m->d_rbeg, m->d_rend, scale, m->d_partial);
   QLX_HIP(hipGetLastError());
@@ -615,7 +643,8 @@ void model_adam(qlx_model* m, hipStream_t s, float scale) {
   const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
   AdamArgs a;
   a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.norms = m->d_norms;
-  a.partial = m->d_partial; a.var_first = m->d_var_first;
+  a.partial = m->norms_fused ? m->d_sqf : m->d_partial;
+  a.var_first = m->norms_fused ? m->d_sqf_first : m->d_var_first;
   a.count = kNumParams; a.scale = scale;
   a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
@@ -701,6 +730,12 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     QLX_HIP(hipMalloc(&m->d_partial, rb.size() * 4));
     QLX_HIP(hipMalloc(&m->d_var_first, vf.size() * 4));
     QLX_HIP(hipMalloc(&m->d_norms, 64));
+    std::vector<int> sf(kNumVars + 1);
+    for (int v = 0; v <= kNumVars; ++v) sf[v] = v < kNumVars ? sq_first(v) : sq_first(kNumVars - 1) + kSqSlots[kNumVars - 1];
+    QLX_HIP(hipMalloc(&m->d_sqf, sf[kNumVars] * 4));
+    QLX_HIP(hipMalloc(&m->d_sqf_first, sf.size() * 4));
+    QLX_HIP(hipMemcpy(m->d_sqf_first, sf.data(), sf.size() * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemset(m->d_sqf, 0, sf[kNumVars] * 4));
     QLX_HIP(hipMemcpy(m->d_rbeg, rb.data(), rb.size() * 8, hipMemcpyHostToDevice));
     QLX_HIP(hipMemcpy(m->d_rend, re.data(), re.size() * 8, hipMemcpyHostToDevice));
     QLX_HIP(hipMemcpy(m->d_var_first, vf.data(), vf.size() * 4, hipMemcpyHostToDevice));
@@ -722,7 +757,7 @@ int32_t qlx_model_destroy(qlx_model* m) {
     (void)hipSetDevice(m->device);
     (void)hipStreamSynchronize(m->stream);
     void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wb3,
-                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->ws};
+                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->d_sqf, m->d_sqf_first, m->ws};
     for (void* p : ptrs) (void)hipFree(p);
     if (m->own_stream) (void)hipStreamDestroy(m->stream);
     delete m;

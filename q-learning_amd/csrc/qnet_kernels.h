@@ -74,8 +74,10 @@ __device__ __forceinline__ int conv1_hwio_from_s2d(int i) {   // i = k * 32 + oc
   return (((4 * ii + dx) * 8 + 4 * j + dy) * 4 + c) * 32 + oc;
 }
 
+// sq (optional): the block's sum of squares of its 64 outputs -> sq[blk] (the layer's weight blocks come
+// first; a block past them holds the bias)
 __device__ __forceinline__ void slab_reduce_block(const float* slab, size_t zstride, int chunks, size_t count, float* out,
-                                                  bool conv1, int blk) {
+                                                  bool conv1, int blk, float* sq = nullptr) {
   __shared__ float part[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t i = (size_t)blk * 64 + lane;
@@ -94,9 +96,18 @@ __device__ __forceinline__ void slab_reduce_block(const float* slab, size_t zstr
   }
   part[wave][lane] = s;
   __syncthreads();
-  if (wave == 0 && i < count) {
-    const size_t d = conv1 && i < 8192 ? (size_t)conv1_hwio_from_s2d((int)i) : i;
-    out[d] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  if (wave == 0) {
+    const float v = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    if (i < count) {
+      const size_t d = conv1 && i < 8192 ? (size_t)conv1_hwio_from_s2d((int)i) : i;
+      out[d] = v;
+    }
+    if (sq) {
+      float q = i < count ? v * v : 0.0f;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+      if (lane == 0) sq[blk] = q;
+    }
   }
 }
 
@@ -114,6 +125,7 @@ struct SlabSeg {
   size_t count;
   float* out;
   int conv1;
+  float* sq;   // per-block square sums (nullable): block b of the segment -> sq[b]
 };
 struct SlabSegs3 {
   SlabSeg seg[3];
@@ -123,7 +135,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce3(SlabSegs3 a) {
   const int b = blockIdx.x;
   const int i = b < a.first_block[1] ? 0 : (b < a.first_block[2] ? 1 : 2);
   const SlabSeg& g = a.seg[i];
-  slab_reduce_block(g.slab, g.zstride, g.chunks, g.count, g.out, g.conv1 != 0, b - a.first_block[i]);
+  slab_reduce_block(g.slab, g.zstride, g.chunks, g.count, g.out, g.conv1 != 0, b - a.first_block[i], g.sq);
 }
 
 __global__ void k_slab_reduce_bias_relu(const float* slab, size_t zstride, int chunks, int M, int N,

@@ -134,7 +134,7 @@ int main(int argc, char** argv) {
     const double fl = 2.0 * B * 512 * 3136;
     char nm[128];
     for (int nf = 0; nf < 2; ++nf) {
-      const auto Pw = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512}, 3136, nf == 1);
+      const auto Pw = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512, nullptr}, 3136, nf == 1);
       const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
 #define RUNW(S, O, R, D)                                                                                                     \
   {                                                                                                                       \
