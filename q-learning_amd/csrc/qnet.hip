@@ -489,7 +489,7 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
     }
     auto kern = store_acts ? k_trunk_fwd<true> : k_trunk_fwd<false>;
     hipLaunchKernelGGL(kern, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkFwdLds, s, table, B, m->wf0, m->wf1, m->wf2,
-                       p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3);
+                       p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3, nullptr);
   }
   {  // fc1: M = B, N = 512, K = 3136.  Small batches split K into kFc1Split fp32 slabs (reduced with bias +
      // ReLU in fixed order) to fill the chip; from 64 M tiles on (B >= 8192) one pass with the epilogue fused

@@ -52,11 +52,15 @@ __device__ __forceinline__ void u8x16_to_bf16(uint4 v, uint4& lo, uint4& hi) {
   hi.w = u8pair_bf16(v.w, 16);
 }
 
-// register prefetch of one sample's frames: chunk c = slot * 441 + pos (nullptr frame = zeros)
-__device__ __forceinline__ void frames_prefetch(const uint8_t* const* table, int b, int B, uint4 (&pf)[kPf]) {
+template <int NT>
+constexpr int pf_chunks() { return (kFrameChunks + NT - 1) / NT; }
+
+// register prefetch of one sample's frames: chunk c = slot * 441 + pos (nullptr frame = zeros); NT threads
+template <int NT = kTrunkThreads>
+__device__ __forceinline__ void frames_prefetch(const uint8_t* const* table, int b, int B, uint4 (&pf)[pf_chunks<NT>()]) {
 #pragma unroll
-  for (int u = 0; u < kPf; ++u) {
-    const int c = threadIdx.x + u * kTrunkThreads;
+  for (int u = 0; u < pf_chunks<NT>(); ++u) {
+    const int c = threadIdx.x + u * NT;
     pf[u] = uint4{0, 0, 0, 0};
     if (b < B && c < kFrameChunks) {
       const int slot = c / 441, pos = c - slot * 441;
@@ -69,15 +73,63 @@ __device__ __forceinline__ void frames_prefetch(const uint8_t* const* table, int
   }
 }
 
-__device__ __forceinline__ void frames_stage(bf16* X, const uint4 (&pf)[kPf]) {
+// the same with the sample's 4 frame pointers already in LDS (fptr[slot]): no dependent pointer load in the
+// issuing wave's path (the table entry is fetched a sample earlier, see k_trunk_fwd)
+template <int NT = kTrunkThreads>
+__device__ __forceinline__ void frames_prefetch_ptrs(const uint8_t* const* fptr, bool valid, uint4 (&pf)[pf_chunks<NT>()]) {
 #pragma unroll
-  for (int u = 0; u < kPf; ++u) {
-    const int c = threadIdx.x + u * kTrunkThreads;
+  for (int u = 0; u < pf_chunks<NT>(); ++u) {
+    const int c = threadIdx.x + u * NT;
+    pf[u] = uint4{0, 0, 0, 0};
+    if (valid && c < kFrameChunks) {
+      const int slot = c / 441, pos = c - slot * 441;
+      const uint8_t* f = fptr[slot];
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      if (f) pf[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(f + pos * 16));
+    }
+  }
+}
+
+// Slot-major variant for the forward trunk: thread tid < 441 owns s2d block pos = tid of all 4 slots, so the
+// frame pointer of each load is wave-uniform (read from LDS, fptr[slot]) and the per-lane address is one
+// 32-bit offset - no 64-bit per-chunk addresses to keep live across the sample.
+__device__ __forceinline__ void frames_prefetch_slots(const uint8_t* const* fptr, bool valid, uint4 (&pf)[4]) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int pos = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    pf[u] = uint4{0, 0, 0, 0};
+    const unsigned long long fv = (unsigned long long)fptr[u];   // uniform: one LDS broadcast -> SGPRs
+    const uint8_t* f = (const uint8_t*)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(fv >> 32)) << 32) |
+                                        (unsigned)__builtin_amdgcn_readfirstlane((int)fv));
+    if (valid && f && pos < 441) pf[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(f + pos * 16));
+  }
+}
+__device__ __forceinline__ void frames_stage_slots(bf16* X, const uint4 (&pf)[4]) {
+  const int pos = threadIdx.x;
+  if (pos < 441) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint4 lo, hi;
+      u8x16_to_bf16(pf[u], lo, hi);
+      uint4* d = reinterpret_cast<uint4*>(X + pos * kXS + u * 16);
+      d[0] = lo;
+      d[1] = hi;
+    }
+  }
+}
+
+// u8 -> bf16 into the staged image X [441][XS] (ch = slot * 16 + sub-pixel)
+template <int NT = kTrunkThreads, int XS = kXS>
+__device__ __forceinline__ void frames_stage(bf16* X, const uint4 (&pf)[pf_chunks<NT>()]) {
+#pragma unroll
+  for (int u = 0; u < pf_chunks<NT>(); ++u) {
+    const int c = threadIdx.x + u * NT;
     if (c < kFrameChunks) {
       const int slot = c / 441, pos = c - slot * 441;
       uint4 lo, hi;
       u8x16_to_bf16(pf[u], lo, hi);
-      uint4* d = reinterpret_cast<uint4*>(X + pos * kXS + slot * 16);
+      uint4* d = reinterpret_cast<uint4*>(X + pos * XS + slot * 16);
       d[0] = lo;
       d[1] = hi;
     }
@@ -85,10 +137,10 @@ __device__ __forceinline__ void frames_stage(bf16* X, const uint4 (&pf)[kPf]) {
 }
 
 // LDS rows [rows][stride] -> global contiguous [rows][cols] with 16-byte chunks
-template <int ROWS, int COLS, int STRIDE>
+template <int ROWS, int COLS, int STRIDE, int NT = kTrunkThreads>
 __device__ __forceinline__ void lds_copy_out(const bf16* src, bf16* dst) {
   constexpr int CPR = COLS / 8;
-  for (int c = threadIdx.x; c < ROWS * CPR; c += kTrunkThreads) {
+  for (int c = threadIdx.x; c < ROWS * CPR; c += NT) {
     const int row = c / CPR, col = (c - row * CPR) * 8;
     *reinterpret_cast<uint4*>(dst + row * COLS + col) = *reinterpret_cast<const uint4*>(src + row * STRIDE + col);
   }
@@ -104,8 +156,11 @@ __device__ __forceinline__ bf16 relu_bf16(float v) { return (bf16)(v > 0.0f ? v 
 // 4 consecutive channels 4 (lane >> 4) + e of one position: one 8-byte LDS store per tile.  The B-fragment
 // LDS reads run D deep ahead of their MFMAs across tile boundaries (ring slot s % D), so a tile's epilogue
 // overlaps the next tile's reads.  addr(t, s) -> LDS pointer of k-step s of tile t for this lane.
-template <int KS, int D, class Addr, class Epi>
-__device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 (&w)[KS], Addr addr, Epi epi) {
+// pre(t) runs at the start of tile t, before the tile's refill reads are issued, and its result is handed to
+// epi(t, acc, pre_value): an LDS value the epilogue needs (e.g. a ReLU mask) is then older than the ring
+// reads in flight, so waiting for it is lgkmcnt(D) instead of a drain of the whole ring.
+template <int KS, int D, class Addr, class Pre, class Epi>
+__device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 (&w)[KS], Addr addr, Pre pre, Epi epi) {
   static_assert(KS % D == 0, "ring depth must divide the k-steps");
   if (t0 >= nt) return;
   bf16x8 a[D];
@@ -114,6 +169,7 @@ __device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 
   for (int t = t0; t < nt; t += dt) {
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const bool more = t + dt < nt;
+    const auto pv = pre(t);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[s], a[s % D], acc, 0, 0, 0);
@@ -124,7 +180,7 @@ __device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // keep the order: this MFMA, then its refill read
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    epi(t, acc);
+    epi(t, acc, pv);
   }
 }
 
@@ -137,13 +193,24 @@ __device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) 
 __device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
 
 // a1 [B][400][32], a2 [B][81][64] (written when STORE12), a3 [B][49][64] (always)
-template <bool STORE12>
+// TIMING (development only): wave 0 accumulates s_memtime cycles per phase (staging, conv1, conv2, conv3)
+// into timing[blockIdx.x * 4 + phase]
+template <bool STORE12, bool TIMING = false>
 __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* const* __restrict__ table, int B,
                                                                 const bf16* __restrict__ wf0, const bf16* __restrict__ wf1,
                                                                 const bf16* __restrict__ wf2, const float* __restrict__ bias0,
                                                                 const float* __restrict__ bias1,
                                                                 const float* __restrict__ bias2, bf16* __restrict__ a1,
-                                                                bf16* __restrict__ a2, bf16* __restrict__ a3) {
+                                                                bf16* __restrict__ a2, bf16* __restrict__ a3,
+                                                                unsigned long long* __restrict__ timing = nullptr) {
+  unsigned long long ph[4] = {0, 0, 0, 0}, tm = 0;
+  auto mark = [&](int i) {
+    if constexpr (TIMING) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (i >= 0) ph[i] += t - tm;
+      tm = t;
+    }
+  };
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   bf16* X = lds;
   bf16* A1 = lds + kLdsX;
@@ -165,21 +232,32 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   __shared__ __attribute__((aligned(16))) float sbias[160];
   if (threadIdx.x < 160)
     sbias[threadIdx.x] = threadIdx.x < 32 ? bias0[threadIdx.x] : (threadIdx.x < 96 ? bias1[threadIdx.x - 32] : bias2[threadIdx.x - 96]);
-  auto bias_relu4 = [](const float* bias, f32x4 acc) {
-    const float4 bv = *reinterpret_cast<const float4*>(bias);
+  auto bias_relu4 = [](float4 bv, f32x4 acc) {
     return pack4_bf16(relu(acc[0] + bv.x), relu(acc[1] + bv.y), relu(acc[2] + bv.z), relu(acc[3] + bv.w));
   };
   // Loads and stores share vmcnt: waiting for a prefetch also waits for every store issued before the wait.
   // Each sample's frames are therefore staged BEFORE the previous sample's a3 copy-out is issued, so the wait
   // never covers fresh stores (a1 / a2 go out during the conv2 / conv3 phases, long before).
-  uint4 pf[kPf];
-  frames_prefetch(table, blockIdx.x, B, pf);
+  // Frame pointers run one sample ahead of the frame data: threads 0-3 load sample b + 2 grid's table entries
+  // while sample b computes and park them in LDS at the next staging, so the data prefetch of sample
+  // b + grid never waits on a dependent pointer load.
+  __shared__ const uint8_t* sptr[4];
+  const uint8_t* pnext = nullptr;   // threads 0-3: table entry (slot = tid) of sample b + grid
+  uint4 pf[4];
+  if (threadIdx.x < 4) sptr[threadIdx.x] = (int)blockIdx.x < B ? table[blockIdx.x * 4 + threadIdx.x] : nullptr;
+  if (threadIdx.x < 4 && (int)(blockIdx.x + gridDim.x) < B) pnext = table[(blockIdx.x + gridDim.x) * 4 + threadIdx.x];
+  lds_barrier();
+  frames_prefetch_slots(sptr, (int)blockIdx.x < B, pf);
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    lds_barrier();   // previous sample's conv phases are done with X / A2
-    frames_stage(X, pf);
+    mark(-1);
+    lds_barrier();   // previous sample's conv phases are done with X / A2 (and the pointer slots)
+    frames_stage_slots(X, pf);
+    if (threadIdx.x < 4) sptr[threadIdx.x] = pnext;
     if (b != (int)blockIdx.x) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)(b - gridDim.x) * 3136);
     lds_barrier();
-    frames_prefetch(table, b + gridDim.x, B, pf);
+    mark(0);
+    frames_prefetch_slots(sptr, b + (int)gridDim.x < B, pf);
+    if (threadIdx.x < 4 && b + 2 * (int)gridDim.x < B) pnext = table[(b + 2 * gridDim.x) * 4 + threadIdx.x];
     // conv1: M = 400 (25 tiles of 16), N = 32, K = 256: k-step s covers tap (i, j) = (s >> 2, (s >> 1) & 1)
     conv_tiles<8, 4>(
         wave >> 1, 4, 25, w1,
@@ -187,10 +265,12 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
           const int m = t * 16 + r, ox = m / 20, oy = m - ox * 20;
           return X + ((ox + (s >> 2)) * 21 + oy + ((s >> 1) & 1)) * kXS + 32 * (s & 1) + 8 * g;
         },
-        [&](int t, f32x4 acc) {
-          *reinterpret_cast<uint2*>(A1 + (t * 16 + r) * kA1S + c1 + 4 * g) = bias_relu4(sbias + c1 + 4 * g, acc);
+        [&](int) { return *reinterpret_cast<const float4*>(sbias + c1 + 4 * g); },
+        [&](int t, f32x4 acc, float4 bv) {
+          *reinterpret_cast<uint2*>(A1 + (t * 16 + r) * kA1S + c1 + 4 * g) = bias_relu4(bv, acc);
         });
     lds_barrier();
+    mark(1);
     if (STORE12) lds_copy_out<400, 32, kA1S>(A1, a1 + (size_t)b * 12800);
     // conv2: 4x4 stride 2 over A1 [20][20][32]; M = 81 (6 tiles), k-step s = tap (kh, kw) = (s >> 2, s & 3)
     conv_tiles<16, 4>(
@@ -199,12 +279,13 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
           const int m = min(t * 16 + r, 80), p = m / 9, q = m - p * 9;
           return A1 + ((2 * p + (s >> 2)) * 20 + 2 * q + (s & 3)) * kA1S + 8 * g;
         },
-        [&](int t, f32x4 acc) {
+        [&](int) { return *reinterpret_cast<const float4*>(sbias + 32 + c2 + 4 * g); },
+        [&](int t, f32x4 acc, float4 bv) {
           const int m = t * 16 + r;
-          if (m < 81)
-            *reinterpret_cast<uint2*>(A2 + m * kA2S + c2 + 4 * g) = bias_relu4(sbias + 32 + c2 + 4 * g, acc);
+          if (m < 81) *reinterpret_cast<uint2*>(A2 + m * kA2S + c2 + 4 * g) = bias_relu4(bv, acc);
         });
     lds_barrier();
+    mark(2);
     if (STORE12) lds_copy_out<81, 64, kA2S>(A2, a2 + (size_t)b * 5184);
     // conv3: 3x3 stride 1 over A2 [9][9][64]; M = 49 (4 tiles), k-step s: tap s >> 1, channel half s & 1
     conv_tiles<18, 3>(
@@ -214,11 +295,16 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
           const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
           return A2 + ((p + kh) * 9 + q + kw) * kA2S + 32 * (s & 1) + 8 * g;
         },
-        [&](int t, f32x4 acc) {
+        [&](int) { return *reinterpret_cast<const float4*>(sbias + 96 + c2 + 4 * g); },
+        [&](int t, f32x4 acc, float4 bv) {
           const int m = t * 16 + r;
-          if (m < 49)
-            *reinterpret_cast<uint2*>(A3 + m * kA3S + c2 + 4 * g) = bias_relu4(sbias + 96 + c2 + 4 * g, acc);
+          if (m < 49) *reinterpret_cast<uint2*>(A3 + m * kA3S + c2 + 4 * g) = bias_relu4(bv, acc);
         });
+    mark(3);
+  }
+  if constexpr (TIMING) {
+    if (threadIdx.x == 0)
+      for (int i = 0; i < 4; ++i) timing[blockIdx.x * 4 + i] = ph[i];
   }
   lds_barrier();
   const int last = (int)blockIdx.x + ((B - 1 - (int)blockIdx.x) / (int)gridDim.x) * (int)gridDim.x;
@@ -251,7 +337,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
   const int bn = tid & 31, brg = tid >> 5;   // bias: column bn, rows brg + 16 i
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   auto tr = [](const bf16* pp) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pp)); };
-  uint4 pf[kPf], dv[4];
+  uint4 pf[4], dv[4];
   // dz1 sample block [400][32] -> registers (1600 chunks), one sample ahead like the frames
   auto dz_prefetch = [&](int b) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -263,18 +349,26 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
         dv[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(dz1 + (size_t)b * 12800 + c * 8));
     }
   };
-  frames_prefetch(table, blockIdx.x, B, pf);
+  // frame pointers one sample ahead of the frame data (as in k_trunk_fwd)
+  __shared__ const uint8_t* sptr[4];
+  const uint8_t* pnext = nullptr;
+  if (tid < 4) sptr[tid] = (int)blockIdx.x < B ? table[blockIdx.x * 4 + tid] : nullptr;
+  if (tid < 4 && (int)(blockIdx.x + gridDim.x) < B) pnext = table[(blockIdx.x + gridDim.x) * 4 + tid];
+  lds_barrier();
+  frames_prefetch_slots(sptr, (int)blockIdx.x < B, pf);
   dz_prefetch(blockIdx.x);
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     lds_barrier();   // previous sample's readers are done
-    frames_stage(X, pf);
+    frames_stage_slots(X, pf);
+    if (tid < 4) sptr[tid] = pnext;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + u * kTrunkThreads;
       if (c < 1600) *reinterpret_cast<uint4*>(DZ + (c >> 2) * kDZS + (c & 3) * 8) = dv[u];
     }
     lds_barrier();
-    frames_prefetch(table, b + gridDim.x, B, pf);
+    frames_prefetch_slots(sptr, b + (int)gridDim.x < B, pf);
+    if (tid < 4 && b + 2 * (int)gridDim.x < B) pnext = table[(b + 2 * gridDim.x) * 4 + tid];
     dz_prefetch(b + gridDim.x);
     for (int ms = 0; ms < 13; ++ms) {
       const int m0 = ms * 32;
@@ -419,11 +513,11 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
           const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
           return P3 + ((ih + 2 - kh) * 11 + iw + 2 - kw) * kPadS + 32 * (s & 1) + 8 * g;
         },
-        [&](int t, f32x4 acc) {
+        [&](int t) { return *reinterpret_cast<const bf16x4*>(M2 + min(t * 16 + r, 80) * 72 + c3 + 4 * g); },
+        [&](int t, f32x4 acc, bf16x4 act) {
           const int m = t * 16 + r;
           if (m < 81) {
             const int oh = m / 9, ow = m - oh * 9;
-            const bf16x4 act = *reinterpret_cast<const bf16x4*>(M2 + m * 72 + c3 + 4 * g);
             *reinterpret_cast<uint2*>(P2 + ((oh + 1) * 11 + ow + 1) * kPadS + c3 + 4 * g) =
                 pack4_bf16((float)act[0] > 0.0f ? acc[0] : 0.0f, (float)act[1] > 0.0f ? acc[1] : 0.0f,
                            (float)act[2] > 0.0f ? acc[2] : 0.0f, (float)act[3] > 0.0f ? acc[3] : 0.0f);
@@ -446,7 +540,8 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
             const int tp = s >> 1, th = tp >> 1, tw = tp & 1;
             return P2 + ((i + 1 - th) * 11 + j + 1 - tw) * kPadS + 32 * (s & 1) + 8 * g;
           },
-          [&](int t, f32x4 acc) {
+          [](int) { return 0; },
+          [&](int t, f32x4 acc, int) {
             const int m = t * 16 + r;
             if (m < 100) {
               const int i = m / 10, j = m - i * 10;

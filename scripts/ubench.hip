@@ -128,6 +128,69 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "k_adam_scalar grid %d", grid);
     report(nm, time_us([&] { hipLaunchKernelGGL(k_adam_scalar, dim3(grid), dim3(256), 0, g_s, a); }), adam_bytes, "GB/s");
   }
+  // ---- per-sample conv kernels: time vs batch (intercept = per-launch ramp, slope = per-sample cost)
+  if (argc > 1 && std::string(argv[1]) == "trunk") {
+    set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
+    set_lds_attr(k_trunk_fwd<false>, kTrunkFwdLds);
+    set_lds_attr(k_trunk_bwd_data, kTrunkBwdLds);
+    set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
+    // frames: random u8 s2d frames for BT samples
+    {
+      std::vector<uint8_t> h((size_t)BT * 4 * kFramePix);
+      std::mt19937 r(5);
+      for (auto& x : h) x = (uint8_t)(r() & 255);
+      QLX_HIP(hipMemcpy(w.frames, h.data(), h.size(), hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(k_frame_table, dim3((BT * 4 + 255) / 256), dim3(256), 0, g_s, w.frames, BT, w.table);
+    }
+    fill_bf16(w.dz3, (size_t)BT * 3136, 0.01f, 6);
+    {   // per-phase cycles of the forward (wave 0 of each block), B = 8192 (32 samples per block)
+      unsigned long long* dt = nullptr;
+      QLX_HIP(hipMalloc(&dt, 256 * 4 * 8));
+      set_lds_attr(k_trunk_fwd<false, true>, kTrunkFwdLds);
+      set_lds_attr(k_trunk_fwd<true, true>, kTrunkFwdLds);
+      set_lds_attr(k_trunk_fwd<false, true>, kTrunkFwdLds);
+      set_lds_attr(k_trunk_fwd<true, true>, kTrunkFwdLds);
+      for (int st = 0; st < 2; ++st) {
+        auto k = st ? k_trunk_fwd<true, true> : k_trunk_fwd<false, true>;
+        hipLaunchKernelGGL(k, dim3(256), dim3(kTrunkThreads), kTrunkFwdLds, g_s, w.table, BT, m->wf0, m->wf1, m->wf2, p + var_offset(1),
+                           p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3, dt);
+        std::vector<unsigned long long> h(256 * 4);
+        QLX_HIP(hipMemcpy(h.data(), dt, h.size() * 8, hipMemcpyDeviceToHost));
+        double acc[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 256; ++b)
+          for (int i = 0; i < 4; ++i) acc[i] += (double)h[b * 4 + i] / 256.0 / 32.0;
+        QLX_HIP(hipDeviceSynchronize());
+        printf("trunk_fwd<%s> cycles per sample: stage %.0f conv1 %.0f conv2 %.0f conv3 %.0f total %.0f\n", st ? "store" : "nostore",
+               acc[0], acc[1], acc[2], acc[3], acc[0] + acc[1] + acc[2] + acc[3]);
+      }
+    }
+    for (int B : {256, 512, 1024, 2048, 4096, 8192}) {
+      const double fwd_fl = 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576);
+      const int grid = std::min(B, 256);
+      char nm[96];
+      snprintf(nm, sizeof nm, "trunk_fwd<store> B=%d", B);
+      report(nm, time_us([&] {
+        hipLaunchKernelGGL(k_trunk_fwd<true>, dim3(grid), dim3(kTrunkThreads), kTrunkFwdLds, g_s, w.table, B, m->wf0, m->wf1, m->wf2,
+                           p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3, nullptr);
+      }), fwd_fl, "TF/s");
+      snprintf(nm, sizeof nm, "trunk_fwd<nostore> B=%d", B);
+      report(nm, time_us([&] {
+        hipLaunchKernelGGL(k_trunk_fwd<false>, dim3(grid), dim3(kTrunkThreads), kTrunkFwdLds, g_s, w.table, B, m->wf0, m->wf1, m->wf2,
+                           p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3, nullptr);
+      }), fwd_fl, "TF/s");
+      snprintf(nm, sizeof nm, "trunk_bwd_data B=%d", B);
+      report(nm, time_us([&] {
+        hipLaunchKernelGGL(k_trunk_bwd_data, dim3(grid), dim3(kTrunkThreads), kTrunkBwdLds, g_s, w.dz3, w.a2, w.a1, B, m->wb2, m->wb1,
+                           w.dz2, w.dz1);
+      }), 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512), "TF/s");
+      snprintf(nm, sizeof nm, "conv1_wgrad B=%d", B);
+      report(nm, time_us([&] {
+        hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid), dim3(kTrunkThreads), kConv1WgradLds, g_s, w.table, w.dz1, B, w.slab + kSlabConv1);
+      }), 2.0 * B * 400 * 256 * 32, "TF/s");
+    }
+    qlx_model_destroy(m);
+    return 0;
+  }
   // ---- fc1 GEMMs: variants (register stages S, occupancy, XCD remap)
 #define VARIANTS(X) X(2, 2, false, 0) X(2, 2, true, 0) X(2, 2, true, 1) X(2, 2, true, 2) X(2, 1, true, 0) X(2, 1, true, 1) X(2, 1, true, 2)
   for (int B : {1024, 8192}) {
