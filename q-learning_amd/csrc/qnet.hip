@@ -562,11 +562,11 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     ProfScope ps(m->prof, "trunk_bwd_data", s, 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512));
     static bool attr = false;
     if (!attr) {
-      set_lds_attr(k_trunk_bwd_data, kTrunkBwdLds);
+      set_lds_attr(k_trunk_bwd_data<false>, kTrunkBwdLds);
       attr = true;
     }
-    hipLaunchKernelGGL(k_trunk_bwd_data, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkBwdLds, s, w.dz3, w.a2, w.a1, B, m->wb2,
-                       m->wb1, w.dz2, w.dz1);
+    hipLaunchKernelGGL(k_trunk_bwd_data<false>, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkBwdLds, s, w.dz3, w.a2, w.a1, B,
+                       m->wb2, m->wb1, w.dz2, w.dz1, nullptr);
   }
   // conv3 (3 tap groups of 3 taps) + conv2 (2 groups of 8 taps) weight gradients in one launch, then
   // conv1's; per-block fp32 partials of [dW | db] rows, reduced in fixed order by one grouped launch

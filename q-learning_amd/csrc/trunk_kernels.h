@@ -33,9 +33,18 @@ constexpr int kLdsX = 441 * kXS;         // bf16 elements
 constexpr int kLdsA1 = 400 * kA1S;
 constexpr int kLdsDZ = 416 * kDZS;
 constexpr int kLdsA3 = 49 * kA3S;
+// Forward images use row pitches (in positions) chosen so that the 16-lane im2col read groups stay
+// bank-conflict-free when their positions wrap to the next image row: with the 40-dword (X, A2) / 20-dword
+// (A1, stride-2 reads) position strides the bank window repeats every 8 position steps, and a wrap must
+// advance it like one ordinary step: X pitch 28 (20 output columns), A1 25 (9 columns at stride 2),
+// A2 15 (7 columns).
+constexpr int kXW = 28, kA1W = 25, kA2W = 15;
+constexpr int kLdsXf = 21 * kXW * kXS;
+constexpr int kLdsA1f = 20 * kA1W * kA1S;
+static_assert(9 * kA2W * kA2S <= kLdsXf, "A2 aliases X");
 // A2 aliases X (dead after conv1); A3 has its own region because its copy-out is deferred past the next
 // sample's staging (see k_trunk_fwd)
-constexpr size_t kTrunkFwdLds = (size_t)(kLdsX + kLdsA1 + kLdsA3) * 2;
+constexpr size_t kTrunkFwdLds = (size_t)(kLdsXf + kLdsA1f + kLdsA3) * 2;
 constexpr size_t kConv1WgradLds = (size_t)(kLdsX + kLdsDZ) * 2;
 constexpr int kFrameChunks = 4 * 441;    // 16-byte s2d blocks per sample
 constexpr int kPf = (kFrameChunks + kTrunkThreads - 1) / kTrunkThreads;
@@ -105,14 +114,16 @@ __device__ __forceinline__ void frames_prefetch_slots(const uint8_t* const* fptr
     if (valid && f && pos < 441) pf[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(f + pos * 16));
   }
 }
+template <int PITCH = 21>   // X row pitch in positions
 __device__ __forceinline__ void frames_stage_slots(bf16* X, const uint4 (&pf)[4]) {
   const int pos = threadIdx.x;
   if (pos < 441) {
+    const int row = PITCH == 21 ? pos : (pos / 21) * PITCH + pos % 21;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       uint4 lo, hi;
       u8x16_to_bf16(pf[u], lo, hi);
-      uint4* d = reinterpret_cast<uint4*>(X + pos * kXS + u * 16);
+      uint4* d = reinterpret_cast<uint4*>(X + row * kXS + u * 16);
       d[0] = lo;
       d[1] = hi;
     }
@@ -143,6 +154,16 @@ __device__ __forceinline__ void lds_copy_out(const bf16* src, bf16* dst) {
   for (int c = threadIdx.x; c < ROWS * CPR; c += NT) {
     const int row = c / CPR, col = (c - row * CPR) * 8;
     *reinterpret_cast<uint4*>(dst + row * COLS + col) = *reinterpret_cast<const uint4*>(src + row * STRIDE + col);
+  }
+}
+
+// LDS image rows of W valid positions at pitch PW -> global contiguous [ROWS][COLS]
+template <int ROWS, int COLS, int STRIDE, int W, int PW>
+__device__ __forceinline__ void lds_copy_out_pitched(const bf16* src, bf16* dst) {
+  constexpr int CPR = COLS / 8;
+  for (int c = threadIdx.x; c < ROWS * CPR; c += kTrunkThreads) {
+    const int row = c / CPR, col = (c - row * CPR) * 8, lrow = (row / W) * PW + row % W;
+    *reinterpret_cast<uint4*>(dst + row * COLS + col) = *reinterpret_cast<const uint4*>(src + lrow * STRIDE + col);
   }
 }
 
@@ -213,9 +234,9 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   };
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   bf16* X = lds;
-  bf16* A1 = lds + kLdsX;
+  bf16* A1 = lds + kLdsXf;
   bf16* A2 = lds;               // aliases X
-  bf16* A3 = lds + kLdsX + kLdsA1;
+  bf16* A3 = lds + kLdsXf + kLdsA1f;
   const int wave = wave_id(), lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   const int c1 = (wave & 1) * 16, c2 = (wave & 3) * 16;   // the wave's output-channel slice, conv1 / conv2+3
@@ -251,7 +272,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     mark(-1);
     lds_barrier();   // previous sample's conv phases are done with X / A2 (and the pointer slots)
-    frames_stage_slots(X, pf);
+    frames_stage_slots<kXW>(X, pf);
     if (threadIdx.x < 4) sptr[threadIdx.x] = pnext;
     if (b != (int)blockIdx.x) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)(b - gridDim.x) * 3136);
     lds_barrier();
@@ -263,37 +284,38 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
         wave >> 1, 4, 25, w1,
         [&](int t, int s) {
           const int m = t * 16 + r, ox = m / 20, oy = m - ox * 20;
-          return X + ((ox + (s >> 2)) * 21 + oy + ((s >> 1) & 1)) * kXS + 32 * (s & 1) + 8 * g;
+          return X + ((ox + (s >> 2)) * kXW + oy + ((s >> 1) & 1)) * kXS + 32 * (s & 1) + 8 * g;
         },
         [&](int) { return *reinterpret_cast<const float4*>(sbias + c1 + 4 * g); },
         [&](int t, f32x4 acc, float4 bv) {
-          *reinterpret_cast<uint2*>(A1 + (t * 16 + r) * kA1S + c1 + 4 * g) = bias_relu4(bv, acc);
+          const int m = t * 16 + r, ox = m / 20;
+          *reinterpret_cast<uint2*>(A1 + (ox * kA1W + m - ox * 20) * kA1S + c1 + 4 * g) = bias_relu4(bv, acc);
         });
     lds_barrier();
     mark(1);
-    if (STORE12) lds_copy_out<400, 32, kA1S>(A1, a1 + (size_t)b * 12800);
+    if (STORE12) lds_copy_out_pitched<400, 32, kA1S, 20, kA1W>(A1, a1 + (size_t)b * 12800);
     // conv2: 4x4 stride 2 over A1 [20][20][32]; M = 81 (6 tiles), k-step s = tap (kh, kw) = (s >> 2, s & 3)
     conv_tiles<16, 4>(
         wave >> 2, 2, 6, w2,
         [&](int t, int s) {
           const int m = min(t * 16 + r, 80), p = m / 9, q = m - p * 9;
-          return A1 + ((2 * p + (s >> 2)) * 20 + 2 * q + (s & 3)) * kA1S + 8 * g;
+          return A1 + ((2 * p + (s >> 2)) * kA1W + 2 * q + (s & 3)) * kA1S + 8 * g;
         },
         [&](int) { return *reinterpret_cast<const float4*>(sbias + 32 + c2 + 4 * g); },
         [&](int t, f32x4 acc, float4 bv) {
-          const int m = t * 16 + r;
-          if (m < 81) *reinterpret_cast<uint2*>(A2 + m * kA2S + c2 + 4 * g) = bias_relu4(bv, acc);
+          const int m = t * 16 + r, p = m / 9;
+          if (m < 81) *reinterpret_cast<uint2*>(A2 + (p * kA2W + m - p * 9) * kA2S + c2 + 4 * g) = bias_relu4(bv, acc);
         });
     lds_barrier();
     mark(2);
-    if (STORE12) lds_copy_out<81, 64, kA2S>(A2, a2 + (size_t)b * 5184);
+    if (STORE12) lds_copy_out_pitched<81, 64, kA2S, 9, kA2W>(A2, a2 + (size_t)b * 5184);
     // conv3: 3x3 stride 1 over A2 [9][9][64]; M = 49 (4 tiles), k-step s: tap s >> 1, channel half s & 1
     conv_tiles<18, 3>(
         wave >> 2, 2, 4, w3,
         [&](int t, int s) {
           const int m = min(t * 16 + r, 48), p = m / 7, q = m - p * 7;
           const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
-          return A2 + ((p + kh) * 9 + q + kw) * kA2S + 32 * (s & 1) + 8 * g;
+          return A2 + ((p + kh) * kA2W + q + kw) * kA2S + 32 * (s & 1) + 8 * g;
         },
         [&](int) { return *reinterpret_cast<const float4*>(sbias + 96 + c2 + 4 * g); },
         [&](int t, f32x4 acc, float4 bv) {
@@ -422,22 +444,41 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
 // at +1), so every transposed-conv gather is an unconditional 16-byte LDS read.  W2^T (72 VGPRs) and the
 // parity-packed W1^T (32 VGPRs) are this lane's B fragments for the block's lifetime.
 constexpr int kPadS = 80;                  // padded image row stride (bf16)
-constexpr int kLdsPad = 121 * kPadS;       // [11][11][64 (+8)]
+// Padded images are 11 rows of kW3 / kW2 positions (11 used): the im2col rows a 16-lane read group gathers
+// run along an image row and wrap to the next one; with a row pitch of 17 (dz3, 9 output columns) / 18
+// (dz2, 10 columns) a wrap advances the position index by 1 mod 8, exactly like a step inside a row, so
+// the fragment reads stay bank-conflict-free across wraps (the 40-dword position stride repeats its
+// banks every 8 positions).
+constexpr int kW3 = 17, kW2 = 18;
+constexpr int kLdsPad3 = 11 * kW3 * kPadS, kLdsPad2 = 11 * kW2 * kPadS;
+constexpr int kLdsPad = kLdsPad3 + kLdsPad2;   // both images
 constexpr int kLdsA2M = 81 * 72;           // staged a2 (ReLU mask of dz2), row stride 72
-constexpr size_t kTrunkBwdLds = (size_t)(2 * kLdsPad + kLdsA2M + kLdsA1) * 2;
+constexpr size_t kTrunkBwdLds = (size_t)(kLdsPad + kLdsA2M + kLdsA1) * 2;
 
+// TIMING (development only): wave 0's s_memtime cycles per phase (staging + dz1 copy-out, dz2, dz1) ->
+// timing[blockIdx.x * 4 + phase]
+template <bool TIMING = false>
 __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16* __restrict__ dz3, const bf16* __restrict__ a2,
                                                                      const bf16* __restrict__ a1, int B,
                                                                      const bf16* __restrict__ wb2, const bf16* __restrict__ wb1,
-                                                                     bf16* __restrict__ dz2, bf16* __restrict__ dz1) {
+                                                                     bf16* __restrict__ dz2, bf16* __restrict__ dz1,
+                                                                     unsigned long long* __restrict__ timing) {
+  unsigned long long ph[4] = {0, 0, 0, 0}, tm = 0;
+  auto mark = [&](int i) {
+    if constexpr (TIMING) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (i >= 0) ph[i] += t - tm;
+      tm = t;
+    }
+  };
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   bf16* P3 = lds;                   // dz3, interior (oh + 2, ow + 2)
-  bf16* P2 = lds + kLdsPad;         // dz2 (masked), interior (oh + 1, ow + 1)
-  bf16* M2 = lds + 2 * kLdsPad;     // a2
+  bf16* P2 = lds + kLdsPad3;        // dz2 (masked), interior (oh + 1, ow + 1)
+  bf16* M2 = lds + kLdsPad;         // a2
   bf16* D1 = M2 + kLdsA2M;          // dz1 parity rows before masking: [400][32] in natural (ih, iw) order
   const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int r = lane & 15, g = lane >> 4;
-  for (int i = tid; i < 2 * kLdsPad / 8; i += kTrunkThreads) *reinterpret_cast<uint4*>(lds + i * 8) = uint4{0, 0, 0, 0};
+  for (int i = tid; i < kLdsPad / 8; i += kTrunkThreads) *reinterpret_cast<uint4*>(lds + i * 8) = uint4{0, 0, 0, 0};
   const int c3 = (wave & 3) * 16;       // phase A: the wave's 16 channels of dz2
   bf16x8 w3[18], w2[8];                 // A operands (row = lane & 15 of the wave's channel slice)
 #pragma unroll
@@ -489,13 +530,14 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
   prefetch(blockIdx.x);
   lds_barrier();   // borders zeroed
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    mark(-1);
     lds_barrier();   // previous sample's readers are done
 #pragma unroll
     for (int u = 0; u < kPB; ++u) {
       const int c = tid + u * kTrunkThreads;
       if (c < kC3) {
         const int row = c >> 3, col = (c & 7) * 8, oh = row / 7, ow = row - oh * 7;
-        *reinterpret_cast<uint4*>(P3 + ((oh + 2) * 11 + ow + 2) * kPadS + col) = pf[u];
+        *reinterpret_cast<uint4*>(P3 + ((oh + 2) * kW3 + ow + 2) * kPadS + col) = pf[u];
       } else if (c < kCT) {
         const int cc = c - kC3, row = cc >> 3, col = (cc & 7) * 8;
         *reinterpret_cast<uint4*>(M2 + row * 72 + col) = pf[u];
@@ -503,6 +545,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
     }
     if (b != (int)blockIdx.x) dz1_out(b - gridDim.x);
     lds_barrier();
+    mark(0);
     prefetch(b + gridDim.x);
     prefetch_mask(b);
     // phase A: dz2 (wave: channel slice c3, tiles wave >> 2, +2, ...)
@@ -511,24 +554,25 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
         [&](int t, int s) {
           const int m = min(t * 16 + r, 80), ih = m / 9, iw = m - ih * 9;
           const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3;
-          return P3 + ((ih + 2 - kh) * 11 + iw + 2 - kw) * kPadS + 32 * (s & 1) + 8 * g;
+          return P3 + ((ih + 2 - kh) * kW3 + iw + 2 - kw) * kPadS + 32 * (s & 1) + 8 * g;
         },
         [&](int t) { return *reinterpret_cast<const bf16x4*>(M2 + min(t * 16 + r, 80) * 72 + c3 + 4 * g); },
         [&](int t, f32x4 acc, bf16x4 act) {
           const int m = t * 16 + r;
           if (m < 81) {
             const int oh = m / 9, ow = m - oh * 9;
-            *reinterpret_cast<uint2*>(P2 + ((oh + 1) * 11 + ow + 1) * kPadS + c3 + 4 * g) =
+            *reinterpret_cast<uint2*>(P2 + ((oh + 1) * kW2 + ow + 1) * kPadS + c3 + 4 * g) =
                 pack4_bf16((float)act[0] > 0.0f ? acc[0] : 0.0f, (float)act[1] > 0.0f ? acc[1] : 0.0f,
                            (float)act[2] > 0.0f ? acc[2] : 0.0f, (float)act[3] > 0.0f ? acc[3] : 0.0f);
           }
         });
     lds_barrier();
+    mark(1);
     // dz2 -> global (81 x 64)
     for (int c = tid; c < 648; c += kTrunkThreads) {
       const int row = c >> 3, col = (c & 7) * 8, oh = row / 9, ow = row - oh * 9;
       *reinterpret_cast<uint4*>(dz2 + (size_t)b * 5184 + row * 64 + col) =
-          *reinterpret_cast<const uint4*>(P2 + ((oh + 1) * 11 + ow + 1) * kPadS + col);
+          *reinterpret_cast<const uint4*>(P2 + ((oh + 1) * kW2 + ow + 1) * kPadS + col);
     }
     // phase B: dz1 parity classes; wave = 16-column slice of N = p*32 + c (p = wave >> 1)
     {
@@ -538,7 +582,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
           [&](int t, int s) {
             const int m = min(t * 16 + r, 99), i = m / 10, j = m - i * 10;
             const int tp = s >> 1, th = tp >> 1, tw = tp & 1;
-            return P2 + ((i + 1 - th) * 11 + j + 1 - tw) * kPadS + 32 * (s & 1) + 8 * g;
+            return P2 + ((i + 1 - th) * kW2 + j + 1 - tw) * kPadS + 32 * (s & 1) + 8 * g;
           },
           [](int) { return 0; },
           [&](int t, f32x4 acc, int) {
@@ -551,6 +595,11 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_bwd_data(const bf16*
           });
     }
     lds_barrier();
+    mark(2);
+  }
+  if constexpr (TIMING) {
+    if (threadIdx.x == 0)
+      for (int i = 0; i < 4; ++i) timing[blockIdx.x * 4 + i] = ph[i];
   }
   lds_barrier();
   const int last = (int)blockIdx.x + ((B - 1 - (int)blockIdx.x) / (int)gridDim.x) * (int)gridDim.x;

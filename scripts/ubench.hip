@@ -132,7 +132,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "trunk") {
     set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
     set_lds_attr(k_trunk_fwd<false>, kTrunkFwdLds);
-    set_lds_attr(k_trunk_bwd_data, kTrunkBwdLds);
+    set_lds_attr(k_trunk_bwd_data<false>, kTrunkBwdLds);
+    set_lds_attr(k_trunk_bwd_data<true>, kTrunkBwdLds);
     set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
     // frames: random u8 s2d frames for BT samples
     {
@@ -164,6 +165,21 @@ int main(int argc, char** argv) {
                acc[0], acc[1], acc[2], acc[3], acc[0] + acc[1] + acc[2] + acc[3]);
       }
     }
+    {
+      unsigned long long* dt = nullptr;
+      QLX_HIP(hipMalloc(&dt, 256 * 4 * 8));
+      QLX_HIP(hipMemset(dt, 0, 256 * 4 * 8));
+      hipLaunchKernelGGL(k_trunk_bwd_data<true>, dim3(256), dim3(kTrunkThreads), kTrunkBwdLds, g_s, w.dz3, w.a2, w.a1, BT, m->wb2,
+                         m->wb1, w.dz2, w.dz1, dt);
+      QLX_HIP(hipDeviceSynchronize());
+      std::vector<unsigned long long> h(256 * 4);
+      QLX_HIP(hipMemcpy(h.data(), dt, h.size() * 8, hipMemcpyDeviceToHost));
+      double acc[4] = {0, 0, 0, 0};
+      for (int b = 0; b < 256; ++b)
+        for (int i = 0; i < 4; ++i) acc[i] += (double)h[b * 4 + i] / 256.0 / 32.0;
+      printf("trunk_bwd_data cycles per sample: stage+dz1out %.0f dz2 %.0f dz2out+dz1 %.0f total %.0f\n", acc[0], acc[1], acc[2],
+             acc[0] + acc[1] + acc[2]);
+    }
     for (int B : {256, 512, 1024, 2048, 4096, 8192}) {
       const double fwd_fl = 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576);
       const int grid = std::min(B, 256);
@@ -180,8 +196,8 @@ int main(int argc, char** argv) {
       }), fwd_fl, "TF/s");
       snprintf(nm, sizeof nm, "trunk_bwd_data B=%d", B);
       report(nm, time_us([&] {
-        hipLaunchKernelGGL(k_trunk_bwd_data, dim3(grid), dim3(kTrunkThreads), kTrunkBwdLds, g_s, w.dz3, w.a2, w.a1, B, m->wb2, m->wb1,
-                           w.dz2, w.dz1);
+        hipLaunchKernelGGL(k_trunk_bwd_data<false>, dim3(grid), dim3(kTrunkThreads), kTrunkBwdLds, g_s, w.dz3, w.a2, w.a1, B, m->wb2,
+                           m->wb1, w.dz2, w.dz1, nullptr);
       }), 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512), "TF/s");
       snprintf(nm, sizeof nm, "conv1_wgrad B=%d", B);
       report(nm, time_us([&] {
