@@ -28,7 +28,7 @@ PEAK_HBM_GBS = 8000.0         # HBM3E spec
 GEMM_SCOPES = ("trunk_fwd", "trunk_fwd_nostore", "trunk_bwd_data", "fc1_fwd", "fc1_bwd", "conv23_wgrad", "conv1_wgrad")
 # profiler scope -> the rocprofv3 kernel symbol it launches (for the committed PMC traffic lookup)
 SCOPE_KERNEL = {"trunk_fwd": "k_trunk_fwdILb1E", "trunk_fwd_nostore": "k_trunk_fwdILb0E", "trunk_bwd_data": "k_trunk_bwd_data",
-                "conv1_wgrad": "k_conv1_wgrad", "conv23_wgrad": "k_conv23_wgrad", "fc1_bwd": "k_gemm_pair"}
+                "conv1_wgrad": "k_conv1_wgrad", "conv23_wgrad": "k_conv23_wgrad", "fc1_bwd": "k_fc1_bwd"}
 HBM_SCOPES = ("adam", "env_step", "replay_push")
 
 

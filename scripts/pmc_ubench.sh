@@ -8,7 +8,7 @@ RE="${QLX_PMC_REGEX:-k_gemm}"
 run() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RE" --pmc "$@" --output-format csv -d gpurun_out/pmcu/$name -o c -- \
-    ./scripts/ubench gemm > gpurun_out/pmcu/$name.log 2>&1
+    ./scripts/ubench ${QLX_UB_MODE:-gemm} > gpurun_out/pmcu/$name.log 2>&1
 }
 run sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE || exit 1
 run mix SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE || exit 1
