@@ -235,3 +235,93 @@ size_t orc_state_size() { return sizeof(OrcState); }
 int orc_num_threads() { return omp_get_max_threads(); }
 
 }  // extern "C"
+
+// ---------------- BallGame (ballgame_ref.h) ----------------
+#include "ballgame_ref.h"
+
+extern "C" {
+
+size_t orc_bg_state_size() { return sizeof(BgState); }
+void orc_bg_initial_state(uint64_t seed, uint32_t env_id, uint32_t reset_count, BgState* out) {
+  Stream s(seed, env_id, reset_count, P_BALLGAME);
+  bg_random_initial_state(*out, s);
+  out->reset_count = reset_count;
+}
+// Environment::step on a caller-held state (seed / id only matter for resets, which the caller drives)
+void orc_bg_step(BgState* st, int action, float* reward, uint8_t* done) {
+  BgEnv e;
+  e.s = *st;
+  e.seed = 0;
+  e.id = 0;
+  bool d;
+  bg_env_step(e, (uint8_t)action, reward, &d);
+  *st = e.s;
+  *done = d ? 1 : 0;
+}
+void orc_bg_obs(const BgState* st, uint8_t* out) { bg_obs(*st, out); }
+uint64_t orc_gen_range_usize_single(uint64_t seed, uint32_t c1, uint32_t c2, uint32_t purpose, uint64_t start, uint64_t n) {
+  Stream s(seed, c1, c2, purpose, start);
+  return gen_range_usize_single(s, n);
+}
+
+void* orc_bg_net_new(uint64_t seed) { auto* n = new BgNet; bg_net_init_glorot(*n, seed); return n; }
+void orc_bg_net_free(void* h) { delete (BgNet*)h; }
+int orc_bg_var_size(int v) { return kBgVarSize[v]; }
+void orc_bg_net_get(void* h, int var, int which, float* out) {
+  BgNet* n = (BgNet*)h;
+  const auto& src = which == 0 ? n->w[var] : which == 1 ? n->m[var] : n->v[var];
+  std::memcpy(out, src.data(), src.size() * sizeof(float));
+}
+void orc_bg_net_set(void* h, int var, int which, const float* in) {
+  BgNet* n = (BgNet*)h;
+  auto& dst = which == 0 ? n->w[var] : which == 1 ? n->m[var] : n->v[var];
+  std::memcpy(dst.data(), in, dst.size() * sizeof(float));
+}
+void orc_bg_net_forward(void* h, const uint8_t* x, int B, float* q, float* a1, float* a2, float* a3) {
+  BgActs a;
+  bg_net_forward(*(BgNet*)h, x, B, a);
+  std::memcpy(q, a.q.data(), a.q.size() * 4);
+  if (a1) std::memcpy(a1, a.a1.data(), a.a1.size() * 4);
+  if (a2) std::memcpy(a2, a.a2.data(), a.a2.size() * 4);
+  if (a3) std::memcpy(a3, a.a3.data(), a.a3.size() * 4);
+}
+float orc_bg_net_train(void* h, const uint8_t* x, const uint8_t* actions, const float* y, int B, float* grads_out,
+                       float* norms_out) {
+  BgNet* n = (BgNet*)h;
+  BgActs a;
+  bg_net_forward(*n, x, B, a);
+  BgGrads g;
+  const float loss = bg_net_loss_backward(*n, x, actions, y, B, a, g);
+  if (grads_out) {
+    size_t off = 0;
+    for (int v = 0; v < kBgVars; ++v) { std::memcpy(grads_out + off, g.g[v].data(), kBgVarSize[v] * 4); off += kBgVarSize[v]; }
+  }
+  bg_net_apply_adam(*n, g, norms_out);
+  return loss;
+}
+
+void* orc_bg_learner_new(const BgParams* p) { return new BgLearner(*p); }
+void orc_bg_learner_free(void* h) { delete (BgLearner*)h; }
+void orc_bg_learner_vector_step(void* h) { ((BgLearner*)h)->vector_step(); }
+void* orc_bg_learner_net(void* h, int which) { BgLearner* l = (BgLearner*)h; return which == 0 ? (void*)&l->online : (void*)&l->target; }
+void orc_bg_learner_counters(void* h, uint64_t* out /*[6]*/, double* eps, float* running_reward) {
+  BgLearner* l = (BgLearner*)h;
+  out[0] = l->step_count; out[1] = l->vec_steps; out[2] = l->update_count; out[3] = l->episode_count;
+  out[4] = l->replay.size(); out[5] = l->solved() ? 1 : 0;
+  *eps = l->epsilon; *running_reward = l->running_reward;
+}
+int orc_bg_learner_last(void* h, uint8_t* actions, float* rewards, uint8_t* dones, float* losses, uint64_t* indices,
+                        float* targets) {
+  BgLearner* l = (BgLearner*)h;
+  const size_t N = l->p.n_envs;
+  if (actions) std::memcpy(actions, l->last_actions.data(), N);
+  if (rewards) std::memcpy(rewards, l->last_rewards.data(), N * 4);
+  if (dones) std::memcpy(dones, l->last_dones.data(), N);
+  if (losses) std::memcpy(losses, l->last_losses.data(), l->last_losses.size() * 4);
+  if (indices) std::memcpy(indices, l->last_indices.data(), l->last_indices.size() * 8);
+  if (targets) std::memcpy(targets, l->last_targets.data(), l->last_targets.size() * 4);
+  return (int)l->last_losses.size();
+}
+void orc_bg_learner_env_state(void* h, uint32_t e, BgState* out) { *out = ((BgLearner*)h)->envs[e].s; }
+
+}  // extern "C"

@@ -57,6 +57,15 @@ def default_params(**kw):
     return p
 
 
+# BallGame state (oracle/ballgame_ref.h BgState = qlx_ballgame_state): field[x*3+y] in
+# {0 empty, 1 goal, 2 ball, 3 obstacle}
+BG_STATE_DTYPE = np.dtype([("field", "u1", (9,)), ("ball_x", "u1"), ("ball_y", "u1"), ("pad", "u1"), ("steps", "<u4"),
+                           ("reset_count", "<u4")])
+assert BG_STATE_DTYPE.itemsize == 20
+BG_VAR_SHAPES = [(2, 2, 4, 32), (32,), (1, 1, 32, 32), (32,), (288, 512), (512,), (512, 5), (5,)]
+BG_VAR_SIZES = [int(np.prod(s)) for s in BG_VAR_SHAPES]
+P_BALLGAME = 6
+
 VAR_SHAPES = [(8, 8, 4, 32), (32,), (4, 4, 32, 64), (64,), (3, 3, 64, 64), (64,), (3136, 512), (512,), (512, 3), (3,)]
 VAR_SIZES = [int(np.prod(s)) for s in VAR_SHAPES]
 STATE_BYTES = 84 * 84 * 4
@@ -123,6 +132,32 @@ def lib():
         L.orc_learner_replay_get.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.orc_learner_params_size.restype = C.c_size_t
         L.orc_state_size.restype = C.c_size_t
+        # BallGame (oracle/ballgame_ref.h)
+        L.orc_bg_state_size.restype = C.c_size_t
+        L.orc_bg_initial_state.argtypes = [u64, u32, u32, vp]
+        L.orc_bg_step.argtypes = [vp, i32, vp, vp]
+        L.orc_bg_obs.argtypes = [vp, vp]
+        L.orc_gen_range_usize_single.argtypes = [u64, u32, u32, u32, u64, u64]
+        L.orc_gen_range_usize_single.restype = u64
+        L.orc_bg_net_new.argtypes = [u64]
+        L.orc_bg_net_new.restype = vp
+        L.orc_bg_net_free.argtypes = [vp]
+        L.orc_bg_net_get.argtypes = [vp, i32, i32, vp]
+        L.orc_bg_net_set.argtypes = [vp, i32, i32, vp]
+        L.orc_bg_net_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.orc_bg_net_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
+        L.orc_bg_net_train.restype = f32
+        L.orc_bg_learner_new.argtypes = [C.POINTER(LearnerParams)]
+        L.orc_bg_learner_new.restype = vp
+        L.orc_bg_learner_free.argtypes = [vp]
+        L.orc_bg_learner_vector_step.argtypes = [vp]
+        L.orc_bg_learner_net.argtypes = [vp, i32]
+        L.orc_bg_learner_net.restype = vp
+        L.orc_bg_learner_counters.argtypes = [vp, vp, C.POINTER(C.c_double), C.POINTER(C.c_float)]
+        L.orc_bg_learner_last.argtypes = [vp] * 7
+        L.orc_bg_learner_last.restype = i32
+        L.orc_bg_learner_env_state.argtypes = [vp, u32, vp]
+        assert L.orc_bg_state_size() == BG_STATE_DTYPE.itemsize
         assert L.orc_learner_params_size() == C.sizeof(LearnerParams)
         assert L.orc_state_size() == STATE_DTYPE.itemsize
         _lib = L
@@ -343,3 +378,123 @@ class Learner:
         d = np.zeros(B, np.uint8)
         lib().orc_learner_replay_get(self.h, _p(idx), B, _p(s), _p(sn), _p(a), _p(r), _p(d))
         return s, sn, a, r, d
+
+
+# ---------------- BallGame ----------------
+def bg_initial_state(seed, env_id, reset_count=0):
+    st = np.zeros(1, dtype=BG_STATE_DTYPE)
+    lib().orc_bg_initial_state(seed, env_id, reset_count, _p(st))
+    return st
+
+
+def bg_step(st, action):
+    """Environment::step on a 1-element BG_STATE_DTYPE array (in place): (reward, done)."""
+    r = np.zeros(1, np.float32)
+    d = np.zeros(1, np.uint8)
+    lib().orc_bg_step(_p(st), int(action), _p(r), _p(d))
+    return float(r[0]), bool(d[0])
+
+
+def bg_obs(st):
+    out = np.zeros((3, 3, 4), np.uint8)
+    lib().orc_bg_obs(_p(st), _p(out))
+    return out
+
+
+def bg_state_from_field(field, ball, steps=0):
+    st = np.zeros(1, dtype=BG_STATE_DTYPE)
+    st["field"][0] = np.asarray(field, np.uint8).reshape(9)
+    st["ball_x"], st["ball_y"], st["steps"] = ball[0], ball[1], steps
+    return st
+
+
+def gen_range_usize_single(seed, c1, c2, purpose, start, n):
+    return int(lib().orc_gen_range_usize_single(seed, c1, c2, purpose, start, n))
+
+
+class BgNet:
+    def __init__(self, seed=2, handle=None, owned=True):
+        self.h = handle if handle is not None else lib().orc_bg_net_new(seed)
+        self.owned = owned and handle is None
+
+    def __del__(self):
+        if getattr(self, "owned", False) and getattr(self, "h", None):
+            if _lib is not None:
+                _lib.orc_bg_net_free(self.h)
+            self.h = None
+
+    def get(self, var, which=0):
+        out = np.zeros(BG_VAR_SIZES[var], np.float32)
+        lib().orc_bg_net_get(self.h, var, which, _p(out))
+        return out.reshape(BG_VAR_SHAPES[var])
+
+    def set(self, var, arr, which=0):
+        a = np.ascontiguousarray(arr, dtype=np.float32).reshape(-1)
+        assert a.size == BG_VAR_SIZES[var]
+        lib().orc_bg_net_set(self.h, var, which, _p(a))
+
+    def weights(self):
+        return [self.get(v) for v in range(8)]
+
+    def forward(self, x, acts=False):
+        x = np.ascontiguousarray(x, dtype=np.uint8)
+        B = x.shape[0]
+        q = np.zeros((B, 5), np.float32)
+        a1, a2, a3 = (np.zeros((B, 288), np.float32), np.zeros((B, 288), np.float32), np.zeros((B, 512), np.float32))
+        lib().orc_bg_net_forward(self.h, _p(x), B, _p(q), _p(a1), _p(a2), _p(a3))
+        return (q, a1, a2, a3) if acts else q
+
+    def train(self, x, actions, y):
+        x = np.ascontiguousarray(x, dtype=np.uint8)
+        a = np.ascontiguousarray(actions, dtype=np.uint8)
+        y = np.ascontiguousarray(y, dtype=np.float32)
+        g = np.zeros(sum(BG_VAR_SIZES), np.float32)
+        nrm = np.zeros(8, np.float32)
+        loss = lib().orc_bg_net_train(self.h, _p(x), _p(a), _p(y), x.shape[0], _p(g), _p(nrm))
+        return loss, g, nrm
+
+
+class BgLearner:
+    def __init__(self, params):
+        self.params = params
+        self.N = params.n_envs
+        self.B = params.batch_size
+        self.h = lib().orc_bg_learner_new(C.byref(params))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            if _lib is not None:
+                _lib.orc_bg_learner_free(self.h)
+            self.h = None
+
+    def vector_step(self):
+        lib().orc_bg_learner_vector_step(self.h)
+
+    def counters(self):
+        out = np.zeros(6, dtype=np.uint64)
+        eps = C.c_double()
+        rr = C.c_float()
+        lib().orc_bg_learner_counters(self.h, _p(out), C.byref(eps), C.byref(rr))
+        keys = ["step_count", "vec_steps", "update_count", "episode_count", "replay_len", "solved"]
+        d = {k: int(v) for k, v in zip(keys, out)}
+        d["epsilon"] = eps.value
+        d["running_reward"] = rr.value
+        return d
+
+    def last(self, max_updates=4096):
+        N, B = self.N, self.B
+        a, r, d = np.zeros(N, np.uint8), np.zeros(N, np.float32), np.zeros(N, np.uint8)
+        losses = np.zeros(max_updates, np.float32)
+        idx = np.zeros(max_updates * B, np.uint64)
+        tg = np.zeros(max_updates * B, np.float32)
+        n = lib().orc_bg_learner_last(self.h, _p(a), _p(r), _p(d), _p(losses), _p(idx), _p(tg))
+        return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
+                    targets=tg[:n * B].reshape(n, B))
+
+    def net(self, which=0):
+        return BgNet(handle=lib().orc_bg_learner_net(self.h, which), owned=False)
+
+    def env_state(self, e):
+        s = np.zeros(1, dtype=BG_STATE_DTYPE)
+        lib().orc_bg_learner_env_state(self.h, e, _p(s))
+        return s[0]
