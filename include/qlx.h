@@ -10,6 +10,9 @@
  *   generate_distinct_random_ids        src/ql-with-tensorflow/src/learn/self_driving_tf_q_learner.rs:276-296
  *   DeepQLearningModel                  src/ql-with-tensorflow/src/ml_model/model.rs:29-77
  *   SelfDrivingQLearner / Parameter     src/ql-with-tensorflow/src/learn/self_driving_tf_q_learner.rs:20-139
+ *   BallGameTestEnvironment (2nd env)   src/ql/src/test/ballgame_test_environment.rs:12-262,
+ *                                        src/ql-with-tensorflow/src/test/ballgame_test_env_addons.rs:7-50,
+ *                                        src/ql-with-tensorflow/python_model/create_ql_model_ballgame_3x3x4_5_512.py
  *
  * Conventions
  *   - Opaque handles; every call returns int32_t status (QLX_OK = 0, < 0 = error) and
@@ -42,6 +45,7 @@ extern "C" {
 #define QLX_E_IO (-6)
 
 #define QLX_ENV_BREAKOUT 1
+#define QLX_ENV_BALLGAME 2
 #define QLX_ARCH_NATURE_DQN 1 /* Conv(32,8,s4)-Conv(64,4,s2)-Conv(64,3,s1)-Dense512-Dense3 */
 
 const char* qlx_last_error(void);
@@ -59,9 +63,9 @@ typedef struct qlx_breakout_state {
 
 typedef struct qlx_env qlx_env;
 
-/* Action::ACTION_SPACE (breakout_environment.rs:103) */
+/* Action::ACTION_SPACE (breakout_environment.rs:103; BallGame 5, ballgame_test_environment.rs:239) */
 int32_t qlx_env_action_space(int32_t kind);
-/* Environment::episode_reward_goal_mean (breakout_environment.rs:203-206): bricks - 1 = 59 */
+/* Environment::episode_reward_goal_mean (breakout_environment.rs:203-206): bricks - 1 = 59; BallGame 9.5 (:88) */
 float qlx_env_reward_goal_mean(int32_t kind);
 
 /* BreakoutEnvironment::new x n_envs on `device`; env i draws its ball launch angle from the
@@ -200,6 +204,57 @@ int32_t qlx_learner_profile_filter(qlx_learner* l, const char* name_or_null);
 int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* total_us, double* total_work,
                                 uint64_t* launches);
 int32_t qlx_learner_profile_names(qlx_learner* l, char* buf, size_t cap);
+
+/* ---------------- BallGame (BallGameTestEnvironment + its 3x3x4 -> 5 Q-model) ----------------
+ * The reference's second Environment / DeepQLearningModel pair, batched on the GPU.  Same conventions as
+ * above; actions West 0, North 1, East 2, South 3, Nothing 4 (ballgame_test_environment.rs:240-249). */
+
+typedef struct qlx_ballgame_state { /* BallGameState (:92-97) */
+  uint8_t field[9];                  /* index x * 3 + y: 0 empty, 1 goal, 2 ball, 3 obstacle */
+  uint8_t ball_x, ball_y, pad;
+  uint32_t steps;
+  uint32_t reset_count;
+} qlx_ballgame_state;
+
+typedef struct qlx_bg_env qlx_bg_env;
+/* BallGameTestEnvironment::new x n_envs: env i's random_initial_state (:100-123) draws gen_range(0..3) from
+ * the build's stream (seed, i, reset_count, purpose 6) instead of thread_rng. */
+int32_t qlx_bg_env_create(uint32_t n_envs, uint64_t seed, int32_t device, qlx_bg_env** out);
+int32_t qlx_bg_env_destroy(qlx_bg_env* env);
+int32_t qlx_bg_env_reset(qlx_bg_env* env, const uint8_t* mask_or_null);
+/* Environment::step (:69-86) for all envs (host arrays of n_envs; actions >= 5 fail with QLX_E_INVALID). */
+int32_t qlx_bg_env_step(qlx_bg_env* env, const uint8_t* actions, float* rewards, uint8_t* dones);
+/* to_multi_dim_array: out[n][3][3][4] u8 one-hot (x, y, channel = entry). */
+int32_t qlx_bg_env_obs(qlx_bg_env* env, uint8_t* out);
+int32_t qlx_bg_env_states(qlx_bg_env* env, qlx_ballgame_state* out);
+int32_t qlx_bg_env_set_states(qlx_bg_env* env, const qlx_ballgame_state* in);
+
+typedef struct qlx_bg_model qlx_bg_model;
+/* Conv(32, 2x2 same)-Conv(32, 1x1)-Dense512-Dense5 in fp32; GlorotUniform from stream (seed, var, 1);
+ * 8 variables k0 [2,2,4,32] b0 k1 [1,1,32,32] b1 k2 [288,512] b2 k3 [512,5] b3. */
+int32_t qlx_bg_model_create(uint64_t seed, int32_t device, qlx_bg_model** out);
+int32_t qlx_bg_model_destroy(qlx_bg_model* m);
+int64_t qlx_bg_model_var_size(int32_t var);
+int32_t qlx_bg_model_get_var(qlx_bg_model* m, int32_t var, int32_t which, float* out);
+int32_t qlx_bg_model_set_var(qlx_bg_model* m, int32_t var, int32_t which, const float* in);
+int64_t qlx_bg_model_iterations(qlx_bg_model* m);
+int32_t qlx_bg_model_predict(qlx_bg_model* m, const uint8_t* obs /*[n][3][3][4]*/, uint32_t n, float* q_out, uint8_t* actions);
+int32_t qlx_bg_model_batch_max_q(qlx_bg_model* m, const uint8_t* obs, uint32_t n, float* out);
+/* train_model (.py:71-85): MSE of q_a, backward, clip_by_norm(1) per variable, Adam. */
+int32_t qlx_bg_model_train(qlx_bg_model* m, const uint8_t* obs, const uint8_t* actions, const float* y, uint32_t batch,
+                           float* loss_out, float* grads_out, float* norms_out);
+
+typedef struct qlx_bg_learner qlx_bg_learner;
+/* SelfDrivingQLearner over BallGame (same qlx_params and vector-step semantics as qlx_learner). */
+int32_t qlx_bg_learner_create(const qlx_params* p, int32_t device, qlx_bg_learner** out);
+int32_t qlx_bg_learner_destroy(qlx_bg_learner* l);
+int32_t qlx_bg_learner_run(qlx_bg_learner* l, uint64_t n_vector_steps);
+int32_t qlx_bg_learner_sync(qlx_bg_learner* l);
+int32_t qlx_bg_learner_stats_get(qlx_bg_learner* l, qlx_learner_stats* out);
+int32_t qlx_bg_learner_last(qlx_bg_learner* l, uint8_t* actions, float* rewards, uint8_t* dones, float* losses,
+                            uint64_t* indices, float* targets, uint32_t* n_updates);
+qlx_bg_env* qlx_bg_learner_env(qlx_bg_learner* l);
+qlx_bg_model* qlx_bg_learner_model(qlx_bg_learner* l, int32_t which /* 0 online, 1 target */);
 
 #ifdef __cplusplus
 }

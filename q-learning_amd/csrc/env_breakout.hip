@@ -484,8 +484,10 @@ using namespace qlx;
 
 extern "C" {
 
-int32_t qlx_env_action_space(int32_t kind) { return kind == QLX_ENV_BREAKOUT ? kActions : -1; }
-float qlx_env_reward_goal_mean(int32_t kind) { return kind == QLX_ENV_BREAKOUT ? (float)(kNumBricks - 1) : -1.0f; }
+int32_t qlx_env_action_space(int32_t kind) { return kind == QLX_ENV_BREAKOUT ? kActions : kind == QLX_ENV_BALLGAME ? 5 : -1; }
+float qlx_env_reward_goal_mean(int32_t kind) {
+  return kind == QLX_ENV_BREAKOUT ? (float)(kNumBricks - 1) : kind == QLX_ENV_BALLGAME ? 9.5f : -1.0f;
+}
 
 int32_t qlx_env_create(int32_t kind, uint32_t n_envs, uint64_t seed, int32_t device, qlx_env** out) {
   return guard([&] {

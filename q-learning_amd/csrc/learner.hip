@@ -28,9 +28,9 @@ ReplayView replay_view(const qlx_replay* rb);
 // ---- acting: epsilon-greedy (self_driving_tf_q_learner.rs:153-167) --------------------------
 // step_count of env e in this vector step = step_before + e + 1; epsilon used = eps_table[step_count - 1]
 // (value after step_count - 1 decrements). Draws: f64 from words 0-1, the random action from word 2 on.
-__global__ void k_select_actions(uint32_t n, uint64_t step_before, uint64_t pure_random, const double* eps_table,
-                                 uint64_t eps_len, double eps_min, uint64_t seed, uint32_t id_offset, uint32_t vec_step,
-                                 const float* q, uint8_t* actions) {
+__global__ void k_select_actions(uint32_t n, uint32_t n_actions, uint64_t step_before, uint64_t pure_random,
+                                 const double* eps_table, uint64_t eps_len, double eps_min, uint64_t seed, uint32_t id_offset,
+                                 uint32_t vec_step, const float* q, uint8_t* actions) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const uint64_t sc = step_before + e + 1;
@@ -43,25 +43,26 @@ __global__ void k_select_actions(uint32_t n, uint64_t step_before, uint64_t pure
   uint8_t a;
   if (random) {
     RngStream sa(seed, id_offset + e, vec_step, P_ACT, 2);
-    a = (uint8_t)uniform_u8(sa, kActions);
+    a = (uint8_t)uniform_u8(sa, n_actions);
   } else {   // tf.argmax over Q(s): first maximal index
-    const float q0 = q[e * 3], q1 = q[e * 3 + 1], q2 = q[e * 3 + 2];
     int best = 0;
-    float bv = q0;
-    if (q1 > bv) { best = 1; bv = q1; }
-    if (q2 > bv) best = 2;
+    float bv = q[e * n_actions];
+    for (uint32_t j = 1; j < n_actions; ++j)
+      if (q[e * n_actions + j] > bv) { best = (int)j; bv = q[e * n_actions + j]; }
     a = (uint8_t)best;
   }
   actions[e] = a;
 }
 
+void launch_select_actions(hipStream_t s, uint32_t n, uint32_t n_actions, uint64_t step_before, uint64_t pure_random,
+                           const double* eps_table, uint64_t eps_len, double eps_min, uint64_t seed, uint32_t id_offset,
+                           uint32_t vec_step, const float* q, uint8_t* actions) {
+  hipLaunchKernelGGL(k_select_actions, dim3((n + 255) / 256), dim3(256), 0, s, n, n_actions, step_before, pure_random, eps_table,
+                     eps_len, eps_min, seed, id_offset, vec_step, q, actions);
+  QLX_HIP(hipGetLastError());
+}
+
 // ---- episode bookkeeping (learn_episode :172-174, :214-224) -----------------------------------
-struct Book {
-  uint64_t episode_count;
-  float running_reward;
-  uint32_t hist_len;     // current entries in the episode reward ring
-  uint32_t hist_head;    // index of the oldest entry
-};
 
 // One wave, envs in order: ep_reward += r; an env whose episode ended (done, or max_steps_per_episode
 // steps) pushes its reward into the FIFO of episode rewards, counts the episode and is marked for reset.
@@ -107,6 +108,34 @@ __global__ __launch_bounds__(64) void k_episode_book(uint32_t n, const float* re
     }
     *book = b;
   }
+}
+
+void launch_episode_book(hipStream_t s, uint32_t n, const float* rewards, const uint8_t* dones, const uint32_t* ep_steps,
+                         uint64_t max_steps, float* ep_reward, float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask) {
+  hipLaunchKernelGGL(k_episode_book, dim3(1), dim3(64), 0, s, n, rewards, dones, ep_steps, max_steps, ep_reward, hist, hist_cap,
+                     book, reset_mask);
+  QLX_HIP(hipGetLastError());
+}
+
+std::vector<double> epsilon_table(const qlx_params& p) {
+  std::vector<double> eps;
+  double e = p.epsilon_max;
+  const double delta = (p.epsilon_max - p.epsilon_min) / p.epsilon_greedy_steps;
+  const size_t cap = 1u << 26;
+  while (eps.size() < cap) {
+    eps.push_back(e);
+    if (e <= p.epsilon_min) break;
+    e = std::max(e - delta, p.epsilon_min);
+  }
+  return eps;
+}
+
+void learner_book_stats(const Book& b, const float* ring, uint32_t ring_cap, float goal, float pct, float* running, uint64_t* solved) {
+  *running = b.running_reward;
+  if (b.hist_len == 0) { *solved = 0; return; }
+  float mn = ring[b.hist_head % ring_cap];
+  for (uint32_t i = 0; i < b.hist_len; ++i) mn = std::min(mn, ring[(b.hist_head + i) % ring_cap]);
+  *solved = (b.running_reward >= goal && mn >= goal * pct) ? 1 : 0;
 }
 
 // ---- replay sample gather: frame pointer tables + metadata of one update ------------------------
@@ -232,9 +261,8 @@ static void learner_vector_step(qlx_learner* L) {
   }
   {
     ProfScope ps(&L->prof, "select", s);
-    hipLaunchKernelGGL(k_select_actions, dim3((N + 255) / 256), dim3(256), 0, s, N, step_before,
-                       L->p.epsilon_pure_random_steps, L->d_eps, L->eps_len, L->p.epsilon_min, L->p.learner_seed,
-                       (uint32_t)L->rank * N, (uint32_t)L->vec_steps, L->online->w.q, L->d_actions);
+    launch_select_actions(s, N, kActions, step_before, L->p.epsilon_pure_random_steps, L->d_eps, L->eps_len, L->p.epsilon_min,
+                          L->p.learner_seed, (uint32_t)L->rank * N, (uint32_t)L->vec_steps, L->online->w.q, L->d_actions);
   }
   L->step_count += N;
   // ---- env step (physics + frame) and replay push
@@ -248,9 +276,8 @@ static void learner_vector_step(qlx_learner* L) {
   }
   {
     ProfScope ps(&L->prof, "episode_reset", s);
-    hipLaunchKernelGGL(k_episode_book, dim3(1), dim3(64), 0, s, N, L->d_rewards, L->d_dones, L->env->d_ep_steps,
-                       L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
-                       (uint32_t)L->p.episode_reward_history_buffer_len, L->d_book, L->d_reset);
+    launch_episode_book(s, N, L->d_rewards, L->d_dones, L->env->d_ep_steps, L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
+                        (uint32_t)L->p.episode_reward_history_buffer_len, L->d_book, L->d_reset);
     env_launch_reset(L->env, L->d_reset, 1);
   }
   // ---- training updates
@@ -338,15 +365,7 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       env_launch_reset(L->env, nullptr, 0);
     }
     // epsilon table: eps_k after k decrements, k = 0.. until epsilon_min (repeated f64 subtraction)
-    std::vector<double> eps;
-    double e = p->epsilon_max;
-    const double delta = (p->epsilon_max - p->epsilon_min) / p->epsilon_greedy_steps;
-    const size_t cap = 1u << 26;
-    while (eps.size() < cap) {
-      eps.push_back(e);
-      if (e <= p->epsilon_min) break;
-      e = std::max(e - delta, p->epsilon_min);
-    }
+    const std::vector<double> eps = epsilon_table(*p);
     L->eps_len = eps.size();
     QLX_HIP(hipMalloc(&L->d_eps, eps.size() * sizeof(double)));
     QLX_HIP(hipMemcpy(L->d_eps, eps.data(), eps.size() * sizeof(double), hipMemcpyHostToDevice));

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "qlx_internal.h"
 
@@ -44,6 +45,26 @@ struct qlx_replay {
 };
 
 namespace qlx {
+// episode bookkeeping state of a learner (learner.hip k_episode_book)
+struct Book {
+  uint64_t episode_count;
+  float running_reward;
+  uint32_t hist_len;     // current entries in the episode reward ring
+  uint32_t hist_head;    // index of the oldest entry
+};
+// shared launchers of the learner loop (learner.hip / replay.hip), used by both environments' learners
+void launch_episode_book(hipStream_t s, uint32_t n, const float* rewards, const uint8_t* dones, const uint32_t* ep_steps,
+                         uint64_t max_steps, float* ep_reward, float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask);
+void launch_select_actions(hipStream_t s, uint32_t n, uint32_t n_actions, uint64_t step_before, uint64_t pure_random,
+                           const double* eps_table, uint64_t eps_len, double eps_min, uint64_t seed, uint32_t id_offset,
+                           uint32_t vec_step, const float* q, uint8_t* actions);
+void launch_sample_distinct(hipStream_t s, uint64_t seed, uint32_t first_update, uint32_t n_updates, uint32_t rank, uint64_t len,
+                            uint32_t batch, uint64_t* d_out);
+// epsilon after k decrements, k = 0 .. until epsilon_min (repeated f64 subtraction, learn_episode :164-167)
+std::vector<double> epsilon_table(const qlx_params& p);
+// solved() over the episode reward ring (self_driving_tf_q_learner.rs:134-139)
+void learner_book_stats(const Book& b, const float* ring, uint32_t ring_cap, float goal, float pct, float* running, uint64_t* solved);
+
 void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, uint8_t* d_dones);
 void env_launch_reset(qlx_env* env, const uint8_t* d_mask, int bump);
 void replay_launch_push(qlx_replay* rb, qlx_env* env, hipStream_t s, const uint8_t* d_actions, const float* d_rewards,

@@ -62,7 +62,7 @@ constexpr int kNumBricks = 60;
 __host__ __device__ inline int s2d_offset(int x, int y) { return ((x >> 2) * kBlocks + (y >> 2)) * 16 + (x & 3) * 4 + (y & 3); }
 
 // ---- Philox4x32-10 counter-based RNG (build-defined stream) ------------
-enum Purpose : uint32_t { P_BALL = 1, P_ACT = 2, P_SAMPLE = 3, P_INIT = 4, P_SYNTH = 5 };
+enum Purpose : uint32_t { P_BALL = 1, P_ACT = 2, P_SAMPLE = 3, P_INIT = 4, P_SYNTH = 5, P_BALLGAME = 6 };
 
 __host__ __device__ inline void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                                        uint32_t out[4]) {
@@ -131,6 +131,16 @@ __host__ __device__ inline uint32_t uniform_u8(RngStream& s, uint32_t n) {
   for (;;) {
     const uint64_t m = (uint64_t)s.u32() * n;
     if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+  }
+}
+
+// rand 0.8.5 UniformInt<usize>::sample_single_inclusive(0, n - 1) (`rng.gen_range(0..n)` on usize): u64 draws,
+// zone = (range << leading_zeros(range)) - 1
+__host__ __device__ inline uint64_t uniform_usize_single(RngStream& s, uint64_t n) {
+  const uint64_t zone = (n << __builtin_clzll(n)) - 1;
+  for (;;) {
+    const unsigned __int128 m = (unsigned __int128)s.u64() * n;
+    if ((uint64_t)m <= zone) return (uint64_t)(m >> 64);
   }
 }
 

@@ -129,6 +129,20 @@ def lib():
         "qlx_learner_profile_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)], i32),
         "qlx_learner_profile_filter": ([vp, C.c_char_p], i32),
         "qlx_learner_profile_names": ([vp, C.c_char_p, C.c_size_t], i32),
+        # BallGame
+        "qlx_bg_env_create": ([u32, u64, i32, C.POINTER(vp)], i32), "qlx_bg_env_destroy": ([vp], i32),
+        "qlx_bg_env_reset": ([vp, u8p], i32), "qlx_bg_env_step": ([vp, u8p, vp, u8p], i32),
+        "qlx_bg_env_obs": ([vp, u8p], i32), "qlx_bg_env_states": ([vp, vp], i32), "qlx_bg_env_set_states": ([vp, vp], i32),
+        "qlx_bg_model_create": ([u64, i32, C.POINTER(vp)], i32), "qlx_bg_model_destroy": ([vp], i32),
+        "qlx_bg_model_var_size": ([i32], C.c_int64), "qlx_bg_model_get_var": ([vp, i32, i32, vp], i32),
+        "qlx_bg_model_set_var": ([vp, i32, i32, vp], i32), "qlx_bg_model_iterations": ([vp], C.c_int64),
+        "qlx_bg_model_predict": ([vp, vp, u32, vp, vp], i32), "qlx_bg_model_batch_max_q": ([vp, vp, u32, vp], i32),
+        "qlx_bg_model_train": ([vp, vp, vp, vp, u32, vp, vp, vp], i32),
+        "qlx_bg_learner_create": ([C.POINTER(Params), i32, C.POINTER(vp)], i32), "qlx_bg_learner_destroy": ([vp], i32),
+        "qlx_bg_learner_run": ([vp, u64], i32), "qlx_bg_learner_sync": ([vp], i32),
+        "qlx_bg_learner_stats_get": ([vp, C.POINTER(LearnerStats)], i32),
+        "qlx_bg_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
+        "qlx_bg_learner_env": ([vp], vp), "qlx_bg_learner_model": ([vp, i32], vp),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name, None)
@@ -416,3 +430,169 @@ def dist_unique_id():
     buf = (C.c_uint8 * 128)()
     _check(lib().qlx_dist_unique_id(buf))
     return bytes(buf)
+
+
+# ---------------- BallGame (the reference's second environment / model pair) ----------------
+BG_ACTION_SPACE = 5
+BG_VAR_SHAPES = [(2, 2, 4, 32), (32,), (1, 1, 32, 32), (32,), (288, 512), (512,), (512, 5), (5,)]
+BG_STATE_DTYPE = np.dtype([("field", "u1", (9,)), ("ball_x", "u1"), ("ball_y", "u1"), ("pad", "u1"), ("steps", "<u4"),
+                           ("reset_count", "<u4")])
+
+
+class BallGameEnvironment:
+    """Batched `impl Environment for BallGameTestEnvironment` (ballgame_test_environment.rs:59-89)."""
+
+    ACTION_SPACE = BG_ACTION_SPACE
+
+    def __init__(self, n_envs=1, seed=0xBA11, device=0, handle=None):
+        self._owned = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            _check(lib().qlx_bg_env_create(n_envs, seed, device, C.byref(h)))
+            handle = h.value
+        self.h = handle
+        self.n = n_envs
+
+    def close(self):
+        if getattr(self, "_owned", False) and getattr(self, "h", None):
+            lib().qlx_bg_env_destroy(self.h)
+        self.h = None
+
+    __del__ = close
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        _check(lib().qlx_bg_env_reset(self.h, _p(m)))
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.uint8)
+        r = np.zeros(self.n, np.float32)
+        d = np.zeros(self.n, np.uint8)
+        _check(lib().qlx_bg_env_step(self.h, _p(a), _p(r), _p(d)))
+        return r, d.astype(bool)
+
+    def state(self):
+        out = np.zeros((self.n, 3, 3, 4), np.uint8)
+        _check(lib().qlx_bg_env_obs(self.h, _p(out)))
+        return out
+
+    def states(self):
+        out = np.zeros(self.n, dtype=BG_STATE_DTYPE)
+        _check(lib().qlx_bg_env_states(self.h, _p(out)))
+        return out
+
+    def set_states(self, st):
+        a = np.ascontiguousarray(st, dtype=BG_STATE_DTYPE)
+        assert a.shape == (self.n,)
+        _check(lib().qlx_bg_env_set_states(self.h, _p(a)))
+
+    @staticmethod
+    def episode_reward_goal_mean():
+        return float(lib().qlx_env_reward_goal_mean(2))
+
+
+class BallGameModel:
+    """The 3x3x4 -> 5 Q-model (create_ql_model_ballgame_3x3x4_5_512.py) in fp32 HIP kernels."""
+
+    def __init__(self, seed=2, device=0, handle=None):
+        self._owned = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            _check(lib().qlx_bg_model_create(seed, device, C.byref(h)))
+            handle = h.value
+        self.h = handle
+
+    def close(self):
+        if getattr(self, "_owned", False) and getattr(self, "h", None):
+            lib().qlx_bg_model_destroy(self.h)
+        self.h = None
+
+    __del__ = close
+
+    def get(self, var, which=0):
+        out = np.zeros(int(np.prod(BG_VAR_SHAPES[var])), np.float32)
+        _check(lib().qlx_bg_model_get_var(self.h, var, which, _p(out)))
+        return out.reshape(BG_VAR_SHAPES[var])
+
+    def set(self, var, arr, which=0):
+        a = np.ascontiguousarray(arr, dtype=np.float32).reshape(-1)
+        _check(lib().qlx_bg_model_set_var(self.h, var, which, _p(a)))
+
+    def weights(self):
+        return [self.get(v) for v in range(8)]
+
+    def iterations(self):
+        return int(lib().qlx_bg_model_iterations(self.h))
+
+    def q_values(self, states):
+        x = np.ascontiguousarray(states, dtype=np.uint8)
+        n = x.shape[0]
+        q = np.zeros((n, BG_ACTION_SPACE), np.float32)
+        a = np.zeros(n, np.uint8)
+        _check(lib().qlx_bg_model_predict(self.h, _p(x), n, _p(q), _p(a)))
+        return q, a
+
+    def batch_predict_max_future_reward(self, states):
+        x = np.ascontiguousarray(states, dtype=np.uint8)
+        out = np.zeros(x.shape[0], np.float32)
+        _check(lib().qlx_bg_model_batch_max_q(self.h, _p(x), x.shape[0], _p(out)))
+        return out
+
+    def train(self, states, actions, updated_q_values, want_grads=False):
+        x = np.ascontiguousarray(states, dtype=np.uint8)
+        a = np.ascontiguousarray(actions, dtype=np.uint8)
+        y = np.ascontiguousarray(updated_q_values, dtype=np.float32)
+        loss = np.zeros(1, np.float32)
+        nrm = np.zeros(8, np.float32)
+        g = np.zeros(sum(int(np.prod(s)) for s in BG_VAR_SHAPES), np.float32) if want_grads else None
+        _check(lib().qlx_bg_model_train(self.h, _p(x), _p(a), _p(y), x.shape[0], _p(loss), _p(g), _p(nrm)))
+        return (float(loss[0]), g, nrm) if want_grads else float(loss[0])
+
+
+class BallGameLearner:
+    """SelfDrivingQLearner over n BallGame envs on one GPU (same vector-step semantics as SelfDrivingQLearner)."""
+
+    def __init__(self, param, device=0):
+        self.param = param
+        h = C.c_void_p()
+        _check(lib().qlx_bg_learner_create(C.byref(param), device, C.byref(h)))
+        self.h = h.value
+        self.environment = BallGameEnvironment(handle=lib().qlx_bg_learner_env(self.h), n_envs=param.n_envs)
+        self.model = BallGameModel(handle=lib().qlx_bg_learner_model(self.h, 0))
+        self.stabilized_model = BallGameModel(handle=lib().qlx_bg_learner_model(self.h, 1))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().qlx_bg_learner_destroy(self.h)
+        self.h = None
+
+    __del__ = close
+
+    def vector_step(self):
+        _check(lib().qlx_bg_learner_run(self.h, 1))
+
+    def run(self, n):
+        _check(lib().qlx_bg_learner_run(self.h, n))
+
+    def sync(self):
+        _check(lib().qlx_bg_learner_sync(self.h))
+
+    def stats(self):
+        s = LearnerStats()
+        _check(lib().qlx_bg_learner_stats_get(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in LearnerStats._fields_}
+
+    def solved(self):
+        return bool(self.stats()["solved"])
+
+    def last(self, max_updates=4096):
+        N, B = self.param.n_envs, self.param.batch_size
+        a, r, d = np.zeros(N, np.uint8), np.zeros(N, np.float32), np.zeros(N, np.uint8)
+        losses = np.zeros(max_updates, np.float32)
+        idx = np.zeros(max_updates * B, np.uint64)
+        tg = np.zeros(max_updates * B, np.float32)
+        nu = C.c_uint32()
+        _check(lib().qlx_bg_learner_last(self.h, _p(a), _p(r), _p(d), _p(losses), _p(idx), _p(tg), C.byref(nu)))
+        n = nu.value
+        return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
+                    targets=tg[:n * B].reshape(n, B))
