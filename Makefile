@@ -15,7 +15,7 @@ STRICT := -ffp-contract=off
 LDFLAGS := -shared -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 
 OBJS := $(OUT)/obj/common.o $(OUT)/obj/env_breakout.o $(OUT)/obj/replay.o $(OUT)/obj/qnet.o $(OUT)/obj/learner.o \
-        $(OUT)/obj/ballgame.o
+        $(OUT)/obj/ballgame.o $(OUT)/obj/tf_bundle.o
 
 HDRS := include/qlx.h $(wildcard $(SRC)/*.h)
 
@@ -40,6 +40,9 @@ $(OUT)/obj/qnet.o: $(SRC)/qnet.hip $(HDRS) | $(OUT)/obj
 
 $(OUT)/obj/learner.o: $(SRC)/learner.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
+
+$(OUT)/obj/tf_bundle.o: $(SRC)/tf_bundle.cpp $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # BallGame env step is restated like the reference's f32 rewards (no FMA-sensitive math); the net is fp32 SIMT
 $(OUT)/obj/ballgame.o: $(SRC)/ballgame.hip $(HDRS) | $(OUT)/obj

@@ -135,6 +135,9 @@ int32_t qlx_model_batch_max_q(qlx_model* m, const uint8_t* obs, uint32_t n, floa
  * concatenated; norms_out (may be NULL) the 10 per-variable L2 norms before clipping. */
 int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions, const float* y, uint32_t batch,
                         float* loss_out, float* grads_out, float* norms_out);
+/* Load a TF SavedModel / checkpoint bundle of the reference Breakout model (layer_with_weights-0..4 kernel /
+ * bias, OPTIMIZER_SLOT m / v, optimizer/iter; shapes checked against saved/ql_model_breakout_84x84x4_3_32). */
+int32_t qlx_model_load_tf(qlx_model* m, const char* bundle_prefix);
 /* Debug view of intermediate activations of the last predict: layer 1..4 as fp32 host arrays. */
 int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out);
 /* write_checkpoint (model.rs:67-70): weights + Adam slots + iterations in a flat file. */
@@ -244,6 +247,10 @@ int32_t qlx_bg_model_batch_max_q(qlx_bg_model* m, const uint8_t* obs, uint32_t n
 int32_t qlx_bg_model_train(qlx_bg_model* m, const uint8_t* obs, const uint8_t* actions, const float* y, uint32_t batch,
                            float* loss_out, float* grads_out, float* norms_out);
 
+/* Load a TF SavedModel / checkpoint bundle of the reference model (variables/variables.index + .data, e.g.
+ * python_model/saved/ql_model_ballgame_3x3x4_5_512/variables/variables): weights, Adam m / v and iterations. */
+int32_t qlx_bg_model_load_tf(qlx_bg_model* m, const char* bundle_prefix);
+
 typedef struct qlx_bg_learner qlx_bg_learner;
 /* SelfDrivingQLearner over BallGame (same qlx_params and vector-step semantics as qlx_learner). */
 int32_t qlx_bg_learner_create(const qlx_params* p, int32_t device, qlx_bg_learner** out);
@@ -255,6 +262,18 @@ int32_t qlx_bg_learner_last(qlx_bg_learner* l, uint8_t* actions, float* rewards,
                             uint64_t* indices, float* targets, uint32_t* n_updates);
 qlx_bg_env* qlx_bg_learner_env(qlx_bg_learner* l);
 qlx_bg_model* qlx_bg_learner_model(qlx_bg_learner* l, int32_t which /* 0 online, 1 target */);
+
+/* ---------------- TF tensor bundles (the reference's model / checkpoint storage) ----------------
+ * Host-only reader of variables.index (SSTable of BundleEntryProto) + variables.data-*; block and tensor
+ * crc32c are verified.  Replaces SavedModelBundle::load's variable restore (q_learning_model.rs:47-52). */
+typedef struct qlx_tf_bundle qlx_tf_bundle;
+int32_t qlx_tf_bundle_open(const char* prefix /* ".../variables/variables" */, qlx_tf_bundle** out);
+int32_t qlx_tf_bundle_close(qlx_tf_bundle* b);
+int32_t qlx_tf_bundle_count(const qlx_tf_bundle* b);
+/* dtype: TF DataType enum (1 = float, 9 = int64); dims: up to 8 */
+int32_t qlx_tf_bundle_entry(const qlx_tf_bundle* b, int32_t i, char* name, size_t cap, int32_t* dtype, int64_t* dims,
+                            int32_t* ndims, int64_t* nbytes);
+int32_t qlx_tf_bundle_read(const qlx_tf_bundle* b, const char* name, void* out, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -782,6 +782,21 @@ int32_t qlx_bg_model_set_var(qlx_bg_model* m, int32_t var, int32_t which, const 
 
 int64_t qlx_bg_model_iterations(qlx_bg_model* m) { return m ? m->iterations : -1; }
 
+int32_t qlx_bg_model_load_tf(qlx_bg_model* m, const char* prefix) {
+  return guard([&] {
+    QLX_CHECK(m && prefix, QLX_E_INVALID, "null argument");
+    std::vector<float> w, mm, vv;
+    int64_t it = 0;
+    load_keras_bundle(prefix, 4, kVarSize, w, mm, vv, &it);
+    QLX_HIP(hipSetDevice(m->device));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    QLX_HIP(hipMemcpy(m->d_params, w.data(), kParams * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_m, mm.data(), kParams * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_v, vv.data(), kParams * 4, hipMemcpyHostToDevice));
+    m->iterations = it;
+  });
+}
+
 int32_t qlx_bg_model_predict(qlx_bg_model* m, const uint8_t* obs, uint32_t n, float* q_out, uint8_t* actions) {
   return guard([&] {
     QLX_CHECK(m && obs && n > 0, QLX_E_INVALID, "bad argument");

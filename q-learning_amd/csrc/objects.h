@@ -65,6 +65,12 @@ std::vector<double> epsilon_table(const qlx_params& p);
 // solved() over the episode reward ring (self_driving_tf_q_learner.rs:134-139)
 void learner_book_stats(const Book& b, const float* ring, uint32_t ring_cap, float goal, float pct, float* running, uint64_t* solved);
 
+// Reads the Keras SavedModel variables of `n_layers` weight layers (kernel, bias, Adam m / v) from a TF bundle
+// into host arrays laid out like the flat parameter vector (variable 2L = kernel L, 2L + 1 = bias L) and the
+// optimizer iteration count.  Shapes must multiply to var_sizes.  (tf_bundle.cpp)
+void load_keras_bundle(const char* prefix, int n_layers, const int* var_sizes, std::vector<float>& w, std::vector<float>& m,
+                       std::vector<float>& v, int64_t* iterations);
+
 void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, uint8_t* d_dones);
 void env_launch_reset(qlx_env* env, const uint8_t* d_mask, int bump);
 void replay_launch_push(qlx_replay* rb, qlx_env* env, hipStream_t s, const uint8_t* d_actions, const float* d_rewards,

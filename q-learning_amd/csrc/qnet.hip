@@ -896,6 +896,23 @@ int32_t qlx_model_write_checkpoint(qlx_model* m, const char* path) {
   });
 }
 
+int32_t qlx_model_load_tf(qlx_model* m, const char* prefix) {
+  return guard([&] {
+    QLX_CHECK(m && prefix, QLX_E_INVALID, "null argument");
+    std::vector<float> w, mm, vv;
+    int64_t it = 0;
+    load_keras_bundle(prefix, 5, kVarSize, w, mm, vv, &it);
+    QLX_HIP(hipSetDevice(m->device));
+    QLX_HIP(hipStreamSynchronize(m->stream));
+    QLX_HIP(hipMemcpy(m->d_params, w.data(), kNumParams * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_m, mm.data(), kNumParams * 4, hipMemcpyHostToDevice));
+    QLX_HIP(hipMemcpy(m->d_v, vv.data(), kNumParams * 4, hipMemcpyHostToDevice));
+    m->iterations = it;
+    model_pack(m);
+    QLX_HIP(hipStreamSynchronize(m->stream));
+  });
+}
+
 int32_t qlx_model_read_checkpoint(qlx_model* m, const char* path) {
   return guard([&] {
     QLX_CHECK(m && path, QLX_E_INVALID, "bad argument");

@@ -143,6 +143,11 @@ def lib():
         "qlx_bg_learner_stats_get": ([vp, C.POINTER(LearnerStats)], i32),
         "qlx_bg_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_bg_learner_env": ([vp], vp), "qlx_bg_learner_model": ([vp, i32], vp),
+        "qlx_bg_model_load_tf": ([vp, C.c_char_p], i32), "qlx_model_load_tf": ([vp, C.c_char_p], i32),
+        "qlx_tf_bundle_open": ([C.c_char_p, C.POINTER(vp)], i32), "qlx_tf_bundle_close": ([vp], i32),
+        "qlx_tf_bundle_count": ([vp], i32),
+        "qlx_tf_bundle_entry": ([vp, i32, C.c_char_p, C.c_size_t, C.POINTER(i32), vp, C.POINTER(i32), C.POINTER(C.c_int64)], i32),
+        "qlx_tf_bundle_read": ([vp, C.c_char_p, vp, C.c_size_t], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name, None)
@@ -303,6 +308,10 @@ class DeepQLearningModel:
 
     def copy_from(self, other):
         _check(lib().qlx_model_copy_weights(self.h, other.h))
+
+    def load_tf(self, bundle_prefix):
+        """Weights, Adam slots and iterations from a TF SavedModel / checkpoint bundle of the reference model."""
+        _check(lib().qlx_model_load_tf(self.h, str(bundle_prefix).encode()))
 
     def q_values(self, states):
         x = np.ascontiguousarray(states, dtype=np.uint8)
@@ -524,6 +533,10 @@ class BallGameModel:
     def iterations(self):
         return int(lib().qlx_bg_model_iterations(self.h))
 
+    def load_tf(self, bundle_prefix):
+        """Weights, Adam slots and iterations from the reference's SavedModel variables bundle."""
+        _check(lib().qlx_bg_model_load_tf(self.h, str(bundle_prefix).encode()))
+
     def q_values(self, states):
         x = np.ascontiguousarray(states, dtype=np.uint8)
         n = x.shape[0]
@@ -596,3 +609,39 @@ class BallGameLearner:
         n = nu.value
         return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
                     targets=tg[:n * B].reshape(n, B))
+
+
+TF_DTYPES = {1: np.float32, 2: np.float64, 3: np.int32, 9: np.int64}
+
+
+class TfBundle:
+    """TF tensor bundle (variables.index + variables.data-*) read by libqlx's host-side SSTable reader."""
+
+    def __init__(self, prefix):
+        h = C.c_void_p()
+        _check(lib().qlx_tf_bundle_open(str(prefix).encode(), C.byref(h)))
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().qlx_tf_bundle_close(self.h)
+        self.h = None
+
+    __del__ = close
+
+    def entries(self):
+        """{name: (dtype enum, shape tuple, byte size)}"""
+        out = {}
+        for i in range(lib().qlx_tf_bundle_count(self.h)):
+            name = C.create_string_buffer(512)
+            dt, nd, nb = C.c_int32(), C.c_int32(), C.c_int64()
+            dims = np.zeros(8, np.int64)
+            _check(lib().qlx_tf_bundle_entry(self.h, i, name, 512, C.byref(dt), _p(dims), C.byref(nd), C.byref(nb)))
+            out[name.value.decode()] = (dt.value, tuple(int(d) for d in dims[:nd.value]), nb.value)
+        return out
+
+    def read(self, name):
+        dt, shape, nbytes = self.entries()[name]
+        buf = np.zeros(nbytes, np.uint8)
+        _check(lib().qlx_tf_bundle_read(self.h, name.encode(), _p(buf), nbytes))
+        return buf.view(TF_DTYPES[dt]).reshape(shape)

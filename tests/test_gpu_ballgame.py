@@ -168,3 +168,25 @@ def test_learner_learns_ballgame():
         if st["running_reward"] >= 9.0:
             break
     assert best >= 9.0, (best, st)
+
+
+def test_reference_saved_weights_load_and_forward():
+    """The reference's own exported BallGame variables (tests/golden) loaded through the TF-bundle reader
+    into the GPU model: identical weights, Adam slots and iterations; Q values equal the oracle's on them."""
+    import os
+    qlx = _qlx()
+    prefix = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ballgame_saved_variables", "variables")
+    m = qlx.BallGameModel(seed=99)
+    m.load_tf(prefix)
+    bundle = qlx.TfBundle(prefix)
+    ref = O.BgNet(seed=99)
+    for v in range(8):
+        name = f"layer_with_weights-{v // 2}/{('kernel', 'bias')[v % 2]}/.ATTRIBUTES/VARIABLE_VALUE"
+        w = bundle.read(name)
+        assert np.array_equal(m.get(v), w), v
+        assert not m.get(v, which=1).any() and not m.get(v, which=2).any()
+        ref.set(v, w)
+    assert m.iterations() == 0
+    x = rand_obs(256, 4)
+    q, _ = m.q_values(x)
+    assert np.allclose(q, ref.forward(x), rtol=1e-4, atol=1e-5)
