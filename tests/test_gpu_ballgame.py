@@ -167,6 +167,8 @@ def test_learner_learns_ballgame():
         best = max(best, st["running_reward"])
         if st["running_reward"] >= 9.0:
             break
+    print(f"\nballgame learning: running_reward {st['running_reward']:.3f} after {st['step_count']} env-steps, "
+          f"{st['update_count']} updates, {st['episode_count']} episodes, epsilon {st['epsilon']:.3f}")
     assert best >= 9.0, (best, st)
 
 
