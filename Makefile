@@ -15,7 +15,7 @@ STRICT := -ffp-contract=off
 LDFLAGS := -shared -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 
 OBJS := $(OUT)/obj/common.o $(OUT)/obj/env_breakout.o $(OUT)/obj/replay.o $(OUT)/obj/qnet.o $(OUT)/obj/learner.o \
-        $(OUT)/obj/ballgame.o $(OUT)/obj/tf_bundle.o
+        $(OUT)/obj/ballgame.o $(OUT)/obj/tf_bundle.o $(OUT)/obj/per.o
 
 HDRS := include/qlx.h $(wildcard $(SRC)/*.h)
 
@@ -47,6 +47,10 @@ $(OUT)/obj/tf_bundle.o: $(SRC)/tf_bundle.cpp $(HDRS) | $(OUT)/obj
 # BallGame env step is restated like the reference's f32 rewards (no FMA-sensitive math); the net is fp32 SIMT
 $(OUT)/obj/ballgame.o: $(SRC)/ballgame.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# sum-tree descent and IS weights are compared bit-for-bit with the oracle: no contraction
+$(OUT)/obj/per.o: $(SRC)/per.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
 
 $(OUT)/libqlx.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) $(OBJS) $(LDFLAGS) -o $@

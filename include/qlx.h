@@ -165,8 +165,16 @@ typedef struct qlx_params { /* Parameter (self_driving_tf_q_learner.rs:20-67) + 
   uint64_t learner_seed;
   uint64_t init_seed;
   uint32_t rank;
-  uint32_t pad;
+  uint32_t flags;     /* QLX_LEARNER_* extensions beyond the reference (0 = the reference algorithm) */
+  float per_alpha;    /* prioritized replay: P(i) ~ p_i^alpha, p_i = |td_i| + per_eps */
+  float per_beta;     /* importance-sampling exponent, w_i = (len P(i))^-beta / max_batch w */
+  float per_eps;
+  uint32_t pad2;
 } qlx_params;
+
+/* qlx_params.flags */
+#define QLX_LEARNER_DOUBLE_DQN 1u  /* y = r + gamma Q_target(s', argmax_a Q_online(s')) (van Hasselt et al. 2016) */
+#define QLX_LEARNER_PER 2u         /* proportional prioritized replay on an HBM sum tree (Schaul et al. 2016) */
 
 void qlx_params_default(qlx_params* p);
 
@@ -191,6 +199,10 @@ int32_t qlx_learner_stats_get(qlx_learner* l, qlx_learner_stats* out);
  * number of updates of that step in *n_updates. */
 int32_t qlx_learner_last(qlx_learner* l, uint8_t* actions, float* rewards, uint8_t* dones, float* losses,
                          uint64_t* indices, float* targets, uint32_t* n_updates);
+/* Prioritized replay state (learner created with QLX_LEARNER_PER): IS weights of the last vector step's batches
+ * [n_updates][B], the sum tree's leaves [history_buffer_len] (priority^alpha per physical replay slot), the
+ * priority new transitions enter with; any may be NULL. */
+int32_t qlx_learner_priorities(qlx_learner* l, float* is_weights, float* leaves, float* per_max);
 qlx_env* qlx_learner_env(qlx_learner* l);
 qlx_replay* qlx_learner_replay(qlx_learner* l);
 qlx_model* qlx_learner_model(qlx_learner* l, int32_t which /* 0 online, 1 target */);
@@ -207,6 +219,20 @@ int32_t qlx_learner_profile_filter(qlx_learner* l, const char* name_or_null);
 int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* total_us, double* total_work,
                                 uint64_t* launches);
 int32_t qlx_learner_profile_names(qlx_learner* l, char* buf, size_t cap);
+
+/* ---------------- prioritized-replay sum tree (beyond the reference) ----------------
+ * The learner's HBM sum tree as a standalone object: leaves = priorities of `capacity` slots, proportional
+ * sampling of n_updates batches of `batch` draws (draw b of update u: stream (seed, first_update + u, rank,
+ * purpose 7, word b)), IS weights (len P(i))^-beta normalised per batch, and last-writer-wins priority
+ * updates p = (|td| + eps)^alpha.  Oracle: oracle/learner_ref.h SumTree / per_sample. */
+typedef struct qlx_sumtree qlx_sumtree;
+int32_t qlx_sumtree_create(uint64_t capacity, int32_t device, qlx_sumtree** out);
+int32_t qlx_sumtree_destroy(qlx_sumtree* t);
+int32_t qlx_sumtree_set_leaves(qlx_sumtree* t, const float* leaves /* [capacity], finite >= 0 */);
+int32_t qlx_sumtree_get(qlx_sumtree* t, float* leaves, float* total, float* per_max);
+int32_t qlx_sumtree_sample(qlx_sumtree* t, uint64_t seed, uint32_t first_update, uint32_t n_updates, uint32_t rank, uint64_t len,
+                           float beta, uint32_t batch, uint64_t* slots /* [n_updates][batch] */, float* weights);
+int32_t qlx_sumtree_update(qlx_sumtree* t, const uint64_t* slots, const float* td_abs, uint32_t n, float alpha, float eps);
 
 /* ---------------- BallGame (BallGameTestEnvironment + its 3x3x4 -> 5 Q-model) ----------------
  * The reference's second Environment / DeepQLearningModel pair, batched on the GPU.  Same conventions as

@@ -90,7 +90,9 @@ struct BgParams {   // field layout = qlx_params (include/qlx.h)
   uint64_t learner_seed;
   uint64_t init_seed;
   uint32_t rank;
-  uint32_t pad;
+  uint32_t flags;      // bit 0 double DQN, bit 1 prioritized replay (qlx.h QLX_LEARNER_*)
+  float per_alpha, per_beta, per_eps;
+  uint32_t pad2;
 };
 
 struct BgTransition { uint8_t action; BgState s, s_next; float reward; bool done; };

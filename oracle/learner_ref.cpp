@@ -2,6 +2,7 @@
 #include "learner_ref.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "rng_ref.h"
@@ -22,13 +23,30 @@ void generate_distinct_random_ids(uint64_t seed, uint32_t update_idx, uint32_t r
   }
 }
 
+void per_sample(const SumTree& st, uint64_t seed, uint32_t update_idx, uint32_t rank, uint64_t len, float beta, int B,
+                uint64_t* slots, float* weights) {
+  const float T = st.t[1];
+  const float seg = T / (float)B;
+  float wmax = 0.0f;
+  for (int b = 0; b < B; ++b) {
+    Stream s(seed, update_idx, rank, P_PER, (uint64_t)b);
+    const float r = gen_range_f32(s, 0.0f, 1.0f);
+    const float u = seg * ((float)b + r);
+    slots[b] = st.find(u);
+    const float p = st.t[st.L + slots[b]] / T;
+    weights[b] = std::pow((float)len * p, -beta);
+    wmax = std::max(wmax, weights[b]);
+  }
+  for (int b = 0; b < B; ++b) weights[b] = weights[b] / wmax;
+}
+
 static StateRef snapshot(const Env& e) {   // Environment::state_as_rc / step_as_rc (prelude.rs:36,52-58)
   auto s = std::make_shared<std::vector<uint8_t>>(kStateBytes);
   env_state_tensor(e, s->data());
   return s;
 }
 
-Learner::Learner(const LearnerParams& prm) : p(prm), replay(prm.history_buffer_len) {
+Learner::Learner(const LearnerParams& prm) : p(prm), replay(prm.history_buffer_len), tree(prm.history_buffer_len) {
   envs.resize(p.n_envs);
   state.resize(p.n_envs);
   ep_reward.assign(p.n_envs, 0.0f);
@@ -50,6 +68,7 @@ void Learner::vector_step() {
   last_losses.clear();
   last_indices.clear();
   last_targets.clear();
+  last_weights.clear();
   last_q.clear();
   const uint64_t step_before = step_count;
   // ---- acting (learn_episode :150-167) ----
@@ -88,6 +107,8 @@ void Learner::vector_step() {
     ep_reward[e] += r;
     ep_steps[e] += 1;
     replay.add({last_actions[e], state[e], nxt, r, done});
+    if (p.flags & 2u) tree.set(total_pushed % p.history_buffer_len, per_max);   // new transitions at max priority
+    total_pushed += 1;
     state[e] = nxt;
     last_rewards[e] = r;
     last_dones[e] = done ? 1 : 0;
@@ -108,42 +129,83 @@ void Learner::vector_step() {
   }
   // ---- training updates (:181-202) ----
   const uint64_t triggers = step_count / p.update_after_actions - step_before / p.update_after_actions;
-  if (replay.len() > p.batch_size)
-    for (uint64_t t = 0; t < triggers; ++t) update();
+  if (replay.len() > p.batch_size && triggers > 0) {
+    // every batch of the vector step is drawn from the replay (and priorities) as they stand after the pushes
+    const int B = (int)p.batch_size;
+    const uint64_t len = replay.len();
+    std::vector<uint64_t> idx((size_t)triggers * B);
+    std::vector<float> isw((size_t)triggers * B, 1.0f);
+    for (uint64_t t = 0; t < triggers; ++t) {
+      if (p.flags & 2u) {
+        const uint64_t start = (total_pushed - len) % p.history_buffer_len;
+        std::vector<uint64_t> slots(B);
+        per_sample(tree, p.learner_seed, (uint32_t)(update_count + t), p.rank, len, p.per_beta, B, slots.data(), &isw[t * B]);
+        for (int b = 0; b < B; ++b) idx[t * B + b] = (slots[b] + p.history_buffer_len - start) % p.history_buffer_len;
+      } else {
+        generate_distinct_random_ids(p.learner_seed, (uint32_t)(update_count + t), p.rank, len, B, &idx[t * B]);
+      }
+    }
+    std::vector<float> y((size_t)triggers * B);
+    for (uint64_t t = 0; t < triggers; ++t) targets(&idx[t * B], &y[t * B]);
+    for (uint64_t t = 0; t < triggers; ++t) update(&idx[t * B], (p.flags & 2u) ? &isw[t * B] : nullptr, &y[t * B]);
+  }
   if (p.target_sync_steps > 0 && step_count / p.target_sync_steps != step_before / p.target_sync_steps)
     qnet_copy_weights(target, online);
   vec_steps += 1;
 }
 
-void Learner::update() {
+// Bellman targets of one sampled batch from the nets as they stand before the vector step's updates:
+// y = r + gamma * max_a Q_target(s') (reference), or with double DQN r + gamma * Q_target(s', argmax_a Q_online(s'));
+// y = r if done.  (Without double DQN this equals computing y inside each update: the target net does not move.)
+void Learner::targets(const uint64_t* idx, float* y) const {
   const int B = (int)p.batch_size;
-  std::vector<uint64_t> idx(B);
-  generate_distinct_random_ids(p.learner_seed, (uint32_t)update_count, p.rank, replay.len(), B, idx.data());
-  std::vector<uint8_t> xs((size_t)B * kStateBytes), xn((size_t)B * kStateBytes), act(B);
-  std::vector<float> rew(B), y(B);
-  std::vector<uint8_t> dn(B);
+  std::vector<uint8_t> xn((size_t)B * kStateBytes);
+  for (int b = 0; b < B; ++b) std::memcpy(&xn[(size_t)b * kStateBytes], replay.buf[idx[b]].s_next->data(), kStateBytes);
+  Acts at;
+  qnet_forward(target, xn.data(), B, at);   // batch_predict_max_future_reward
+  Acts an;
+  if (p.flags & 1u) qnet_forward(online, xn.data(), B, an);   // double DQN: the online net picks a*
+  for (int b = 0; b < B; ++b) {
+    const Transition& t = replay.buf[idx[b]];
+    float v;
+    if (p.flags & 1u) {
+      v = at.q[(size_t)b * kActions + argmax_first(&an.q[(size_t)b * kActions], kActions)];
+    } else {
+      v = at.q[(size_t)b * kActions];
+      for (int j = 1; j < kActions; ++j) v = std::max(v, at.q[(size_t)b * kActions + j]);
+    }
+    y[b] = t.reward + v * p.gamma;            // add_arrays(reward, array_mul(max_future, gamma))
+    if (t.done) y[b] = t.reward;
+  }
+}
+
+void Learner::update(const uint64_t* idx, const float* isw, const float* y) {
+  const int B = (int)p.batch_size;
+  std::vector<uint8_t> xs((size_t)B * kStateBytes), act(B);
   for (int b = 0; b < B; ++b) {   // ReplayBuffer::get_many
     const Transition& t = replay.buf[idx[b]];
     std::memcpy(&xs[(size_t)b * kStateBytes], t.s->data(), kStateBytes);
-    std::memcpy(&xn[(size_t)b * kStateBytes], t.s_next->data(), kStateBytes);
-    act[b] = t.action; rew[b] = t.reward; dn[b] = t.done ? 1 : 0;
-  }
-  Acts at;
-  qnet_forward(target, xn.data(), B, at);   // batch_predict_max_future_reward
-  for (int b = 0; b < B; ++b) {
-    float mx = at.q[(size_t)b * kActions];
-    for (int j = 1; j < kActions; ++j) mx = std::max(mx, at.q[(size_t)b * kActions + j]);
-    y[b] = rew[b] + mx * p.gamma;            // add_arrays(reward, array_mul(max_future, gamma))
-    if (dn[b]) y[b] = rew[b];
+    act[b] = t.action;
   }
   Acts ao;
   qnet_forward(online, xs.data(), B, ao);
   Grads g;
-  const float loss = qnet_loss_backward(online, xs.data(), act.data(), y.data(), B, ao, g);
+  std::vector<float> td(B);
+  const float loss = qnet_loss_backward(online, xs.data(), act.data(), y, B, ao, g, isw, td.data());
   qnet_apply_adam(online, g, nullptr);
+  if (p.flags & 2u) {   // new priorities (|td| + eps)^alpha, in batch order (a repeated slot keeps its last value)
+    const uint64_t start = (total_pushed - replay.len()) % p.history_buffer_len;
+    for (int b = 0; b < B; ++b) {
+      const float pr = std::pow(td[b] + p.per_eps, p.per_alpha);
+      tree.set((start + idx[b]) % p.history_buffer_len, pr);
+      per_max = std::max(per_max, pr);
+    }
+  }
   last_losses.push_back(loss);
-  last_indices.insert(last_indices.end(), idx.begin(), idx.end());
-  last_targets.insert(last_targets.end(), y.begin(), y.end());
+  last_indices.insert(last_indices.end(), idx, idx + B);
+  last_targets.insert(last_targets.end(), y, y + B);
+  last_weights.insert(last_weights.end(), isw ? isw : y, (isw ? isw : y) + B);
+  if (!isw) std::fill(last_weights.end() - B, last_weights.end(), 1.0f);
   update_count += 1;
 }
 

@@ -13,6 +13,9 @@
 //   update_after_actions crossed by step_count, if replay.len > batch.
 //   Target network: never synced when target_sync_steps == 0 (the reference: the sync is commented
 //   out at :205-210 and update_target_network_after_num_steps is never read).
+//   All U batches of a vector step are sampled, and their Bellman targets computed, before its first update.
+// Beyond the reference (flags): double DQN targets (a* = argmax of the online net as it stands
+//   before the vector step's updates) and proportional prioritized replay (SumTree below).
 #pragma once
 #include <cstdint>
 #include <deque>
@@ -44,7 +47,9 @@ struct LearnerParams {   // layout mirrored by tests/oracle.py (ctypes)
   uint64_t learner_seed;
   uint64_t init_seed;
   uint32_t rank;
-  uint32_t pad;
+  uint32_t flags;      // bit 0 double DQN, bit 1 prioritized replay (qlx.h QLX_LEARNER_*)
+  float per_alpha, per_beta, per_eps;
+  uint32_t pad2;
 };
 
 using StateRef = std::shared_ptr<std::vector<uint8_t>>;   // Rc<BreakoutState> tensor view [x][y][slot]
@@ -59,6 +64,37 @@ struct Replay {   // replay_buffer.rs: five parallel VecDeques share one FIFO po
   size_t len() const { return buf.size(); }
 };
 
+constexpr uint32_t P_PER = 7;   // prioritized-replay draws: c1 = update index, c2 = rank, word = sample
+
+// Proportional prioritized replay (Schaul et al. 2016) - beyond the reference.
+// Leaves = replay slots (physical FIFO positions), values p^alpha; every internal node = left + right in f32
+// (so the tree is a pure function of the leaves).  Batch b of B draws u = (T / B) * (b + r_b), r_b =
+// gen_range_f32(0, 1) from Stream(seed, update, rank, P_PER, word b), and descends: left iff u < left sum
+// (or the right subtree is empty), else u -= left sum.  IS weights w = (len * leaf / T)^-beta / max over the
+// batch.
+struct SumTree {
+  uint32_t L = 1;   // leaves (power of two >= capacity)
+  std::vector<float> t;
+  explicit SumTree(uint64_t cap) { while (L < cap) L <<= 1; t.assign(2 * (size_t)L, 0.0f); }
+  void set(uint64_t leaf, float v) {
+    size_t i = L + leaf;
+    t[i] = v;
+    for (i >>= 1; i >= 1; i >>= 1) t[i] = t[2 * i] + t[2 * i + 1];
+  }
+  uint64_t find(float u) const {
+    size_t i = 1;
+    while (i < L) {
+      const float left = t[2 * i];
+      if (u < left || t[2 * i + 1] == 0.0f) i = 2 * i;
+      else { u -= left; i = 2 * i + 1; }
+    }
+    return i - L;
+  }
+};
+// one prioritized batch: physical slots and normalised IS weights
+void per_sample(const SumTree& st, uint64_t seed, uint32_t update_idx, uint32_t rank, uint64_t len, float beta, int B,
+                uint64_t* slots, float* weights);
+
 // self_driving_tf_q_learner.rs:276-296 with the build's counter-based stream
 void generate_distinct_random_ids(uint64_t seed, uint32_t update_idx, uint32_t rank, uint64_t len, int B, uint64_t* out);
 
@@ -69,6 +105,9 @@ struct Learner {
   std::vector<float> ep_reward;
   std::vector<uint64_t> ep_steps;
   Replay replay;
+  uint64_t total_pushed = 0;   // FIFO position of the next push (prioritized replay maps slots <-> logical indices)
+  SumTree tree;
+  float per_max = 1.0f;        // largest leaf value so far (new transitions enter at it)
   QNet online, target;
   uint64_t step_count = 0;
   double epsilon;
@@ -85,10 +124,13 @@ struct Learner {
   std::vector<uint64_t> last_indices;   // [n_updates][B]
   std::vector<float> last_q;            // [N][3] acting Q values (if computed)
   std::vector<float> last_targets;      // [n_updates][B] y
+  std::vector<float> last_weights;      // [n_updates][B] IS weights (1 without prioritized replay)
 
   explicit Learner(const LearnerParams& prm);
   void vector_step();
-  void update();
+  void targets(const uint64_t* idx, float* y) const;
+  // logical indices of the batch, IS weights (or null), Bellman targets
+  void update(const uint64_t* idx, const float* isw, const float* y);
   bool solved() const;
 };
 

@@ -230,6 +230,23 @@ void orc_learner_replay_get(void* h, const uint64_t* idx, int B, uint8_t* s, uin
     if (d) d[b] = t.done ? 1 : 0;
   }
 }
+// prioritized replay state: IS weights of the last vector step's batches, the sum tree's leaves [cap], per_max
+void orc_learner_per(void* h, float* weights, float* leaves, float* per_max) {
+  Learner* l = (Learner*)h;
+  if (weights) std::memcpy(weights, l->last_weights.data(), l->last_weights.size() * 4);
+  if (leaves) std::memcpy(leaves, l->tree.t.data() + l->tree.L, l->p.history_buffer_len * 4);
+  if (per_max) *per_max = l->per_max;
+}
+// one prioritized draw per update u < U from a tree over the given leaves [cap] (physical slots)
+void orc_per_sample(const float* leaves, uint64_t cap, uint64_t seed, uint32_t first_update, uint32_t n_updates, uint32_t rank,
+                    uint64_t len, float beta, int B, uint64_t* slots, float* weights, float* total) {
+  SumTree st(cap);
+  for (uint64_t i = 0; i < cap; ++i) st.t[st.L + i] = leaves[i];
+  for (size_t i = st.L - 1; i >= 1; --i) st.t[i] = st.t[2 * i] + st.t[2 * i + 1];
+  if (total) *total = st.t[1];
+  for (uint32_t u = 0; u < n_updates; ++u)
+    per_sample(st, seed, first_update + u, rank, len, beta, B, slots + (size_t)u * B, weights + (size_t)u * B);
+}
 size_t orc_learner_params_size() { return sizeof(LearnerParams); }
 size_t orc_state_size() { return sizeof(OrcState); }
 int orc_num_threads() { return omp_get_max_threads(); }

@@ -165,7 +165,7 @@ static void conv_bwd(const ConvCfg& c, const float* in, const float* out, const 
 }
 
 float qnet_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* actions, const float* y, int B,
-                         const Acts& a, Grads& g) {
+                         const Acts& a, Grads& g, const float* weights, float* td_abs) {
   for (int v = 0; v < kNumVars; ++v) g.g[v].assign(kVarSize[v], 0.0f);
   // Huber(delta=1), error = y_pred - y_true, mean over batch (keras SUM_OVER_BATCH_SIZE)
   std::vector<float> dq((size_t)B * kActions, 0.0f);
@@ -174,10 +174,12 @@ float qnet_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* action
     const float qa = a.q[(size_t)b * kActions + actions[b]];
     const float e = qa - y[b];
     const float ae = std::fabs(e);
+    const float w = weights ? weights[b] : 1.0f;   // prioritized replay importance-sampling weight
     const float h = ae <= 1.0f ? 0.5f * e * e : ae - 0.5f;
-    loss_sum += h;
+    loss_sum += w * h;
     const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
-    dq[(size_t)b * kActions + actions[b]] = ge / (float)B;
+    dq[(size_t)b * kActions + actions[b]] = (w * ge) / (float)B;
+    if (td_abs) td_abs[b] = ae;
   }
   const float loss = (float)(loss_sum / (double)B);
 

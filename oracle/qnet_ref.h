@@ -45,8 +45,9 @@ void qnet_forward(const QNet& q, const uint8_t* x, int B, Acts& acts);
 
 struct Grads { std::vector<float> g[kNumVars]; };
 // Huber loss + full backward. Returns the loss; grads are the raw (unclipped) gradients.
+// weights (optional): per-sample loss weights (prioritized-replay IS weights); td_abs (optional): |q_a - y| out
 float qnet_loss_backward(const QNet& q, const uint8_t* x, const uint8_t* actions, const float* y, int B,
-                         const Acts& acts, Grads& grads);
+                         const Acts& acts, Grads& grads, const float* weights = nullptr, float* td_abs = nullptr);
 // clip_by_norm per variable + ResourceApplyAdam, iterations += 1
 void qnet_apply_adam(QNet& q, const Grads& grads, float* norms_out /*[10] or null*/);
 

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "objects.h"
+#include "per.h"
 #include "profiler.h"
 #include "qnet.h"
 #include "replay_dev.h"
@@ -191,6 +192,8 @@ struct qlx_learner {
   float* d_losses = nullptr;       // [max_updates]
   float* d_targets = nullptr;      // [max_updates][B]
   uint32_t max_updates = 0;
+  bool ddqn = false, per = false;  // qlx_params.flags
+  qlx::PerState prio;              // prioritized replay (per.hip)
   // host counters
   uint64_t step_count = 0, vec_steps = 0, update_count = 0;
   uint32_t last_updates = 0;
@@ -215,10 +218,19 @@ static void learner_targets(qlx_learner* L, uint32_t U) {
     hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, s, rv, L->d_idx, n, L->d_tab_s, L->d_tab_sn, L->d_bact,
                        L->d_brew, L->d_bdone);
   }
+  const float* q_select = nullptr;
+  if (L->ddqn) {   // double DQN: a* = argmax Q_online(s') from the online net as it stands before this step's updates
+    qlx_model* on = L->online;
+    model_forward_trunk(on, L->d_tab_sn, (int)n, s, false);
+    Fc2Args oa = fc2_args(on, (int)n);
+    launch_fc2(0, oa, (int)n, s);
+    q_select = on->w.q;
+  }
   qlx_model* tg = L->target;
   model_workspace(tg, (int)n);
   model_forward_trunk(tg, L->d_tab_sn, (int)n, s, false);
   Fc2Args ta = fc2_args(tg, (int)n);
+  ta.q_select = q_select;
   ta.rewards = L->d_brew;
   ta.dones = L->d_bdone;
   ta.gamma = L->p.gamma;
@@ -234,7 +246,8 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
   const uint8_t* bact = L->d_bact + (size_t)u_local * B;
   // online: forward, Huber, backward
   model_forward_trunk(on, tab_s, (int)B, s);
-  model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s);
+  model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s,
+                 L->per ? L->prio.d_w + (size_t)u_local * B : nullptr, L->per ? L->prio.d_td + (size_t)u_local * B : nullptr);
   float scale = 1.0f;
   if (L->comm) {
     ProfScope ps(&L->prof, "allreduce", s);
@@ -273,6 +286,7 @@ static void learner_vector_step(qlx_learner* L) {
   {
     ProfScope ps(&L->prof, "replay_push", s, 2.0 * 7056.0 * N + 10.0 * N);   // frame read + write + metadata
     replay_launch_push(L->rb, L->env, s, L->d_actions, L->d_rewards, L->d_dones);
+    if (L->per) per_launch_push(s, L->prio.leaves(), L->rb->cap, L->rb->total - N, N, L->prio.d_max);
   }
   {
     ProfScope ps(&L->prof, "episode_reset", s);
@@ -287,12 +301,24 @@ static void learner_vector_step(qlx_learner* L) {
   if (L->rb->len() > L->B && triggers > 0) {
     const uint32_t U = (uint32_t)triggers;
     QLX_CHECK(U <= L->max_updates, QLX_E_STATE, "too many updates per vector step");
+    const uint64_t cap = L->rb->cap, start = (L->rb->total - L->rb->len()) % cap;
     {
       ProfScope ps(&L->prof, "sample", s);
-      replay_launch_sample(L->rb, s, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank, L->B, L->d_idx);
+      if (L->per) {
+        per_launch_build(s, L->prio.d_tree, L->prio.L);
+        per_launch_sample(s, L->prio.d_tree, L->prio.L, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank,
+                          L->rb->len(), L->p.per_beta, L->B, cap, start, L->d_idx, L->prio.d_w);
+      } else {
+        replay_launch_sample(L->rb, s, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank, L->B, L->d_idx);
+      }
     }
     learner_targets(L, U);
     for (uint32_t u = 0; u < U; ++u) learner_update(L, u);
+    if (L->per) {
+      ProfScope ps(&L->prof, "priorities", s);
+      per_launch_update(s, L->d_idx, L->prio.d_td, U * L->B, cap, start, L->p.per_alpha, L->p.per_eps, L->prio.d_owner,
+                        L->prio.leaves(), L->prio.d_max);
+    }
     L->last_updates = U;
   }
   const uint64_t ts = L->p.target_sync_steps;
@@ -328,6 +354,9 @@ void qlx_params_default(qlx_params* p) {
   p->env_seed = 0x51A5EED;
   p->learner_seed = 1;
   p->init_seed = 2;
+  p->per_alpha = 0.6f;   // Schaul et al. 2016 proportional variant
+  p->per_beta = 0.4f;
+  p->per_eps = 1e-6f;
 }
 
 int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** out) {
@@ -336,8 +365,13 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
     QLX_CHECK(p->n_envs > 0 && p->batch_size > 0 && p->batch_size <= 4096, QLX_E_INVALID, "bad n_envs / batch_size");
     QLX_CHECK(p->update_after_actions > 0 && p->history_buffer_len >= p->batch_size, QLX_E_INVALID, "bad parameters");
     QLX_CHECK(p->episode_reward_history_buffer_len > 0, QLX_E_INVALID, "episode_reward_history_buffer_len must be > 0");
+    QLX_CHECK((p->flags & ~(QLX_LEARNER_DOUBLE_DQN | QLX_LEARNER_PER)) == 0, QLX_E_INVALID, "unknown learner flags");
+    QLX_CHECK(!(p->flags & QLX_LEARNER_PER) || (p->per_alpha >= 0.0f && p->per_beta >= 0.0f && p->per_eps > 0.0f),
+              QLX_E_INVALID, "prioritized replay needs alpha >= 0, beta >= 0, eps > 0");
     current_device_checked(device);
     auto* L = new qlx_learner;
+    L->ddqn = (p->flags & QLX_LEARNER_DOUBLE_DQN) != 0;
+    L->per = (p->flags & QLX_LEARNER_PER) != 0;
     L->p = *p;
     L->device = device;
     L->N = p->n_envs;
@@ -397,6 +431,8 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
     QLX_HIP(hipGetLastError());
     model_workspace(L->online, (int)std::max(N, B));
     model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
+    if (L->ddqn) model_workspace(L->online, (int)(L->max_updates * B));   // + the online pass over s'
+    if (L->per) L->prio.init(p->history_buffer_len, UB);
     QLX_HIP(hipStreamSynchronize(L->stream));
     *out = L;
   });
@@ -416,6 +452,7 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
                     L->d_hist, L->d_book, L->d_idx, (void*)L->d_tab_s, (void*)L->d_tab_sn, L->d_bact, L->d_brew,
                     L->d_bdone, L->d_losses, L->d_targets};
     for (void* p : ptrs) (void)hipFree(p);
+    L->prio.release();
     (void)hipStreamDestroy(L->stream);
     delete L;
   });
@@ -496,6 +533,17 @@ int32_t qlx_learner_last(qlx_learner* L, uint8_t* actions, float* rewards, uint8
     if (U && indices) QLX_HIP(hipMemcpy(indices, L->d_idx, (size_t)U * L->B * 8, hipMemcpyDeviceToHost));
     if (U && targets) QLX_HIP(hipMemcpy(targets, L->d_targets, (size_t)U * L->B * 4, hipMemcpyDeviceToHost));
     if (n_updates) *n_updates = U;
+  });
+}
+
+int32_t qlx_learner_priorities(qlx_learner* L, float* is_weights, float* leaves, float* per_max) {
+  return guard([&] {
+    QLX_CHECK(L && L->per, QLX_E_STATE, "learner was created without QLX_LEARNER_PER");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    const uint32_t U = L->last_updates;
+    if (U && is_weights) QLX_HIP(hipMemcpy(is_weights, L->prio.d_w, (size_t)U * L->B * 4, hipMemcpyDeviceToHost));
+    if (leaves) QLX_HIP(hipMemcpy(leaves, L->prio.leaves(), L->prio.cap * 4, hipMemcpyDeviceToHost));
+    if (per_max) QLX_HIP(hipMemcpy(per_max, L->prio.d_max, 4, hipMemcpyDeviceToHost));
   });
 }
 

@@ -62,7 +62,7 @@ constexpr int kNumBricks = 60;
 __host__ __device__ inline int s2d_offset(int x, int y) { return ((x >> 2) * kBlocks + (y >> 2)) * 16 + (x & 3) * 4 + (y & 3); }
 
 // ---- Philox4x32-10 counter-based RNG (build-defined stream) ------------
-enum Purpose : uint32_t { P_BALL = 1, P_ACT = 2, P_SAMPLE = 3, P_INIT = 4, P_SYNTH = 5, P_BALLGAME = 6 };
+enum Purpose : uint32_t { P_BALL = 1, P_ACT = 2, P_SAMPLE = 3, P_INIT = 4, P_SYNTH = 5, P_BALLGAME = 6, P_PER = 7 };
 
 __host__ __device__ inline void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                                        uint32_t out[4]) {

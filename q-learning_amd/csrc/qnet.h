@@ -83,10 +83,13 @@ struct Fc2Args {
   const uint8_t* dones;    // mode 2
   float gamma;             // mode 2
   float* y_out;            // mode 2
+  const float* q_select;   // mode 2, double DQN: [B][3] online Q(s'), a* = its first argmax, y uses q[a*] (else max)
   const uint8_t* actions;  // training head
   const float* y;          // training head
   float* gsample;          // training head: dloss/dq_a per sample
   float* hsample;          // training head: per-sample Huber value
+  const float* weights;    // training head (optional): per-sample loss weights (prioritized-replay IS weights)
+  float* td_abs;           // training head (optional): |q_a - y| out
 };
 // fc2 kernel arguments for the model's last forward; consumes pending fc1 partials (the fc2 launch that
 // follows materialises a4)
@@ -97,8 +100,9 @@ void model_pack(qlx_model* m);
 // store_acts = false skips writing a1/a2 (only a3 is needed when no backward pass follows)
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts = true);
 // Huber head + backward after model_forward_trunk: loss -> *loss_dev, raw gradients -> m->d_grads
+// weights (optional): per-sample loss weights; td_abs (optional): |q_a - y| per sample out
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
-                    hipStream_t s);
+                    hipStream_t s, const float* weights = nullptr, float* td_abs = nullptr);
 // per-variable norm partials for Adam: with scale == 1 (no all-reduce since the backward) the producers'
 // fused partials are used as they are; otherwise per-range sums of squares of the scaled gradients
 void model_norms(qlx_model* m, hipStream_t s, float scale);

@@ -169,8 +169,18 @@ __global__ __launch_bounds__(256) void k_fc2(Fc2Args A) {
     if (q1 > bv) { best = 1; bv = q1; }
     if (q2 > bv) { best = 2; }
     A.argmax[b] = (uint8_t)best;
-  } else if (MODE == 2) {   // max_a Q_target(s') -> r + max * gamma, or r if done
-    const float mx = fmaxf(fmaxf(q0, q1), q2);
+  } else if (MODE == 2) {   // max_a Q_target(s') (or Q_target(s', argmax Q_online(s'))) -> r + v * gamma, or r if done
+    float mx;
+    if (A.q_select) {
+      const float* qs = A.q_select + b * 3;
+      int best = 0;
+      float bv = qs[0];
+      if (qs[1] > bv) { best = 1; bv = qs[1]; }
+      if (qs[2] > bv) best = 2;
+      mx = best == 0 ? q0 : (best == 1 ? q1 : q2);
+    } else {
+      mx = fmaxf(fmaxf(q0, q1), q2);
+    }
     const float r = A.rewards[b];
     A.y_out[b] = A.dones[b] ? r : r + mx * A.gamma;
   }
@@ -204,11 +214,13 @@ __global__ __launch_bounds__(256) void k_fc2_train(Fc2Args A, bf16* dz4) {
   const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
   const float e = qa - A.y[b];
   const float ae = fabsf(e);
-  const float g = (ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f)) / (float)A.B;
+  const float wgt = A.weights ? A.weights[b] : 1.0f;   // prioritized replay: the IS weight scales h and dloss/dq
+  const float g = (wgt * (ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f))) / (float)A.B;
   if (lane == 0) {
     A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2;
-    A.hsample[b] = ae <= 1.0f ? 0.5f * e * e : ae - 0.5f;
+    A.hsample[b] = wgt * (ae <= 1.0f ? 0.5f * e * e : ae - 0.5f);
     A.gsample[b] = g;
+    if (A.td_abs) A.td_abs[b] = ae;
   }
   bf16x8 d;
 #pragma unroll
@@ -526,7 +538,7 @@ Fc2Args fc2_args(qlx_model* m, int B) {
 // Huber loss (mean over the batch -> *loss_dev) and its raw, unclipped gradients into m->d_grads, after
 // model_forward_trunk on the same batch; actions / y are device arrays [B]
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
-                    hipStream_t s) {
+                    hipStream_t s, const float* weights, float* td_abs) {
   ModelWs& w = m->w;
   float* G = m->d_grads;
   {  // head: q, Huber, dz4 (one wave per sample)
@@ -536,6 +548,8 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
     a.y = y;
     a.gsample = w.gs;
     a.hsample = w.hs;
+    a.weights = weights;
+    a.td_abs = td_abs;
     hipLaunchKernelGGL(k_fc2_train, dim3((B + 3) / 4), dim3(256), 0, s, a, w.dz4);
   }
   // fc1 in one launch of two independent GEMMs (both only read dz4 / a3), plus dW4 / db4 / loss:

@@ -62,8 +62,15 @@ class Params(C.Structure):
         ("learner_seed", C.c_uint64),
         ("init_seed", C.c_uint64),
         ("rank", C.c_uint32),
-        ("pad", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("per_alpha", C.c_float),
+        ("per_beta", C.c_float),
+        ("per_eps", C.c_float),
+        ("pad2", C.c_uint32),
     ]
+
+DOUBLE_DQN = 1
+PER = 2
 
 
 class LearnerStats(C.Structure):
@@ -78,7 +85,7 @@ def Parameter(**kw):
                epsilon_greedy_steps=1_000_000.0, max_steps_per_episode=10_000, epsilon_pure_random_steps=50_000,
                history_buffer_len=1_000_000, update_after_actions=4, target_sync_steps=0,
                episode_reward_history_buffer_len=100, n_envs=1, batch_size=32, env_seed=0x51A5EED, learner_seed=1,
-               init_seed=2, rank=0, pad=0)
+               init_seed=2, rank=0, flags=0, per_alpha=0.6, per_beta=0.4, per_eps=1e-6, pad2=0)
     for k, v in kw.items():
         setattr(p, k, v)
     return p
@@ -124,6 +131,11 @@ def lib():
         "qlx_learner_stats_get": ([vp, C.POINTER(LearnerStats)], i32),
         "qlx_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_learner_env": ([vp], vp), "qlx_learner_replay": ([vp], vp), "qlx_learner_model": ([vp, i32], vp),
+        "qlx_learner_priorities": ([vp, vp, vp, vp], i32),
+        "qlx_sumtree_create": ([u64, i32, C.POINTER(vp)], i32), "qlx_sumtree_destroy": ([vp], i32),
+        "qlx_sumtree_set_leaves": ([vp, vp], i32), "qlx_sumtree_get": ([vp, vp, vp, vp], i32),
+        "qlx_sumtree_sample": ([vp, u64, u32, u32, u32, u64, C.c_float, u32, vp, vp], i32),
+        "qlx_sumtree_update": ([vp, vp, vp, u32, C.c_float, C.c_float], i32),
         "qlx_dist_unique_id": ([vp], i32), "qlx_learner_dist_init": ([vp, i32, i32, vp], i32),
         "qlx_learner_profile": ([vp, i32], i32),
         "qlx_learner_profile_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)], i32),
@@ -411,6 +423,17 @@ class SelfDrivingQLearner:
         return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
                     targets=tg[:n * B].reshape(n, B))
 
+    def priorities(self, max_updates=4096):
+        """Prioritized replay (flags & PER): IS weights [n_updates][B] of the last vector step, sum-tree leaves
+        [history_buffer_len], the priority new transitions enter with."""
+        B = self.param.batch_size
+        w = np.zeros(max_updates * B, np.float32)
+        leaves = np.zeros(self.param.history_buffer_len, np.float32)
+        pmax = C.c_float()
+        n = self.last()["losses"].shape[0]
+        _check(lib().qlx_learner_priorities(self.h, _p(w), _p(leaves), C.byref(pmax)))
+        return w[:n * B].reshape(n, B), leaves, pmax.value
+
     def dist_init(self, world, rank, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
         _check(lib().qlx_learner_dist_init(self.h, world, rank, buf))
@@ -612,6 +635,48 @@ class BallGameLearner:
 
 
 TF_DTYPES = {1: np.float32, 2: np.float64, 3: np.int32, 9: np.int64}
+
+
+class SumTree:
+    """Proportional prioritized-replay sum tree in HBM (per.hip; beyond the reference, SURVEY §8f #3)."""
+
+    def __init__(self, capacity, device=0):
+        self.capacity = int(capacity)
+        h = C.c_void_p()
+        _check(lib().qlx_sumtree_create(self.capacity, device, C.byref(h)))
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().qlx_sumtree_destroy(self.h)
+        self.h = None
+
+    __del__ = close
+
+    def set_leaves(self, leaves):
+        x = np.ascontiguousarray(leaves, dtype=np.float32)
+        if x.shape != (self.capacity,):
+            raise ValueError("leaves must have shape (capacity,)")
+        _check(lib().qlx_sumtree_set_leaves(self.h, _p(x)))
+
+    def get(self):
+        leaves = np.zeros(self.capacity, np.float32)
+        total, pmax = C.c_float(), C.c_float()
+        _check(lib().qlx_sumtree_get(self.h, _p(leaves), C.byref(total), C.byref(pmax)))
+        return leaves, total.value, pmax.value
+
+    def sample(self, seed, first_update, n_updates, rank, length, beta, batch):
+        slots = np.zeros(n_updates * batch, np.uint64)
+        w = np.zeros(n_updates * batch, np.float32)
+        _check(lib().qlx_sumtree_sample(self.h, seed, first_update, n_updates, rank, length, beta, batch, _p(slots), _p(w)))
+        return slots.reshape(n_updates, batch), w.reshape(n_updates, batch)
+
+    def update(self, slots, td_abs, alpha, eps):
+        s_ = np.ascontiguousarray(slots, dtype=np.uint64).ravel()
+        t_ = np.ascontiguousarray(td_abs, dtype=np.float32).ravel()
+        if s_.shape != t_.shape:
+            raise ValueError("slots and td_abs must have the same length")
+        _check(lib().qlx_sumtree_update(self.h, _p(s_), _p(t_), s_.shape[0], alpha, eps))
 
 
 class TfBundle:

@@ -41,8 +41,15 @@ class LearnerParams(C.Structure):
         ("learner_seed", C.c_uint64),
         ("init_seed", C.c_uint64),
         ("rank", C.c_uint32),
-        ("pad", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("per_alpha", C.c_float),
+        ("per_beta", C.c_float),
+        ("per_eps", C.c_float),
+        ("pad2", C.c_uint32),
     ]
+
+
+DOUBLE_DQN, PER = 1, 2   # LearnerParams.flags (include/qlx.h QLX_LEARNER_*)
 
 
 def default_params(**kw):
@@ -51,7 +58,8 @@ def default_params(**kw):
                       epsilon_min=0.1, epsilon_greedy_steps=1_000_000.0, max_steps_per_episode=10_000,
                       epsilon_pure_random_steps=50_000, history_buffer_len=1_000_000, update_after_actions=4,
                       target_sync_steps=0, episode_reward_history_buffer_len=100, n_envs=1, batch_size=32,
-                      env_seed=0x51A5EED, learner_seed=1, init_seed=2, rank=0, pad=0)
+                      env_seed=0x51A5EED, learner_seed=1, init_seed=2, rank=0, flags=0, per_alpha=0.6,
+                      per_beta=0.4, per_eps=1e-6, pad2=0)
     for k, v in kw.items():
         setattr(p, k, v)
     return p
@@ -131,6 +139,8 @@ def lib():
         L.orc_learner_env_tensor.argtypes = [vp, u32, vp]
         L.orc_learner_replay_get.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.orc_learner_params_size.restype = C.c_size_t
+        L.orc_learner_per.argtypes = [vp, vp, vp, vp]
+        L.orc_per_sample.argtypes = [vp, u64, u64, u32, u32, u32, u64, f32, i32, vp, vp, vp]
         L.orc_state_size.restype = C.c_size_t
         # BallGame (oracle/ballgame_ref.h)
         L.orc_bg_state_size.restype = C.c_size_t
@@ -315,6 +325,17 @@ class QNet:
         return loss, out, norms
 
 
+def per_sample(leaves, seed, first_update, n_updates, rank, length, beta, batch):
+    """oracle/learner_ref.h SumTree + per_sample over the given leaves: (slots [U][B], IS weights [U][B], total)"""
+    x = np.ascontiguousarray(leaves, dtype=np.float32)
+    slots = np.zeros(n_updates * batch, np.uint64)
+    w = np.zeros(n_updates * batch, np.float32)
+    total = C.c_float()
+    lib().orc_per_sample(_p(x), x.shape[0], seed, first_update, n_updates, rank, length, beta, batch, _p(slots), _p(w),
+                         C.byref(total))
+    return slots.reshape(n_updates, batch), w.reshape(n_updates, batch), total.value
+
+
 class Learner:
     def __init__(self, params):
         self.params = params
@@ -354,6 +375,15 @@ class Learner:
         n = lib().orc_learner_last(self.h, _p(a), _p(r), _p(d), _p(losses), _p(idx), _p(tg), _p(q))
         return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
                     targets=tg[:n * B].reshape(n, B), q=q)
+
+    def priorities(self):
+        """(IS weights [n_updates][B] of the last vector step, sum-tree leaves [cap], per_max)"""
+        n = self.last()["losses"].shape[0]
+        w = np.zeros(max(n, 1) * self.B, np.float32)
+        leaves = np.zeros(self.params.history_buffer_len, np.float32)
+        pmax = C.c_float()
+        lib().orc_learner_per(self.h, _p(w), _p(leaves), C.byref(pmax))
+        return w[:n * self.B].reshape(n, self.B), leaves, pmax.value
 
     def qnet(self, which=0):
         return QNet(handle=lib().orc_learner_qnet(self.h, which), owned=False)
