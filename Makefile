@@ -15,7 +15,7 @@ STRICT := -ffp-contract=off
 LDFLAGS := -shared -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 
 OBJS := $(OUT)/obj/common.o $(OUT)/obj/env_breakout.o $(OUT)/obj/replay.o $(OUT)/obj/qnet.o $(OUT)/obj/learner.o \
-        $(OUT)/obj/ballgame.o $(OUT)/obj/tf_bundle.o $(OUT)/obj/per.o
+        $(OUT)/obj/ballgame.o $(OUT)/obj/tf_bundle.o $(OUT)/obj/per.o $(OUT)/obj/stats.o
 
 HDRS := include/qlx.h $(wildcard $(SRC)/*.h)
 
@@ -50,6 +50,9 @@ $(OUT)/obj/ballgame.o: $(SRC)/ballgame.hip $(HDRS) | $(OUT)/obj
 
 # sum-tree descent and IS weights are compared bit-for-bit with the oracle: no contraction
 $(OUT)/obj/per.o: $(SRC)/per.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
+
+$(OUT)/obj/stats.o: $(SRC)/stats.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
 
 $(OUT)/libqlx.so: $(OBJS)

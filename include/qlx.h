@@ -203,6 +203,13 @@ int32_t qlx_learner_last(qlx_learner* l, uint8_t* actions, float* rewards, uint8
  * [n_updates][B], the sum tree's leaves [history_buffer_len] (priority^alpha per physical replay slot), the
  * priority new transitions enter with; any may be NULL. */
 int32_t qlx_learner_priorities(qlx_learner* l, float* is_weights, float* leaves, float* per_max);
+/* Learning statistics (learning_update_log, self_driving_tf_q_learner.rs:235-273): per-action counts over the
+ * replay's actions [3] (device histogram), the episode reward history oldest first (n = entries, up to cap
+ * copied), and the log text itself (UTF-8; *len = full length, buf gets up to cap - 1 bytes + NUL).  Actions are
+ * listed in numeric order (the reference iterates a hash map). */
+int32_t qlx_learner_action_counts(qlx_learner* l, uint64_t* counts);
+int32_t qlx_learner_episode_rewards(qlx_learner* l, float* out, uint64_t cap, uint64_t* n);
+int32_t qlx_learner_update_log(qlx_learner* l, char* buf, size_t cap, size_t* len);
 qlx_env* qlx_learner_env(qlx_learner* l);
 qlx_replay* qlx_learner_replay(qlx_learner* l);
 qlx_model* qlx_learner_model(qlx_learner* l, int32_t which /* 0 online, 1 target */);
@@ -219,6 +226,16 @@ int32_t qlx_learner_profile_filter(qlx_learner* l, const char* name_or_null);
 int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* total_us, double* total_work,
                                 uint64_t* launches);
 int32_t qlx_learner_profile_names(qlx_learner* l, char* buf, size_t cap);
+
+/* ---------------- DBSCAN over f32 (src/ql/src/util/dbscan.rs:209-341) ----------------
+ * cluster_analysis(values, max_neighbor_distance, core_point_min_neighbors) with Distance = |a - b|, exact, in
+ * O(n log n): labels[i] = cluster position (clusters ordered by lowest member index, as the reference returns
+ * them) or -1 for noise.  _format renders the reference's Display ("Yx(B..C), ..., Yx(noise)", :91-133).
+ * Values and max_neighbor_distance must be finite, max_neighbor_distance >= 0. */
+int32_t qlx_dbscan_f32(const float* values, uint64_t n, float max_neighbor_distance, uint64_t core_point_min_neighbors,
+                       int32_t* labels, uint64_t* n_clusters);
+int32_t qlx_dbscan_f32_format(const float* values, uint64_t n, float max_neighbor_distance, uint64_t core_point_min_neighbors,
+                              char* buf, size_t cap, size_t* len);
 
 /* ---------------- prioritized-replay sum tree (beyond the reference) ----------------
  * The learner's HBM sum tree as a standalone object: leaves = priorities of `capacity` slots, proportional
@@ -286,6 +303,10 @@ int32_t qlx_bg_learner_sync(qlx_bg_learner* l);
 int32_t qlx_bg_learner_stats_get(qlx_bg_learner* l, qlx_learner_stats* out);
 int32_t qlx_bg_learner_last(qlx_bg_learner* l, uint8_t* actions, float* rewards, uint8_t* dones, float* losses,
                             uint64_t* indices, float* targets, uint32_t* n_updates);
+/* learning_update_log for BallGame: counts [5] by numeric action, reward history, log text (qlx_learner_* above) */
+int32_t qlx_bg_learner_action_counts(qlx_bg_learner* l, uint64_t* counts);
+int32_t qlx_bg_learner_episode_rewards(qlx_bg_learner* l, float* out, uint64_t cap, uint64_t* n);
+int32_t qlx_bg_learner_update_log(qlx_bg_learner* l, char* buf, size_t cap, size_t* len);
 qlx_bg_env* qlx_bg_learner_env(qlx_bg_learner* l);
 qlx_bg_model* qlx_bg_learner_model(qlx_bg_learner* l, int32_t which /* 0 online, 1 target */);
 

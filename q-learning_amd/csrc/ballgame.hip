@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "objects.h"
+#include "stats.h"
 
 namespace qlx {
 namespace bg {
@@ -976,6 +977,49 @@ int32_t qlx_bg_learner_stats_get(qlx_bg_learner* L, qlx_learner_stats* out) {
     float loss = 0.0f;
     if (L->last_updates) QLX_HIP(hipMemcpy(&loss, L->d_losses + L->last_updates - 1, 4, hipMemcpyDeviceToHost));
     out->last_loss = loss;
+  });
+}
+
+static std::vector<float> bg_episode_rewards(qlx_bg_learner* L) {
+  QLX_HIP(hipStreamSynchronize(L->stream));
+  Book b;
+  QLX_HIP(hipMemcpy(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost));
+  std::vector<float> ring(L->p.episode_reward_history_buffer_len), out(b.hist_len);
+  QLX_HIP(hipMemcpy(ring.data(), L->d_hist, ring.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < b.hist_len; ++i) out[i] = ring[(b.hist_head + i) % ring.size()];
+  return out;
+}
+
+int32_t qlx_bg_learner_action_counts(qlx_bg_learner* L, uint64_t* counts) {
+  return guard([&] {
+    QLX_CHECK(L && counts, QLX_E_INVALID, "null argument");
+    std::vector<uint64_t> c;
+    action_counts(L->stream, L->d_ra, std::min(L->total, L->cap), bg::kA, c);
+    std::copy(c.begin(), c.end(), counts);
+  });
+}
+
+int32_t qlx_bg_learner_episode_rewards(qlx_bg_learner* L, float* out, uint64_t cap, uint64_t* n) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    const std::vector<float> r = bg_episode_rewards(L);
+    if (n) *n = r.size();
+    if (out) std::copy(r.begin(), r.begin() + std::min<uint64_t>(cap, r.size()), out);
+  });
+}
+
+int32_t qlx_bg_learner_update_log(qlx_bg_learner* L, char* buf, size_t cap, size_t* len) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    // BallGameAction Display (ballgame_test_environment.rs:222-234) by numeric value West 0 .. Nothing 4
+    static const char* const kNames[bg::kA] = {"\xE2\x86\x90", "\xE2\x86\x91", "\xE2\x86\x92", "\xE2\x86\x93", "o"};
+    qlx_learner_stats st;
+    int32_t rc = qlx_bg_learner_stats_get(L, &st);
+    QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+    LogInputs in{st.episode_count, st.step_count, L->p.gamma, st.epsilon, 9.5f, L->p.lowest_episode_reward_goal_threshold_pct,
+                 bg_episode_rewards(L), {}, kNames};
+    action_counts(L->stream, L->d_ra, std::min(L->total, L->cap), bg::kA, in.counts);
+    copy_text(learning_log(in), buf, cap, len);
   });
 }
 

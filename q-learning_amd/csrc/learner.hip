@@ -21,6 +21,7 @@
 #include "profiler.h"
 #include "qnet.h"
 #include "replay_dev.h"
+#include "stats.h"
 
 namespace qlx {
 
@@ -544,6 +545,49 @@ int32_t qlx_learner_priorities(qlx_learner* L, float* is_weights, float* leaves,
     if (U && is_weights) QLX_HIP(hipMemcpy(is_weights, L->prio.d_w, (size_t)U * L->B * 4, hipMemcpyDeviceToHost));
     if (leaves) QLX_HIP(hipMemcpy(leaves, L->prio.leaves(), L->prio.cap * 4, hipMemcpyDeviceToHost));
     if (per_max) QLX_HIP(hipMemcpy(per_max, L->prio.d_max, 4, hipMemcpyDeviceToHost));
+  });
+}
+
+// ---- learning statistics (learning_update_log, self_driving_tf_q_learner.rs:235-273; stats.hip) ----
+static std::vector<float> learner_episode_rewards(qlx_learner* L) {
+  QLX_HIP(hipStreamSynchronize(L->stream));
+  Book b;
+  QLX_HIP(hipMemcpy(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost));
+  std::vector<float> ring(L->p.episode_reward_history_buffer_len), out(b.hist_len);
+  QLX_HIP(hipMemcpy(ring.data(), L->d_hist, ring.size() * sizeof(float), hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < b.hist_len; ++i) out[i] = ring[(b.hist_head + i) % ring.size()];
+  return out;
+}
+
+int32_t qlx_learner_action_counts(qlx_learner* L, uint64_t* counts) {
+  return guard([&] {
+    QLX_CHECK(L && counts, QLX_E_INVALID, "null argument");
+    std::vector<uint64_t> c;
+    action_counts(L->stream, L->rb->d_action, L->rb->len(), kActions, c);
+    std::copy(c.begin(), c.end(), counts);
+  });
+}
+
+int32_t qlx_learner_episode_rewards(qlx_learner* L, float* out, uint64_t cap, uint64_t* n) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    const std::vector<float> r = learner_episode_rewards(L);
+    if (n) *n = r.size();
+    if (out) std::copy(r.begin(), r.begin() + std::min<uint64_t>(cap, r.size()), out);
+  });
+}
+
+int32_t qlx_learner_update_log(qlx_learner* L, char* buf, size_t cap, size_t* len) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    static const char* const kNames[kActions] = {"None", "Left", "Right"};   // BreakoutAction Debug
+    qlx_learner_stats st;
+    int32_t rc = qlx_learner_stats_get(L, &st);
+    QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+    LogInputs in{st.episode_count, st.step_count, L->p.gamma, st.epsilon, (float)(kNumBricks - 1),
+                 L->p.lowest_episode_reward_goal_threshold_pct, learner_episode_rewards(L), {}, kNames};
+    action_counts(L->stream, L->rb->d_action, L->rb->len(), kActions, in.counts);
+    copy_text(learning_log(in), buf, cap, len);
   });
 }
 

@@ -132,6 +132,13 @@ def lib():
         "qlx_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_learner_env": ([vp], vp), "qlx_learner_replay": ([vp], vp), "qlx_learner_model": ([vp, i32], vp),
         "qlx_learner_priorities": ([vp, vp, vp, vp], i32),
+        "qlx_learner_action_counts": ([vp, vp], i32), "qlx_bg_learner_action_counts": ([vp, vp], i32),
+        "qlx_learner_episode_rewards": ([vp, vp, u64, C.POINTER(u64)], i32),
+        "qlx_bg_learner_episode_rewards": ([vp, vp, u64, C.POINTER(u64)], i32),
+        "qlx_learner_update_log": ([vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)], i32),
+        "qlx_bg_learner_update_log": ([vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)], i32),
+        "qlx_dbscan_f32": ([vp, u64, C.c_float, u64, vp, C.POINTER(u64)], i32),
+        "qlx_dbscan_f32_format": ([vp, u64, C.c_float, u64, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)], i32),
         "qlx_sumtree_create": ([u64, i32, C.POINTER(vp)], i32), "qlx_sumtree_destroy": ([vp], i32),
         "qlx_sumtree_set_leaves": ([vp, vp], i32), "qlx_sumtree_get": ([vp, vp, vp, vp], i32),
         "qlx_sumtree_sample": ([vp, u64, u32, u32, u32, u64, C.c_float, u32, vp, vp], i32),
@@ -169,6 +176,52 @@ def lib():
         fn.restype = res
     _lib = L
     return L
+
+
+def _text(fn, *args):
+    n = C.c_size_t()
+    _check(fn(*args, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value + 1)
+    _check(fn(*args, buf, n.value + 1, C.byref(n)))
+    return buf.raw[:n.value].decode("utf-8")
+
+
+def cluster_analysis(elements, max_neighbor_distance, core_point_min_neighbors):
+    """dbscan::cluster_analysis (dbscan.rs:209-262) over f32 values: (clusters as index lists ordered by their lowest
+    member, noise indices)"""
+    x = np.ascontiguousarray(elements, dtype=np.float32)
+    labels = np.zeros(x.shape[0], np.int32)
+    nc = C.c_uint64()
+    _check(lib().qlx_dbscan_f32(_p(x), x.shape[0], max_neighbor_distance, core_point_min_neighbors, _p(labels), C.byref(nc)))
+    clusters = [np.flatnonzero(labels == c).tolist() for c in range(nc.value)]
+    return clusters, np.flatnonzero(labels < 0).tolist()
+
+
+def cluster_analysis_text(elements, max_neighbor_distance, core_point_min_neighbors):
+    """Display of the ClusterAnalysisResult<f32> (dbscan.rs:91-133)"""
+    x = np.ascontiguousarray(elements, dtype=np.float32)
+    return _text(lib().qlx_dbscan_f32_format, _p(x), x.shape[0], max_neighbor_distance, core_point_min_neighbors)
+
+
+class _LearningStats:
+    """learning_update_log (self_driving_tf_q_learner.rs:235-273) for a learner handle"""
+    _prefix = "qlx_learner"
+
+    def action_counts(self):
+        out = np.zeros(self._n_actions, np.uint64)
+        _check(getattr(lib(), self._prefix + "_action_counts")(self.h, _p(out)))
+        return out
+
+    def episode_rewards(self):
+        n = C.c_uint64()
+        fn = getattr(lib(), self._prefix + "_episode_rewards")
+        _check(fn(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, np.float32)
+        _check(fn(self.h, _p(out), n.value, C.byref(n)))
+        return out
+
+    def learning_update_log(self):
+        return _text(getattr(lib(), self._prefix + "_update_log"), self.h)
 
 
 def exported_symbols():
@@ -372,8 +425,9 @@ class DeepQLearningModel:
         _check(lib().qlx_model_read_checkpoint(self.h, path.encode()))
 
 
-class SelfDrivingQLearner:
+class SelfDrivingQLearner(_LearningStats):
     """SelfDrivingQLearner with n parallel envs on one GPU (vector-step generalisation)."""
+    _n_actions = 3
 
     def __init__(self, param, device=0):
         self.param = param
@@ -585,8 +639,10 @@ class BallGameModel:
         return (float(loss[0]), g, nrm) if want_grads else float(loss[0])
 
 
-class BallGameLearner:
+class BallGameLearner(_LearningStats):
     """SelfDrivingQLearner over n BallGame envs on one GPU (same vector-step semantics as SelfDrivingQLearner)."""
+    _prefix = "qlx_bg_learner"
+    _n_actions = 5
 
     def __init__(self, param, device=0):
         self.param = param

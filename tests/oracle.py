@@ -141,6 +141,12 @@ def lib():
         L.orc_learner_params_size.restype = C.c_size_t
         L.orc_learner_per.argtypes = [vp, vp, vp, vp]
         L.orc_per_sample.argtypes = [vp, u64, u64, u32, u32, u32, u64, f32, i32, vp, vp, vp]
+        L.orc_dbscan_f32.argtypes = [vp, u64, f32, u64, vp]
+        L.orc_dbscan_f32.restype = u64
+        L.orc_dbscan_f32_format.argtypes = [vp, u64, f32, u64, C.c_char_p, C.c_size_t]
+        L.orc_dbscan_f32_format.restype = C.c_size_t
+        L.orc_update_log.argtypes = [u64, u64, f32, C.c_double, f32, f32, vp, u64, vp, i32, i32, C.c_char_p, C.c_size_t]
+        L.orc_update_log.restype = C.c_size_t
         L.orc_state_size.restype = C.c_size_t
         # BallGame (oracle/ballgame_ref.h)
         L.orc_bg_state_size.restype = C.c_size_t
@@ -323,6 +329,33 @@ class QNet:
             out.append(grads[off:off + VAR_SIZES[v]].reshape(VAR_SHAPES[v]))
             off += VAR_SIZES[v]
         return loss, out, norms
+
+
+def cluster_analysis(elements, eps, min_neighbors):
+    """oracle/stats_ref.cpp generic DBSCAN: (clusters as index lists, noise indices)"""
+    x = np.ascontiguousarray(elements, dtype=np.float32)
+    labels = np.zeros(x.shape[0], np.int32)
+    nc = lib().orc_dbscan_f32(_p(x), x.shape[0], eps, min_neighbors, _p(labels))
+    return [np.flatnonzero(labels == c).tolist() for c in range(nc)], np.flatnonzero(labels < 0).tolist()
+
+
+def cluster_analysis_text(elements, eps, min_neighbors):
+    x = np.ascontiguousarray(elements, dtype=np.float32)
+    n = lib().orc_dbscan_f32_format(_p(x), x.shape[0], eps, min_neighbors, None, 0)
+    buf = C.create_string_buffer(n + 1)
+    lib().orc_dbscan_f32_format(_p(x), x.shape[0], eps, min_neighbors, buf, n + 1)
+    return buf.raw[:n].decode("utf-8")
+
+
+def update_log(episode_count, step_count, gamma, epsilon, goal_mean, pct, rewards, counts, ballgame=False):
+    """oracle/stats_ref.cpp learning_update_log text"""
+    r = np.ascontiguousarray(rewards, dtype=np.float32)
+    c = np.ascontiguousarray(counts, dtype=np.uint64)
+    args = (episode_count, step_count, gamma, epsilon, goal_mean, pct, _p(r), r.shape[0], _p(c), c.shape[0], int(ballgame))
+    n = lib().orc_update_log(*args, None, 0)
+    buf = C.create_string_buffer(n + 1)
+    lib().orc_update_log(*args, buf, n + 1)
+    return buf.raw[:n].decode("utf-8")
 
 
 def per_sample(leaves, seed, first_update, n_updates, rank, length, beta, batch):
