@@ -104,6 +104,13 @@ struct Epi4StoreF32 {   // out[m][n] = v (fp32); sq (optional): [tiles] partials
   }
 };
 
+// sum of squares of 4 values with explicit roundings: a tile's clip_by_norm partial does not depend on where
+// the compiler chooses to contract into FMAs
+__device__ __forceinline__ float sq4(f32x4 v) {
+  return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(v[0], v[0]), __fmul_rn(v[1], v[1])), __fmul_rn(v[2], v[2])),
+                   __fmul_rn(v[3], v[3]));
+}
+
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
   typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
   const bf16x4v v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
@@ -297,9 +304,9 @@ __device__ __forceinline__ void gemm_tile(const GemmProblem<Epi>& P, int tile) {
           const f32x4 v = {acc[t][j][4 * u], acc[t][j][4 * u + 1], acc[t][j][4 * u + 2], acc[t][j][4 * u + 3]};
           epi(m, n, v, bz);
           if constexpr (Epi::kSq) {
-            const float q = ((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]) + v[3] * v[3];
-            if (m == ones_m) sq_ones += q;
-            else sq_main += q;
+            const float q = sq4(v);
+            if (m == ones_m) sq_ones = __fadd_rn(sq_ones, q);
+            else sq_main = __fadd_rn(sq_main, q);
           }
         }
       }

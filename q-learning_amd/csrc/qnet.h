@@ -57,6 +57,9 @@ struct qlx_model {
   int* d_sqf_first = nullptr;
   bool norms_fused = false;   // set by model_norms: Adam reads d_sqf / d_sqf_first instead
   float* d_norms = nullptr;
+  // XCD-aware block -> tile table of the fc1 backward launch (built per batch size, qnet.hip fc1_bwd_map)
+  int* d_fc1bwd_map = nullptr;
+  int fc1bwd_map_B = -1, fc1bwd_grid = 0, fc1bwd_cap = 0;
   void* ws = nullptr;
   int ws_batch = 0;
   int last_batch = 0;

@@ -42,6 +42,16 @@ static int sq_first(int v) {
   return o;
 }
 
+// tf.clip_by_norm + ResourceApplyAdam (legacy Keras) for one element
+__device__ __forceinline__ float adam_elem(float g, float scale, float clipnorm, float denom, float alpha, float beta1,
+                                           float beta2, float eps, float& m, float& v, float w) {
+  // explicit roundings (no contraction): the same bits wherever this is inlined, and the oracle's order
+  const float gc = (g * scale * clipnorm) / denom;
+  m = __fadd_rn(m, __fmul_rn(__fsub_rn(gc, m), 1.0f - beta1));
+  v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(gc, gc), v), 1.0f - beta2));
+  return __fsub_rn(w, __fmul_rn(m, alpha) / __fadd_rn(sqrtf(v), eps));
+}
+
 // ------------------------------------------------------------------------------------------
 // weight packing: fp32 master (Keras layouts) -> bf16 MFMA operand layouts
 
@@ -303,16 +313,52 @@ __device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, fl
   }
 }
 
-// fc1 backward (dW3 + db3 tiles, then dz3 tiles) and the dense-3 weight gradient in one launch
+// fc1 backward (dW3 + db3 tiles, then dz3 tiles) and the dense-3 weight gradient in one launch; block b runs
+// unit map[b] (pair tile < tiles, then fc2 wgrad blocks; -1 = idle), see fc1_bwd_map
 template <class E1, class E2>
-__global__ __launch_bounds__(256, 2) void k_fc1_bwd(GemmProblem<E1> Pw, GemmProblem<E2> Pd, Fc2WgradArgs F) {
-  const int t = blockIdx.x, tg = Pw.tiles() + Pd.tiles();
+__global__ __launch_bounds__(256, 2) void k_fc1_bwd(GemmProblem<E1> Pw, GemmProblem<E2> Pd, Fc2WgradArgs F, const int* map) {
+  const int t = map[blockIdx.x], tg = Pw.tiles() + Pd.tiles();
+  if (t < 0) return;
   if (t < tg) {
     gemm_pair_block<true, true, E1, false, false, E2>(Pw, Pd, t);
   } else {
     extern __shared__ __attribute__((aligned(16))) bf16 lds[];
     fc2_wgrad_block(F, t - tg, reinterpret_cast<float*>(lds));
   }
+}
+
+// Block -> unit table of k_fc1_bwd.  Blocks b and b + 8 share an XCD (round-robin dispatch), so the table gives
+// each XCD whole operand panels: the dW3 tiles of a3 column panels {x, x + 8, ..} (all 4 dz4 panels each) and
+// the dz3 tiles of W3 panels {x + 4, x + 12, ..} (all batch panels each), then its share of the fc2 wgrad
+// blocks.  Every a3 / W3 panel is fetched into one L2 instead of up to eight, and both GEMMs (16 vs 8 k-steps
+// per tile) spread evenly over the XCDs.
+template <class E1, class E2>
+static void fc1_bwd_map(qlx_model* m, const GemmProblem<E1>& Pw, const GemmProblem<E2>& Pd, int extra, hipStream_t s) {
+  if (m->fc1bwd_map_B == Pd.M) return;
+  std::vector<int> lists[8];
+  auto tile_of = [](const auto& P, int mi, int nj) {
+    return P.n_fastest ? mi * P.tiles_n + nj : nj * P.tiles_m + mi;
+  };
+  for (int mi = 0; mi < Pw.tiles_m; ++mi)
+    for (int nj = 0; nj < Pw.tiles_n; ++nj) lists[mi % 8].push_back(tile_of(Pw, mi, nj));
+  for (int nj = 0; nj < Pd.tiles_n; ++nj)
+    for (int mi = 0; mi < Pd.tiles_m; ++mi) lists[(nj + 4) % 8].push_back(Pw.tiles() + tile_of(Pd, mi, nj));
+  const int tg = Pw.tiles() + Pd.tiles();
+  for (int j = 0; j < extra; ++j) lists[j % 8].push_back(tg + j);
+  size_t per = 0;
+  for (auto& l : lists) per = std::max(per, l.size());
+  std::vector<int> map(8 * per, -1);
+  for (int x = 0; x < 8; ++x)
+    for (size_t l = 0; l < lists[x].size(); ++l) map[l * 8 + x] = lists[x][l];
+  if ((int)map.size() > m->fc1bwd_cap) {
+    QLX_HIP(hipStreamSynchronize(s));
+    if (m->d_fc1bwd_map) (void)hipFree(m->d_fc1bwd_map);
+    QLX_HIP(hipMalloc(&m->d_fc1bwd_map, map.size() * sizeof(int)));
+    m->fc1bwd_cap = (int)map.size();
+  }
+  QLX_HIP(hipMemcpy(m->d_fc1bwd_map, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice));
+  m->fc1bwd_grid = (int)map.size();
+  m->fc1bwd_map_B = Pd.M;
 }
 
 void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s) {
@@ -348,6 +394,8 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* g, const int64_t* ra
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+constexpr int kAdamMaxPartials = 832;   // norm partials per variable (the largest: W3's 784 k_sumsq ranges)
+
 struct AdamArgs {
   float* w;
   float* m;
@@ -376,8 +424,19 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     offs[kNumVars] = o;
   }
   for (int v = wave; v < kNumVars; v += 4) {
+    // all of a lane's partials are loaded before the first add (one memory latency, not one per partial),
+    // then summed in the lane-strided order
+    const int first = A.var_first[v], last = A.var_first[v + 1];
+    float p[kAdamMaxPartials / 64];
+#pragma unroll
+    for (int k = 0; k < kAdamMaxPartials / 64; ++k) {
+      const int r = first + lane + 64 * k;
+      p[k] = r < last ? A.partial[r] : 0.0f;
+    }
     float t = 0.0f;
-    for (int r = A.var_first[v] + lane; r < A.var_first[v + 1]; r += 64) t += A.partial[r];
+#pragma unroll
+    for (int k = 0; k < kAdamMaxPartials / 64; ++k)
+      if (first + lane + 64 * k < last) t += p[k];
     for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
     if (lane == 0) {
       nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
@@ -390,11 +449,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     int var = 0;
     while (i >= offs[var + 1]) ++var;
     const float denom = fmaxf(nrm[var], A.clipnorm);
-    const float gc = (A.g[i] * A.scale * A.clipnorm) / denom;
-    float m = A.m[i], v = A.v[i], w = A.w[i];
-    m += (gc - m) * (1.0f - A.beta1);
-    v += (gc * gc - v) * (1.0f - A.beta2);
-    w -= (m * A.alpha) / (sqrtf(v) + A.eps);
+    float m = A.m[i], v = A.v[i];
+    const float w = adam_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
     A.m[i] = m;
     A.v[i] = v;
     A.w[i] = w;
@@ -557,19 +613,22 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
   //   dz3 = (dz4 W3^T) * (a3 > 0)
   {
     ProfScope ps(m->prof, "fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
-    const auto Pw =
-        gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136);
-    QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
     const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
     const Fc2WgradArgs F{w.a4, actions, w.gs, w.hs, B, G + var_offset(8), G + var_offset(9), loss_dev,
                          m->d_sqf + sq_first(8), m->d_sqf + sq_first(9)};
-    auto kern = k_fc1_bwd<Epi4StoreF32, Epi4ReluMask>;
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(kern, GemmCfg::LDS);
-      attr = true;
-    }
-    hipLaunchKernelGGL(kern, dim3(Pw.tiles() + Pd.tiles() + kFc2WgradBlocks), dim3(256), GemmCfg::LDS, s, Pw, Pd, F);
+    auto launch = [&](const auto& Pw, auto kern) {
+      QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
+      static bool attr = false;   // one per instantiation
+      if (!attr) {
+        set_lds_attr(kern, GemmCfg::LDS);
+        attr = true;
+      }
+      fc1_bwd_map(m, Pw, Pd, kFc2WgradBlocks, s);
+      hipLaunchKernelGGL(kern, dim3(m->fc1bwd_grid), dim3(256), GemmCfg::LDS, s, Pw, Pd, F, (const int*)m->d_fc1bwd_map);
+    };
+    launch(gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1,
+                        Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136),
+           k_fc1_bwd<Epi4StoreF32, Epi4ReluMask>);
   }
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
@@ -738,6 +797,8 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
       off += kVarSize[v];
     }
     vf[kNumVars] = (int)rb.size();
+    for (int v = 0; v < kNumVars; ++v)
+      QLX_CHECK(vf[v + 1] - vf[v] <= kAdamMaxPartials && kSqSlots[v] <= kAdamMaxPartials, QLX_E_STATE, "k_adam partial bound");
     m->n_ranges = (int)rb.size();
     QLX_HIP(hipMalloc(&m->d_rbeg, rb.size() * 8));
     QLX_HIP(hipMalloc(&m->d_rend, re.size() * 8));
@@ -771,7 +832,7 @@ int32_t qlx_model_destroy(qlx_model* m) {
     (void)hipSetDevice(m->device);
     (void)hipStreamSynchronize(m->stream);
     void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wb3,
-                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->d_sqf, m->d_sqf_first, m->ws};
+                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->d_sqf, m->d_sqf_first, m->ws, m->d_fc1bwd_map};
     for (void* p : ptrs) (void)hipFree(p);
     if (m->own_stream) (void)hipStreamDestroy(m->stream);
     delete m;

@@ -4,6 +4,7 @@
 //   ./scripts/ubench
 #include "../q-learning_amd/csrc/common.cpp"
 #include "../q-learning_amd/csrc/qnet.hip"
+#include "../q-learning_amd/csrc/tf_bundle.cpp"
 
 #include <cstdio>
 #include <functional>
@@ -208,7 +209,7 @@ int main(int argc, char** argv) {
     return 0;
   }
   // ---- fc1 GEMMs: variants (register stages S, occupancy, XCD remap)
-#define VARIANTS(X) X(2, 2, false, 0) X(2, 2, true, 0) X(2, 2, true, 1) X(2, 2, true, 2) X(2, 1, true, 0) X(2, 1, true, 1) X(2, 1, true, 2)
+#define VARIANTS(X) X(2, 2, false, 0) X(2, 2, true, 0) X(2, 2, true, 1) X(2, 2, true, 2) X(3, 2, true, 0) X(3, 2, true, 1) X(2, 1, true, 0) X(3, 1, true, 0) X(3, 1, true, 1)
   for (int B : {1024, 8192}) {
     const double fl = 2.0 * B * 512 * 3136;
     char nm[128];

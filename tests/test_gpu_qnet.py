@@ -174,3 +174,4 @@ def test_multi_step_training_stays_close():
     q, _ = m.q_values(x)
     # Adam turns gradient noise into fixed-size steps (~lr per element): allow 10% of max|Q| after 5 steps
     assert close(q, ref.forward(x), 1e-1)
+
