@@ -665,7 +665,7 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
       set_lds_attr(kern, lds);
       attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3(used3 * 3 + used2 * 2), dim3(kTrunkThreads), lds, s, w.a2, w.dz3, per3, used3,
+    hipLaunchKernelGGL(kern, dim3(wgrad_blocks(3, used3) + wgrad_blocks(2, used2)), dim3(kTrunkThreads), lds, s, w.a2, w.dz3, per3, used3,
                        w.slab + kSlabConv3, w.a1, w.dz2, per2, used2, w.slab + kSlabConv2, B);
   }
   const int grid1 = trunk_grid(B);

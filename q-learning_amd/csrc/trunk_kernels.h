@@ -742,17 +742,31 @@ __device__ __forceinline__ void conv_wgrad_body(const bf16* __restrict__ in, con
   }
 }
 
-// conv3 (blocks [0, 3*used3): chunk t % used3, tap group t / used3) and conv2 (the rest) in one launch
+// Block -> (chunk, tap group) of a G-group layer whose blocks start at grid offset t0: blocks b and b + 8 share an
+// XCD (round-robin dispatch), so the G tap groups of one sample chunk are blocks 8 G k + 8 g + x (consecutive
+// dispatch, one XCD) - each sample's activations and dz come from HBM once and from that XCD's L2 for the
+// other groups.  Returns false for the padding blocks of the last round.
+template <int G>
+__device__ __forceinline__ bool wgrad_chunk_group(int t, int used, int& chunk, int& group) {
+  const int x = t & 7, r = t >> 3;
+  group = r % G;
+  chunk = (r / G) * 8 + x;
+  return chunk < used;
+}
+__host__ __device__ __forceinline__ int wgrad_blocks(int groups, int used) { return (used + 7) / 8 * 8 * groups; }
+
+// conv3 (blocks [0, wgrad_blocks(3, used3))) and conv2 (the rest) in one launch
 __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv23_wgrad(const bf16* __restrict__ a2, const bf16* __restrict__ dz3,
                                                                    int per3, int used3, float* slab3, const bf16* __restrict__ a1,
                                                                    const bf16* __restrict__ dz2, int per2, int used2,
                                                                    float* slab2, int B) {
-  int t = blockIdx.x;
-  if (t < 3 * used3) {
-    conv_wgrad_body<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>(a2, dz3, B, per3, slab3, t % used3, t / used3);
-  } else {
-    t -= 3 * used3;
-    conv_wgrad_body<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>(a1, dz2, B, per2, slab2, t % used2, t / used2);
+  const int t = blockIdx.x, n3 = wgrad_blocks(3, used3);
+  int chunk, group;
+  if (t < n3) {
+    if (wgrad_chunk_group<3>(t, used3, chunk, group))
+      conv_wgrad_body<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>(a2, dz3, B, per3, slab3, chunk, group);
+  } else if (wgrad_chunk_group<2>(t - n3, used2, chunk, group)) {
+    conv_wgrad_body<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>(a1, dz2, B, per2, slab2, chunk, group);
   }
 }
 
