@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--replay-ratio", type=int, default=8, help="samples per env-step (reference: 32 per 4 steps)")
     ap.add_argument("--replay", type=int, default=100_000, help="replay capacity per GPU (config C2: 100k)")
-    ap.add_argument("--cpu-sample", type=int, default=400, help="env-steps of the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=2000, help="env-steps of the CPU baseline sample, ~15 s (0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=3)
     return ap.parse_args()
 

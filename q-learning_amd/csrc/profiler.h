@@ -43,6 +43,16 @@ struct Profiler {
     (void)hipEventRecord(r.b, s);
     pending.push_back(r);
   }
+  // Event pair bound to one kernel dispatch (hipExtLaunchKernelGGL start/stop events): no marker packets
+  // around the kernel, so the elapsed time is the kernel's own, as a kernel trace reports it.  Both null when
+  // the scope is not recorded.
+  void ext(const char* name, double work, hipEvent_t* a, hipEvent_t* b) {
+    *a = *b = nullptr;
+    if (!enabled || (!filter.empty() && filter != name)) return;
+    *a = take();
+    *b = take();
+    pending.push_back({name, *a, *b, work});
+  }
   void collect() {   // after the stream is synchronised
     for (auto& r : pending) {
       float ms = 0.0f;

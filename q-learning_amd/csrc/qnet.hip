@@ -5,6 +5,7 @@
 // create_ql_model_ballgame_3x3x4_5_512.py:71-78), legacy keras Adam(lr 2.5e-4, clipnorm 1.0) =
 // tf.clip_by_norm per variable + ResourceApplyAdam (saved_model.pb op names), Huber(delta=1) mean.
 // The reference runs this inside libtensorflow behind Session::run (q_learning_model.rs:107-189).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -547,8 +548,11 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
   const float* p = m->d_params;
   {  // conv1 -> conv2 -> conv3 fused per sample (trunk_kernels.h)
     // scope per role so each maps to one kernel instantiation (trunk_fwd = online pass with stored activations)
-    ProfScope ps(m->prof, store_acts ? "trunk_fwd" : "trunk_fwd_nostore", s,
-                 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576));
+    // timed with dispatch-bound events (bench.py's roofline kernel: its average must match rocprofv3's)
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (m->prof)
+      m->prof->ext(store_acts ? "trunk_fwd" : "trunk_fwd_nostore", 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576),
+                   &ea, &eb);
     static bool attr = false;
     if (!attr) {
       set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
@@ -556,8 +560,9 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
       attr = true;
     }
     auto kern = store_acts ? k_trunk_fwd<true> : k_trunk_fwd<false>;
-    hipLaunchKernelGGL(kern, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkFwdLds, s, table, B, m->wf0, m->wf1, m->wf2,
-                       p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3, nullptr);
+    hipExtLaunchKernelGGL(kern, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkFwdLds, s, ea, eb, 0u, table, B, m->wf0, m->wf1,
+                          m->wf2, p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3,
+                          (unsigned long long*)nullptr);
   }
   {  // fc1: M = B, N = 512, K = 3136.  Small batches split K into kFc1Split fp32 slabs (reduced with bias +
      // ReLU in fixed order) to fill the chip; from 64 M tiles on (B >= 8192) one pass with the epilogue fused
