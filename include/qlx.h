@@ -303,6 +303,8 @@ int32_t qlx_bg_learner_sync(qlx_bg_learner* l);
 int32_t qlx_bg_learner_stats_get(qlx_bg_learner* l, qlx_learner_stats* out);
 int32_t qlx_bg_learner_last(qlx_bg_learner* l, uint8_t* actions, float* rewards, uint8_t* dones, float* losses,
                             uint64_t* indices, float* targets, uint32_t* n_updates);
+/* prioritized replay state of a learner created with QLX_LEARNER_PER (as qlx_learner_priorities) */
+int32_t qlx_bg_learner_priorities(qlx_bg_learner* l, float* is_weights, float* leaves, float* per_max);
 /* learning_update_log for BallGame: counts [5] by numeric action, reward history, log text (qlx_learner_* above) */
 int32_t qlx_bg_learner_action_counts(qlx_bg_learner* l, uint64_t* counts);
 int32_t qlx_bg_learner_episode_rewards(qlx_bg_learner* l, float* out, uint64_t cap, uint64_t* n);

@@ -160,7 +160,7 @@ void bg_net_forward(const BgNet& n, const uint8_t* x, int B, BgActs& a) {
 }
 
 float bg_net_loss_backward(const BgNet& n, const uint8_t* x, const uint8_t* actions, const float* y, int B, const BgActs& a,
-                           BgGrads& g) {
+                           BgGrads& g, const float* weights, float* td_abs) {
   for (int v = 0; v < kBgVars; ++v) g.g[v].assign(kBgVarSize[v], 0.0f);
   const float *k1 = n.w[2].data(), *k2 = n.w[4].data(), *k3 = n.w[6].data();
   // MSE (mean over the batch) of e = q_a - y: dL/dq_a = 2 e / B
@@ -168,8 +168,10 @@ float bg_net_loss_backward(const BgNet& n, const uint8_t* x, const uint8_t* acti
   double loss = 0.0;
   for (int b = 0; b < B; ++b) {
     const float e = a.q[(size_t)b * 5 + actions[b]] - y[b];
-    loss += (double)e * (double)e;
-    dq[(size_t)b * 5 + actions[b]] = 2.0f * e / (float)B;
+    const float w = weights ? weights[b] : 1.0f;   // prioritized-replay IS weight
+    loss += (double)w * ((double)e * (double)e);
+    dq[(size_t)b * 5 + actions[b]] = 2.0f * (w * e) / (float)B;
+    if (td_abs) td_abs[b] = std::fabs(e);
   }
   std::vector<float> dz3((size_t)B * 512), dz2((size_t)B * 288), dz1((size_t)B * 288);
   for (int u = 0; u < 512; ++u)
@@ -273,7 +275,7 @@ void bg_net_apply_adam(BgNet& n, const BgGrads& g, float* norms_out) {
 void generate_distinct_random_ids(uint64_t seed, uint32_t update_idx, uint32_t rank, uint64_t len, int B, uint64_t* out);
 int argmax_first(const float* q, int n);
 
-BgLearner::BgLearner(const BgParams& prm) : p(prm) {
+BgLearner::BgLearner(const BgParams& prm) : p(prm), tree(prm.history_buffer_len) {
   envs.resize(p.n_envs);
   ep_reward.assign(p.n_envs, 0.0f);
   ep_steps.assign(p.n_envs, 0);
@@ -331,6 +333,8 @@ void BgLearner::vector_step() {   // learner_ref.cpp vector_step over BallGame
     t.done = done;
     if (replay.size() >= p.history_buffer_len) replay.pop_front();
     replay.push_back(t);
+    if (p.flags & 2u) tree.set(total_pushed % p.history_buffer_len, per_max);   // new transitions at max priority
+    total_pushed += 1;
     ep_reward[e] += r;
     ep_steps[e] += 1;
     last_rewards[e] = r;
@@ -350,40 +354,75 @@ void BgLearner::vector_step() {   // learner_ref.cpp vector_step over BallGame
     }
   }
   const uint64_t triggers = step_count / p.update_after_actions - step_before / p.update_after_actions;
-  if (replay.size() > p.batch_size)
-    for (uint64_t t = 0; t < triggers; ++t) update();
+  if (replay.size() > p.batch_size && triggers > 0) {   // all batches sampled and targeted up front (learner_ref.cpp)
+    const int B = (int)p.batch_size;
+    const uint64_t len = replay.size();
+    std::vector<uint64_t> idx((size_t)triggers * B);
+    std::vector<float> isw((size_t)triggers * B, 1.0f), y((size_t)triggers * B);
+    for (uint64_t t = 0; t < triggers; ++t) {
+      if (p.flags & 2u) {
+        const uint64_t start = (total_pushed - len) % p.history_buffer_len;
+        std::vector<uint64_t> slots(B);
+        per_sample(tree, p.learner_seed, (uint32_t)(update_count + t), p.rank, len, p.per_beta, B, slots.data(), &isw[t * B]);
+        for (int b = 0; b < B; ++b) idx[t * B + b] = (slots[b] + p.history_buffer_len - start) % p.history_buffer_len;
+      } else {
+        generate_distinct_random_ids(p.learner_seed, (uint32_t)(update_count + t), p.rank, len, B, &idx[t * B]);
+      }
+    }
+    for (uint64_t t = 0; t < triggers; ++t) targets(&idx[t * B], &y[t * B]);
+    for (uint64_t t = 0; t < triggers; ++t) update(&idx[t * B], (p.flags & 2u) ? &isw[t * B] : nullptr, &y[t * B]);
+  }
   if (p.target_sync_steps > 0 && step_count / p.target_sync_steps != step_before / p.target_sync_steps)
     for (int v = 0; v < kBgVars; ++v) target.w[v] = online.w[v];
   vec_steps += 1;
 }
 
-void BgLearner::update() {
+// y = r + gamma max_a Q_target(s') (or, double DQN, r + gamma Q_target(s', argmax_a Q_online(s'))); r if done
+void BgLearner::targets(const uint64_t* idx, float* y) const {
   const int B = (int)p.batch_size;
-  std::vector<uint64_t> idx(B);
-  generate_distinct_random_ids(p.learner_seed, (uint32_t)update_count, p.rank, replay.size(), B, idx.data());
-  std::vector<uint8_t> xs((size_t)B * kBgObs), xn((size_t)B * kBgObs), act(B), dn(B);
-  std::vector<float> rew(B), y(B);
+  std::vector<uint8_t> xn((size_t)B * kBgObs);
+  for (int b = 0; b < B; ++b) bg_obs(replay[idx[b]].s_next, &xn[(size_t)b * kBgObs]);
+  BgActs at, an;
+  bg_net_forward(target, xn.data(), B, at);
+  if (p.flags & 1u) bg_net_forward(online, xn.data(), B, an);
+  for (int b = 0; b < B; ++b) {
+    const BgTransition& t = replay[idx[b]];
+    float v;
+    if (p.flags & 1u) {
+      v = at.q[(size_t)b * 5 + argmax_first(&an.q[(size_t)b * 5], 5)];
+    } else {
+      v = at.q[(size_t)b * 5];
+      for (int j = 1; j < 5; ++j) v = std::max(v, at.q[(size_t)b * 5 + j]);
+    }
+    y[b] = t.done ? t.reward : t.reward + v * p.gamma;
+  }
+}
+
+void BgLearner::update(const uint64_t* idx, const float* isw, const float* y) {
+  const int B = (int)p.batch_size;
+  std::vector<uint8_t> xs((size_t)B * kBgObs), act(B);
   for (int b = 0; b < B; ++b) {
     const BgTransition& t = replay[idx[b]];
     bg_obs(t.s, &xs[(size_t)b * kBgObs]);
-    bg_obs(t.s_next, &xn[(size_t)b * kBgObs]);
-    act[b] = t.action; rew[b] = t.reward; dn[b] = t.done ? 1 : 0;
-  }
-  BgActs at;
-  bg_net_forward(target, xn.data(), B, at);
-  for (int b = 0; b < B; ++b) {
-    float mx = at.q[(size_t)b * 5];
-    for (int j = 1; j < 5; ++j) mx = std::max(mx, at.q[(size_t)b * 5 + j]);
-    y[b] = dn[b] ? rew[b] : rew[b] + mx * p.gamma;
+    act[b] = t.action;
   }
   BgActs ao;
   bg_net_forward(online, xs.data(), B, ao);
   BgGrads g;
-  const float loss = bg_net_loss_backward(online, xs.data(), act.data(), y.data(), B, ao, g);
+  std::vector<float> td(B);
+  const float loss = bg_net_loss_backward(online, xs.data(), act.data(), y, B, ao, g, isw, td.data());
   bg_net_apply_adam(online, g, nullptr);
+  if (p.flags & 2u) {   // (|td| + eps)^alpha per drawn slot, the last draw wins
+    const uint64_t start = (total_pushed - replay.size()) % p.history_buffer_len;
+    for (int b = 0; b < B; ++b) {
+      const float pr = std::pow(td[b] + p.per_eps, p.per_alpha);
+      tree.set((start + idx[b]) % p.history_buffer_len, pr);
+      per_max = std::max(per_max, pr);
+    }
+  }
   last_losses.push_back(loss);
-  last_indices.insert(last_indices.end(), idx.begin(), idx.end());
-  last_targets.insert(last_targets.end(), y.begin(), y.end());
+  last_indices.insert(last_indices.end(), idx, idx + B);
+  last_targets.insert(last_targets.end(), y, y + B);
   update_count += 1;
 }
 

@@ -21,6 +21,7 @@
 #include <deque>
 #include <vector>
 
+#include "learner_ref.h"
 #include "rng_ref.h"
 
 namespace orc {
@@ -67,8 +68,9 @@ struct BgGrads { std::vector<float> g[kBgVars]; };
 
 void bg_net_init_glorot(BgNet& n, uint64_t seed);       // stream (seed, var, 1, P_INIT)
 void bg_net_forward(const BgNet& n, const uint8_t* x /*[B][36]*/, int B, BgActs& a);
+// MSE, raw gradients; weights (optional) per-sample loss weights, td_abs (optional) |q_a - y| out
 float bg_net_loss_backward(const BgNet& n, const uint8_t* x, const uint8_t* actions, const float* y, int B, const BgActs& a,
-                           BgGrads& g);                  // MSE, raw gradients
+                           BgGrads& g, const float* weights = nullptr, float* td_abs = nullptr);
 void bg_net_apply_adam(BgNet& n, const BgGrads& g, float* norms_out /*[8] or null*/);
 
 // ---------------- learner (the vectorised SelfDrivingQLearner of learner_ref.h over BallGame) -------------
@@ -103,6 +105,9 @@ struct BgLearner {
   std::vector<float> ep_reward;
   std::vector<uint64_t> ep_steps;
   std::deque<BgTransition> replay;
+  uint64_t total_pushed = 0;   // prioritized replay (flags bit 1): SumTree over physical slots (learner_ref.h)
+  SumTree tree;
+  float per_max = 1.0f;
   BgNet online, target;
   uint64_t step_count = 0, vec_steps = 0, update_count = 0, episode_count = 0;
   double epsilon;
@@ -114,7 +119,8 @@ struct BgLearner {
 
   explicit BgLearner(const BgParams& prm);
   void vector_step();
-  void update();
+  void targets(const uint64_t* idx, float* y) const;
+  void update(const uint64_t* idx, const float* isw, const float* y);
   bool solved() const;
 };
 

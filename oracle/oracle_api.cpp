@@ -340,5 +340,10 @@ int orc_bg_learner_last(void* h, uint8_t* actions, float* rewards, uint8_t* done
   return (int)l->last_losses.size();
 }
 void orc_bg_learner_env_state(void* h, uint32_t e, BgState* out) { *out = ((BgLearner*)h)->envs[e].s; }
+void orc_bg_learner_per(void* h, float* leaves, float* per_max) {   // sum-tree leaves [cap], per_max
+  BgLearner* l = (BgLearner*)h;
+  if (leaves) std::memcpy(leaves, l->tree.t.data() + l->tree.L, l->p.history_buffer_len * 4);
+  if (per_max) *per_max = l->per_max;
+}
 
 }  // extern "C"

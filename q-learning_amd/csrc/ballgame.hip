@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "objects.h"
+#include "per.h"
 #include "stats.h"
 
 namespace qlx {
@@ -216,11 +217,14 @@ struct HeadArgs {
   const uint8_t* dones;
   float gamma;
   float* y_out;
+  const float* q_select;   // mode 2, double DQN: [B][5] online Q(s'); y uses q[first argmax] instead of max q
   const uint8_t* actions;  // mode 3 (train)
   const float* y;
   float* dq;               // [B][5]
   float* hs;               // [B] squared errors
   float* dz3;              // [B][512]
+  const float* weights;    // mode 3 (optional): per-sample loss weights (prioritized-replay IS weights)
+  float* td_abs;           // mode 3 (optional): |q_a - y| out
 };
 
 // dense 512 -> 5, one wave per sample.  MODE 0: q; 1: argmax (predict_action); 2: y = r + gamma max q (or r if
@@ -252,15 +256,24 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs H) {
   }
   if (MODE == 2 && lane == 0) {
     float mx = q[0];
-    for (int k = 1; k < kA; ++k) mx = fmaxf(mx, q[k]);
+    if (H.q_select) {   // double DQN
+      const float* qs = H.q_select + (size_t)b * kA;
+      int best = 0;
+      for (int k = 1; k < kA; ++k) if (qs[k] > qs[best]) best = k;
+      mx = q[best];
+    } else {
+      for (int k = 1; k < kA; ++k) mx = fmaxf(mx, q[k]);
+    }
     H.y_out[b] = H.dones[b] ? H.rewards[b] : H.rewards[b] + mx * H.gamma;
   }
   if (MODE == 3) {
     const int act = H.actions[b];
     const float e = q[act] - H.y[b];
-    const float g = 2.0f * e / (float)H.B;
+    const float wt = H.weights ? H.weights[b] : 1.0f;
+    const float g = 2.0f * (wt * e) / (float)H.B;
     if (lane == 0) {
-      H.hs[b] = e * e;
+      H.hs[b] = wt * (e * e);
+      if (H.td_abs) H.td_abs[b] = fabsf(e);
       for (int k = 0; k < kA; ++k) H.dq[(size_t)b * kA + k] = k == act ? g : 0.0f;
     }
     for (int n = lane; n < 512; n += 64) H.dz3[(size_t)b * 512 + n] = a[n] > 0.0f ? g * w[n * kA + act] : 0.0f;
@@ -430,7 +443,7 @@ static void head(const HeadArgs& h, hipStream_t s) {
 
 // MSE head + backward after forward() on the same batch: loss -> *loss_dev, raw gradients -> m->d_grads
 static void backward(qlx_bg_model* m, const uint8_t* d_obs, int B, const uint8_t* d_act, const float* d_y, float* loss_dev,
-                     hipStream_t s) {
+                     hipStream_t s, const float* weights = nullptr, float* td_abs = nullptr) {
   BgWs& w = m->w;
   float* G = m->d_grads;
   const float* P = m->d_params;
@@ -440,6 +453,8 @@ static void backward(qlx_bg_model* m, const uint8_t* d_obs, int B, const uint8_t
   h.dq = w.dq;
   h.hs = w.hs;
   h.dz3 = w.dz3;
+  h.weights = weights;
+  h.td_abs = td_abs;
   head<3>(h, s);
   colsum(s, w.hs, B, 1, 1, loss_dev, 1.0f / (float)B);                          // MSE mean
   gemm<true, false, 0>(s, 512, kA, B, w.a3, 512, w.dq, kA, G + var_off(6), kA);  // dW3 = a3^T dq
@@ -512,6 +527,9 @@ struct qlx_bg_learner {
   uint64_t* d_idx = nullptr;
   uint8_t *d_xs = nullptr, *d_xn = nullptr, *d_bact = nullptr, *d_bdone = nullptr;
   float *d_brew = nullptr, *d_targets = nullptr, *d_losses = nullptr;
+  float* d_qsel = nullptr;   // double DQN: online Q(s') of the step's batches [U*B][5]
+  bool ddqn = false, per = false;
+  qlx::PerState prio;
   uint64_t step_count = 0, vec_steps = 0, update_count = 0;
   uint32_t last_updates = 0;
 };
@@ -568,6 +586,7 @@ static void learner_vector_step(qlx_bg_learner* L) {
   L->step_count += N;
   hipLaunchKernelGGL(k_step_push, dim3((N + 255) / 256), dim3(256), 0, s, env->d_state, env->d_ep_steps, N, L->d_actions,
                      L->d_rewards, L->d_dones, L->d_rs, L->d_rsn, L->d_ra, L->d_rr, L->d_rd, L->total, L->cap);
+  if (L->per) per_launch_push(s, L->prio.leaves(), L->cap, L->total, N, L->prio.d_max);
   L->total += N;
   launch_episode_book(s, N, L->d_rewards, L->d_dones, env->d_ep_steps, L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
                       (uint32_t)L->p.episode_reward_history_buffer_len, L->d_book, L->d_reset);
@@ -580,13 +599,28 @@ static void learner_vector_step(qlx_bg_learner* L) {
   if (len > B && triggers > 0) {
     const uint32_t U = (uint32_t)triggers;
     QLX_CHECK(U <= L->max_updates, QLX_E_STATE, "too many updates per vector step");
-    launch_sample_distinct(s, L->p.learner_seed, (uint32_t)L->update_count, U, L->p.rank, len, B, L->d_idx);
+    const uint64_t start = (L->total - len) % L->cap;
+    if (L->per) {
+      per_launch_build(s, L->prio.d_tree, L->prio.L);
+      per_launch_sample(s, L->prio.d_tree, L->prio.L, L->p.learner_seed, (uint32_t)L->update_count, U, L->p.rank, len,
+                        L->p.per_beta, B, L->cap, start, L->d_idx, L->prio.d_w);
+    } else {
+      launch_sample_distinct(s, L->p.learner_seed, (uint32_t)L->update_count, U, L->p.rank, len, B, L->d_idx);
+    }
     const uint32_t n = U * B;
     hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, s, L->d_rs, L->d_rsn, L->d_ra, L->d_rr, L->d_rd, L->total, len,
                        L->cap, L->d_idx, n, L->d_xs, L->d_xn, L->d_bact, L->d_brew, L->d_bdone);
-    // targets of all U updates from the fixed target weights (a sync happens only between vector steps)
+    // targets of all U updates from the fixed target weights (a sync happens only between vector steps); double
+    // DQN picks a* with the online weights as they stand before this step's updates
+    if (L->ddqn) {
+      forward(L->online, L->d_xn, (int)n, s);
+      HeadArgs o = head_args(L->online, (int)n);
+      o.q = L->d_qsel;
+      head<0>(o, s);
+    }
     forward(L->target, L->d_xn, (int)n, s);
     HeadArgs t = head_args(L->target, (int)n);
+    t.q_select = L->ddqn ? L->d_qsel : nullptr;
     t.rewards = L->d_brew;
     t.dones = L->d_bdone;
     t.gamma = L->p.gamma;
@@ -595,10 +629,14 @@ static void learner_vector_step(qlx_bg_learner* L) {
     for (uint32_t u = 0; u < U; ++u) {
       const uint8_t* xs = L->d_xs + (size_t)u * B * kObs;
       forward(L->online, xs, (int)B, s);
-      backward(L->online, xs, (int)B, L->d_bact + (size_t)u * B, L->d_targets + (size_t)u * B, L->d_losses + u, s);
+      backward(L->online, xs, (int)B, L->d_bact + (size_t)u * B, L->d_targets + (size_t)u * B, L->d_losses + u, s,
+               L->per ? L->prio.d_w + (size_t)u * B : nullptr, L->per ? L->prio.d_td + (size_t)u * B : nullptr);
       apply_adam(L->online, s);
       L->update_count += 1;
     }
+    if (L->per)
+      per_launch_update(s, L->d_idx, L->prio.d_td, n, L->cap, start, L->p.per_alpha, L->p.per_eps, L->prio.d_owner,
+                        L->prio.leaves(), L->prio.d_max);
     L->last_updates = U;
   }
   const uint64_t ts = L->p.target_sync_steps;
@@ -860,8 +898,13 @@ int32_t qlx_bg_learner_create(const qlx_params* p, int32_t device, qlx_bg_learne
     QLX_CHECK(p->n_envs > 0 && p->batch_size > 0 && p->batch_size <= 4096, QLX_E_INVALID, "bad n_envs / batch_size");
     QLX_CHECK(p->update_after_actions > 0 && p->history_buffer_len >= p->batch_size, QLX_E_INVALID, "bad parameters");
     QLX_CHECK(p->episode_reward_history_buffer_len > 0, QLX_E_INVALID, "episode_reward_history_buffer_len must be > 0");
+    QLX_CHECK((p->flags & ~(QLX_LEARNER_DOUBLE_DQN | QLX_LEARNER_PER)) == 0, QLX_E_INVALID, "unknown learner flags");
+    QLX_CHECK(!(p->flags & QLX_LEARNER_PER) || (p->per_alpha >= 0.0f && p->per_beta >= 0.0f && p->per_eps > 0.0f),
+              QLX_E_INVALID, "prioritized replay needs alpha >= 0, beta >= 0, eps > 0");
     current_device_checked(device);
     auto* L = new qlx_bg_learner;
+    L->ddqn = (p->flags & QLX_LEARNER_DOUBLE_DQN) != 0;
+    L->per = (p->flags & QLX_LEARNER_PER) != 0;
     L->p = *p;
     L->device = device;
     L->N = p->n_envs;
@@ -916,6 +959,11 @@ int32_t qlx_bg_learner_create(const qlx_params* p, int32_t device, qlx_bg_learne
     QLX_HIP(hipMemsetAsync(L->d_q, 0, (size_t)N * kA * 4, L->stream));
     model_workspace(L->online, (int)std::max(N, B));
     model_workspace(L->target, (int)UB);
+    if (L->ddqn) {
+      model_workspace(L->online, (int)UB);
+      QLX_HIP(hipMalloc(&L->d_qsel, UB * kA * 4));
+    }
+    if (L->per) L->prio.init(L->cap, UB);
     QLX_HIP(hipStreamSynchronize(L->stream));
     *out = L;
   });
@@ -931,8 +979,9 @@ int32_t qlx_bg_learner_destroy(qlx_bg_learner* L) {
     qlx_bg_model_destroy(L->target);
     void* ptrs[] = {L->d_rs, L->d_rsn, L->d_ra, L->d_rd, L->d_rr, L->d_obs, L->d_actions, L->d_dones, L->d_reset, L->d_rewards,
                     L->d_q, L->d_eps, L->d_ep_reward, L->d_hist, L->d_book, L->d_idx, L->d_xs, L->d_xn, L->d_bact, L->d_bdone,
-                    L->d_brew, L->d_targets, L->d_losses};
+                    L->d_brew, L->d_targets, L->d_losses, L->d_qsel};
     for (void* p : ptrs) (void)hipFree(p);
+    L->prio.release();
     (void)hipStreamDestroy(L->stream);
     delete L;
   });
@@ -1020,6 +1069,17 @@ int32_t qlx_bg_learner_update_log(qlx_bg_learner* L, char* buf, size_t cap, size
                  bg_episode_rewards(L), {}, kNames};
     action_counts(L->stream, L->d_ra, std::min(L->total, L->cap), bg::kA, in.counts);
     copy_text(learning_log(in), buf, cap, len);
+  });
+}
+
+int32_t qlx_bg_learner_priorities(qlx_bg_learner* L, float* is_weights, float* leaves, float* per_max) {
+  return guard([&] {
+    QLX_CHECK(L && L->per, QLX_E_STATE, "learner was created without QLX_LEARNER_PER");
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    const uint32_t U = L->last_updates;
+    if (U && is_weights) QLX_HIP(hipMemcpy(is_weights, L->prio.d_w, (size_t)U * L->B * 4, hipMemcpyDeviceToHost));
+    if (leaves) QLX_HIP(hipMemcpy(leaves, L->prio.leaves(), L->prio.cap * 4, hipMemcpyDeviceToHost));
+    if (per_max) QLX_HIP(hipMemcpy(per_max, L->prio.d_max, 4, hipMemcpyDeviceToHost));
   });
 }
 

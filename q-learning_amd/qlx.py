@@ -162,6 +162,7 @@ def lib():
         "qlx_bg_learner_stats_get": ([vp, C.POINTER(LearnerStats)], i32),
         "qlx_bg_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_bg_learner_env": ([vp], vp), "qlx_bg_learner_model": ([vp, i32], vp),
+        "qlx_bg_learner_priorities": ([vp, vp, vp, vp], i32),
         "qlx_bg_model_load_tf": ([vp, C.c_char_p], i32), "qlx_model_load_tf": ([vp, C.c_char_p], i32),
         "qlx_tf_bundle_open": ([C.c_char_p, C.POINTER(vp)], i32), "qlx_tf_bundle_close": ([vp], i32),
         "qlx_tf_bundle_count": ([vp], i32),
@@ -676,6 +677,16 @@ class BallGameLearner(_LearningStats):
 
     def solved(self):
         return bool(self.stats()["solved"])
+
+    def priorities(self, max_updates=4096):
+        """Prioritized replay (flags & PER): IS weights [n_updates][B] of the last vector step, sum-tree leaves, per_max."""
+        B = self.param.batch_size
+        w = np.zeros(max_updates * B, np.float32)
+        leaves = np.zeros(self.param.history_buffer_len, np.float32)
+        pmax = C.c_float()
+        n = self.last()["losses"].shape[0]
+        _check(lib().qlx_bg_learner_priorities(self.h, _p(w), _p(leaves), C.byref(pmax)))
+        return w[:n * B].reshape(n, B), leaves, pmax.value
 
     def last(self, max_updates=4096):
         N, B = self.param.n_envs, self.param.batch_size

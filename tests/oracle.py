@@ -141,6 +141,7 @@ def lib():
         L.orc_learner_params_size.restype = C.c_size_t
         L.orc_learner_per.argtypes = [vp, vp, vp, vp]
         L.orc_per_sample.argtypes = [vp, u64, u64, u32, u32, u32, u64, f32, i32, vp, vp, vp]
+        L.orc_bg_learner_per.argtypes = [vp, vp, vp]
         L.orc_dbscan_f32.argtypes = [vp, u64, f32, u64, vp]
         L.orc_dbscan_f32.restype = u64
         L.orc_dbscan_f32_format.argtypes = [vp, u64, f32, u64, C.c_char_p, C.c_size_t]
@@ -553,6 +554,13 @@ class BgLearner:
         n = lib().orc_bg_learner_last(self.h, _p(a), _p(r), _p(d), _p(losses), _p(idx), _p(tg))
         return dict(actions=a, rewards=r, dones=d, losses=losses[:n], indices=idx[:n * B].reshape(n, B),
                     targets=tg[:n * B].reshape(n, B))
+
+    def priorities(self):
+        """(sum-tree leaves [cap], per_max) of prioritized replay"""
+        leaves = np.zeros(self.params.history_buffer_len, np.float32)
+        pmax = C.c_float()
+        lib().orc_bg_learner_per(self.h, _p(leaves), C.byref(pmax))
+        return leaves, pmax.value
 
     def net(self, which=0):
         return BgNet(handle=lib().orc_bg_learner_net(self.h, which), owned=False)

@@ -192,3 +192,52 @@ def test_reference_saved_weights_load_and_forward():
     x = rand_obs(256, 4)
     q, _ = m.q_values(x)
     assert np.allclose(q, ref.forward(x), rtol=1e-4, atol=1e-5)
+
+
+def test_double_dqn_prioritized_learner_matches_oracle():
+    """BallGame learner with double DQN + prioritized replay vs the oracle: identical first prioritized batches
+    (every leaf at the initial max priority), priorities (|td| + eps)^alpha from the same TD errors, and the
+    counters; later draws follow each side's own priorities."""
+    qlx = _qlx()
+    gpu, ref = make_learners(update_after_actions=32, flags=qlx.DOUBLE_DQN | qlx.PER, epsilon_pure_random_steps=10**6)
+    first = None
+    for v in range(12):
+        gpu.vector_step()
+        ref.vector_step()
+        g, r = gpu.last(), ref.last()
+        assert np.array_equal(g["actions"], r["actions"]) and np.array_equal(g["rewards"], r["rewards"]), v
+        if not len(r["losses"]):
+            continue
+        wg, lg, pg = gpu.priorities()
+        lr, pr = ref.priorities()
+        assert ((wg > 0) & (wg <= 1)).all() and (wg.max(axis=1) == 1.0).all()
+        assert pg >= lg.max() * (1 - 1e-6)
+        if first is None:
+            first = v
+            assert np.array_equal(g["indices"], r["indices"])
+            assert (wg == 1.0).all()
+            assert np.allclose(g["targets"], r["targets"], rtol=1e-3, atol=1e-3)
+            assert np.allclose(lg, lr, rtol=1e-4, atol=1e-6)   # fp32 nets: TD errors agree closely
+    assert first is not None
+    sg, sr = gpu.stats(), ref.counters()
+    for k in ("step_count", "update_count", "replay_len"):
+        assert sg[k] == sr[k], k
+
+
+def test_double_dqn_prioritized_learner_learns_ballgame():
+    """End-to-end learning check of the extensions: double DQN + prioritized replay also masters the game."""
+    qlx = _qlx()
+    gpu, _ = make_learners(n_envs=64, batch_size=256, history_buffer_len=100_000, epsilon_pure_random_steps=5_000,
+                           epsilon_greedy_steps=60_000.0, epsilon_min=0.01, target_sync_steps=2_000,
+                           episode_reward_history_buffer_len=200, update_after_actions=8,
+                           flags=qlx.DOUBLE_DQN | qlx.PER)
+    best = -100.0
+    for chunk in range(40):
+        gpu.run(100)
+        st = gpu.stats()
+        best = max(best, st["running_reward"])
+        if st["running_reward"] >= 9.0:
+            break
+    print(f"\nballgame ddqn+per learning: running_reward {st['running_reward']:.3f} after {st['step_count']} env-steps, "
+          f"{st['update_count']} updates, {st['episode_count']} episodes")
+    assert best >= 9.0, (best, st)
