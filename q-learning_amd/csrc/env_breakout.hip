@@ -366,11 +366,13 @@ __constant__ int8_t c_brick_row[kFrame];
 
 __device__ __forceinline__ uint64_t fbits_h(float f) { return f == 0.0f ? 0ull : (uint64_t)f32_bits(f); }
 
-// One wave (64 lanes) per env: rasterise the frame of the step just taken into ring slot
-// (next_slot - 1) & 3, s2d layout; optionally fold it into the env's running checksum.
+// One 256-thread block per env: rasterise the frame of the step just taken into ring slot (next_slot - 1) & 3,
+// s2d layout (441 16-pixel blocks, ~2 per thread); HASH folds it into the env's running checksum (wrapping u64
+// sums: any reduction order gives the same bits).
+template <bool HASH>
 __global__ __launch_bounds__(256) void k_env_raster(const State* st, uint32_t n, uint8_t* obs, uint64_t* hashes) {
-  const uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  const uint32_t e = blockIdx.x;
+  const int tid = threadIdx.x;
   if (e >= n) return;
   const State s = st[e];
   const int slot = (s.next_slot + 3) & 3;
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(256) void k_env_raster(const State* st, uint32_t n,
   const float S = 600.0f / 84.0f;
   const float rr = 10.0f * 10.0f;
   uint64_t hf = 0;
-  for (int blk = lane; blk < kBlocks * kBlocks; blk += 64) {
+  for (int blk = tid; blk < kBlocks * kBlocks; blk += 256) {
     const int X = blk / kBlocks, Y = blk - X * kBlocks;   // X: image x / 4, Y: image y / 4
     uint32_t w[4];
 #pragma unroll
@@ -398,15 +400,19 @@ __global__ __launch_bounds__(256) void k_env_raster(const State* st, uint32_t n,
         const float ddx = wx - s.ball_x, ddy = wy - s.ball_y;
         if (ddx * ddx + ddy * ddy <= rr) v = 236;
         word |= v << (8 * dy);
-        hf += (uint64_t)v * ((uint64_t)(py * kFrame + px + 1) * kH1);
+        if constexpr (HASH) hf += (uint64_t)v * ((uint64_t)(py * kFrame + px + 1) * kH1);
       }
       w[dx] = word;
     }
     reinterpret_cast<uint4*>(frame)[blk] = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  if (hashes) {
+  if constexpr (HASH) {
+    __shared__ uint64_t part[4];
     for (int off = 32; off > 0; off >>= 1) hf += __shfl_xor(hf, off);
-    if (lane == 0) {
+    if ((tid & 63) == 0) part[tid >> 6] = hf;
+    __syncthreads();
+    if (tid == 0) {
+      hf = part[0] + part[1] + part[2] + part[3];
       const uint64_t f[15] = {fbits_h(s.ball_x), fbits_h(s.ball_y), fbits_h(s.dir_x), fbits_h(s.dir_y),
                               fbits_h(s.panel_min_x), fbits_h(s.panel_min_y), fbits_h(s.panel_max_x),
                               fbits_h(s.panel_max_y), fbits_h(s.panel_speed), s.score, s.finished, s.next_slot,
@@ -465,8 +471,10 @@ void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, u
   const uint32_t n = env->n;
   hipLaunchKernelGGL(k_env_step, dim3((n + 255) / 256), dim3(256), 0, env->stream, env->d_state, env->d_ep_steps, n,
                      d_actions, d_rewards, d_dones, env->acos_thr, env->d_flags);
-  hipLaunchKernelGGL(k_env_raster, dim3((n + 3) / 4), dim3(256), 0, env->stream, env->d_state, n, env->d_obs,
-                     env->hashing ? env->d_hash : nullptr);
+  if (env->hashing)
+    hipLaunchKernelGGL(k_env_raster<true>, dim3(n), dim3(256), 0, env->stream, env->d_state, n, env->d_obs, env->d_hash);
+  else
+    hipLaunchKernelGGL(k_env_raster<false>, dim3(n), dim3(256), 0, env->stream, env->d_state, n, env->d_obs, (uint64_t*)nullptr);
   QLX_HIP(hipGetLastError());
 }
 

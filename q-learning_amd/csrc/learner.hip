@@ -66,18 +66,22 @@ void launch_select_actions(hipStream_t s, uint32_t n, uint32_t n_actions, uint64
 
 // ---- episode bookkeeping (learn_episode :172-174, :214-224) -----------------------------------
 
-// One wave, envs in order: ep_reward += r; an env whose episode ended (done, or max_steps_per_episode
-// steps) pushes its reward into the FIFO of episode rewards, counts the episode and is marked for reset.
-// running_reward is refreshed (sequential f32 sum, oldest first) by every ending with episode_count >= hist
-// cap; only the last such refresh of the step survives and it sums the final FIFO, so it runs once.
-__global__ __launch_bounds__(64) void k_episode_book(uint32_t n, const float* rewards, const uint8_t* dones,
-                                                     const uint32_t* ep_steps, uint64_t max_steps, float* ep_reward,
-                                                     float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask) {
-  const int lane = threadIdx.x;
+// Envs in order: ep_reward += r; an env whose episode ended (done, or max_steps_per_episode steps) pushes its
+// reward into the FIFO of episode rewards, counts the episode and is marked for reset.  The per-env part runs
+// one thread per env (1024 per round); wave 0 then walks the round's endings in env order (ballot per 64 envs)
+// and keeps the Book.  running_reward is refreshed (sequential f32 sum, oldest first) by every ending with
+// episode_count >= hist cap; only the last such refresh of the step survives and it sums the final FIFO, so it
+// runs once: the FIFO is loaded 64 entries per lane-parallel load and summed in order with uniform lane reads.
+__global__ __launch_bounds__(1024) void k_episode_book(uint32_t n, const float* rewards, const uint8_t* dones,
+                                                       const uint32_t* ep_steps, uint64_t max_steps, float* ep_reward,
+                                                       float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask) {
+  __shared__ float s_er[1024];
+  __shared__ uint8_t s_end[1024];
+  const int tid = threadIdx.x, lane = tid & 63;
   Book b = *book;
   bool refresh = false;
-  for (uint32_t base = 0; base < n; base += 64) {
-    const uint32_t e = base + lane;
+  for (uint32_t base = 0; base < n; base += 1024) {
+    const uint32_t e = base + tid;
     bool end = false;
     float er = 0.0f;
     if (e < n) {
@@ -86,35 +90,49 @@ __global__ __launch_bounds__(64) void k_episode_book(uint32_t n, const float* re
       ep_reward[e] = end ? 0.0f : er;
       reset_mask[e] = end ? 1 : 0;
     }
-    unsigned long long bal = __ballot(end);
-    while (bal) {   // uniform loop: every lane tracks the same Book
-      const int l = __builtin_ctzll(bal);
-      bal &= bal - 1;
-      const float v = __shfl(er, l);
-      if (b.hist_len < hist_cap) {
-        if (lane == 0) hist[(b.hist_head + b.hist_len) % hist_cap] = v;
-        b.hist_len += 1;
-      } else {
-        if (lane == 0) hist[b.hist_head] = v;
-        b.hist_head = (b.hist_head + 1) % hist_cap;
+    s_er[tid] = er;
+    s_end[tid] = end ? 1 : 0;
+    __syncthreads();
+    if (tid < 64) {
+      for (int c = 0; c < 1024 && base + c < n; c += 64) {
+        const float v0 = s_er[c + lane];
+        unsigned long long bal = __ballot(s_end[c + lane] != 0);
+        while (bal) {   // uniform loop: every lane tracks the same Book
+          const int l = __builtin_ctzll(bal);
+          bal &= bal - 1;
+          const float v = __shfl(v0, l);
+          if (b.hist_len < hist_cap) {
+            if (lane == 0) hist[(b.hist_head + b.hist_len) % hist_cap] = v;
+            b.hist_len += 1;
+          } else {
+            if (lane == 0) hist[b.hist_head] = v;
+            b.hist_head = (b.hist_head + 1) % hist_cap;
+          }
+          refresh = refresh || b.episode_count >= hist_cap;
+          b.episode_count += 1;
+        }
       }
-      refresh = refresh || b.episode_count >= hist_cap;
-      b.episode_count += 1;
     }
+    __syncthreads();
   }
-  if (lane == 0) {
+  if (tid < 64) {
     if (refresh) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's FIFO stores, before the other lanes read
       float s = 0.0f;
-      for (uint32_t i = 0; i < b.hist_len; ++i) s += hist[(b.hist_head + i) % hist_cap];
+      for (uint32_t c = 0; c < b.hist_len; c += 64) {
+        const float v = c + lane < b.hist_len ? hist[(b.hist_head + c + lane) % hist_cap] : 0.0f;
+        const uint32_t m = b.hist_len - c < 64 ? b.hist_len - c : 64;
+        for (uint32_t j = 0; j < m; ++j) s += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), (int)j));
+      }
       b.running_reward = s / (float)b.hist_len;
     }
-    *book = b;
+    if (lane == 0) *book = b;
   }
 }
 
 void launch_episode_book(hipStream_t s, uint32_t n, const float* rewards, const uint8_t* dones, const uint32_t* ep_steps,
                          uint64_t max_steps, float* ep_reward, float* hist, uint32_t hist_cap, Book* book, uint8_t* reset_mask) {
-  hipLaunchKernelGGL(k_episode_book, dim3(1), dim3(64), 0, s, n, rewards, dones, ep_steps, max_steps, ep_reward, hist, hist_cap,
+  hipLaunchKernelGGL(k_episode_book, dim3(1), dim3(1024), 0, s, n, rewards, dones, ep_steps, max_steps, ep_reward, hist, hist_cap,
                      book, reset_mask);
   QLX_HIP(hipGetLastError());
 }
