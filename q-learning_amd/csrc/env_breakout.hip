@@ -212,8 +212,11 @@ __device__ void init_state(State& s, uint64_t seed, uint32_t env, uint32_t reset
   s.bricks = (1ull << kNumBricks) - 1ull;
 }
 
-// One physics tick (BreakoutMechanics::time_step) for one env.
-__device__ void time_step(State& s, uint32_t action, float acos_thr) {
+// One physics tick (BreakoutMechanics::time_step) for one env, computed by one wave: every lane holds the same
+// ball / panel state, lane o tests contact object o (4 + 60 objects = 64 lanes), and the candidate sums are
+// taken lane by lane in object order, so every float operation is the sequential one.
+static_assert(4 + kNumBricks <= 64, "one lane per contact object");
+__device__ void time_step(State& s, uint32_t action, float acos_thr, int lane) {
   using namespace phys;
   const float tg = 20000000.0f / 1000000000.0f;   // TIME_GRANULARITY.as_secs_f32()
   // Panel::proceed
@@ -239,51 +242,43 @@ __device__ void time_step(State& s, uint32_t action, float acos_thr) {
   x.panel[0] = s.panel_min_x; x.panel[1] = s.panel_min_y; x.panel[2] = s.panel_max_x; x.panel[3] = s.panel_max_y;
   x.bricks = s.bricks;
   x.acos_thr = acos_thr;
-  uint32_t fault = 0;
+  uint32_t fault = 0;   // this lane's fault bits (OR-reduced below)
+  const int o = lane;      // the object this lane tests: 0-3 walls / panel, 4 + id bricks (creation order)
   for (int move = 0;; ++move) {
     if (length(x.mv) < kSpaceGranularity) break;
     if (move > kMaxMoves) { fault |= 4u; break; }
-    // pass 1: which objects produce a candidate, their count and the shortest path (non-NaN)
-    uint64_t hitmask = 0;
-    int count = 0;
-    float shortest = INFINITY;
-    Surface su;
-    // (ContactCandidates::consider asserts the approximation range of every inserted candidate)
-    for (int o = 0; o < 4; ++o)
-      if (candidate(x, o, &su, &fault)) {
-        hitmask |= 1ull << o; ++count;
-        const float pl = su.way + su.approx;
-        if (pl < shortest) shortest = pl;
-        if (!(su.approx >= -0.0f && su.approx <= kPrediction)) fault |= 2u;
-      }
-    for (uint64_t m = x.bricks; m; m &= m - 1) {
-      const int id = __builtin_ctzll(m);
-      if (candidate(x, 4 + id, &su, &fault)) {
-        hitmask |= 1ull << (4 + id); ++count;
-        const float pl = su.way + su.approx;
-        if (pl < shortest) shortest = pl;
-        if (!(su.approx >= -0.0f && su.approx <= kPrediction)) fault |= 2u;
-      }
-    }
+    // pass 1, one object per lane: candidate, count, shortest path (ContactCandidates::consider asserts the
+    // approximation range of every inserted candidate).  The sequential "if (pl < shortest)" keeps the
+    // least non-NaN path, which a min reduction gives in any order.
+    const bool alive = o < 4 || ((x.bricks >> (o - 4)) & 1ull);
+    Surface su = {0.0f, 0.0f, F2{0.0f, 0.0f}};
+    const bool hit = alive && candidate(x, o, &su, &fault);
+    if (hit && !(su.approx >= -0.0f && su.approx <= kPrediction)) fault |= 2u;
+    const float pl = su.way + su.approx;
+    float shortest = hit && pl == pl ? pl : INFINITY;
+    for (int off = 32; off > 0; off >>= 1) shortest = fminf(shortest, __shfl_xor(shortest, off));
+    const uint64_t hitmask = __ballot(hit);
+    const int count = __builtin_popcountll(hitmask);
     if (count == 0) { x.c = add(x.c, x.mv); break; }
-    // pass 2: ContactCandidates::consider keeps {path <= shortest + 0.001} (any single candidate
-    // if it is the only one); sums run in insertion order (walls, panel, bricks ascending).
+    // pass 2: ContactCandidates::consider keeps {path <= shortest + 0.001} (any single candidate if it is the
+    // only one); sums run in insertion order (walls, panel, bricks ascending) = lane order, read lane by lane
     const float thr = shortest + kSpaceGranularity;
     F2 nsum = {0.0f, 0.0f};
     float asum = 0.0f, wsum = 0.0f;
     int kept = 0;
     Surface first = {0.0f, 0.0f, F2{0.0f, 0.0f}};
     uint64_t removed = 0;
+    auto rl = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
     for (uint64_t m = hitmask; m; m &= m - 1) {
-      const int o = __builtin_ctzll(m);
-      candidate(x, o, &su, &fault);
-      if (count > 1 && !(su.way + su.approx <= thr)) continue;
-      if (kept == 0) first = su;
-      nsum = add(nsum, su.n);
-      asum = asum + su.approx;
-      wsum = wsum + su.way;
+      const int oh = __builtin_ctzll(m);
+      const Surface c = {rl(su.way, oh), rl(su.approx, oh), F2{rl(su.n.x, oh), rl(su.n.y, oh)}};
+      if (count > 1 && !(c.way + c.approx <= thr)) continue;
+      if (kept == 0) first = c;
+      nsum = add(nsum, c.n);
+      asum = asum + c.approx;
+      wsum = wsum + c.way;
       ++kept;
-      if (o >= 4) removed |= 1ull << (o - 4);
+      if (oh >= 4) removed |= 1ull << (oh - 4);
     }
     const int nrem = __builtin_popcountll(removed);
     x.bricks &= ~removed;
@@ -301,6 +296,7 @@ __device__ void time_step(State& s, uint32_t action, float acos_thr) {
     if (length(rem) > 0.0f) { x.mv = rem; continue; }
     break;
   }
+  for (int off = 32; off > 0; off >>= 1) fault |= (uint32_t)__shfl_xor((int)fault, off);
   s.ball_x = x.c.x; s.ball_y = x.c.y;
   s.dir_x = dir.x; s.dir_y = dir.y;
   s.bricks = x.bricks;
@@ -345,20 +341,27 @@ __global__ void k_env_clear_frames(uint8_t* obs, uint32_t n, const uint8_t* mask
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < kSlots * kFramePix / 16; i += gridDim.x * blockDim.x) dst[i] = z;
 }
 
-__global__ void k_env_step(State* st, uint32_t* ep_steps, uint32_t n, const uint8_t* actions, float* rewards,
-                           uint8_t* dones, float acos_thr, uint32_t* bad_action) {
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per env (4 envs per 256-thread block)
+__global__ __launch_bounds__(256) void k_env_step(State* st, uint32_t* ep_steps, uint32_t n, const uint8_t* actions, float* rewards,
+                                                  uint8_t* dones, float acos_thr, uint32_t* bad_action) {
+  const uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (e >= n) return;
   State s = st[e];
   uint32_t a = actions[e];
-  if (a >= kActions) { atomicOr(bad_action, 1u); a = 0; }
+  if (a >= kActions) {
+    if (lane == 0) atomicOr(bad_action, 1u);
+    a = 0;
+  }
   const uint32_t prev = s.score;
-  time_step(s, a, acos_thr);
+  time_step(s, a, acos_thr, lane);
   s.next_slot = (s.next_slot + 1) & 3;   // FrameRingBuffer::add advances; the frame goes to the old slot
-  st[e] = s;
-  rewards[e] = (float)(s.score - prev);
-  dones[e] = (uint8_t)s.finished;
-  ep_steps[e] += 1;
+  if (lane == 0) {
+    st[e] = s;
+    rewards[e] = (float)(s.score - prev);
+    dones[e] = (uint8_t)s.finished;
+    ep_steps[e] += 1;
+  }
 }
 
 __constant__ int8_t c_brick_col[kFrame];
@@ -469,7 +472,7 @@ namespace qlx {
 
 void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, uint8_t* d_dones) {
   const uint32_t n = env->n;
-  hipLaunchKernelGGL(k_env_step, dim3((n + 255) / 256), dim3(256), 0, env->stream, env->d_state, env->d_ep_steps, n,
+  hipLaunchKernelGGL(k_env_step, dim3((n + 3) / 4), dim3(256), 0, env->stream, env->d_state, env->d_ep_steps, n,
                      d_actions, d_rewards, d_dones, env->acos_thr, env->d_flags);
   if (env->hashing)
     hipLaunchKernelGGL(k_env_raster<true>, dim3(n), dim3(256), 0, env->stream, env->d_state, n, env->d_obs, env->d_hash);
