@@ -320,25 +320,22 @@ __device__ void time_step(State& s, uint32_t action, float acos_thr, int lane) {
 // ---------------------------------------------------------------------------------------
 // kernels
 
-__global__ void k_env_init(State* st, uint32_t* ep_steps, uint32_t n, uint64_t seed, uint32_t id_offset, const uint8_t* mask,
-                           int bump) {
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  if (mask && !mask[e]) return;
-  const uint32_t rc = bump ? st[e].reset_count + 1 : 0;
-  State s;
-  init_state(s, seed, id_offset + e, rc);
-  st[e] = s;
-  ep_steps[e] = 0;
-}
-
-// zero the 4 ring frames of envs selected by mask (FrameRingBuffer::new)
-__global__ void k_env_clear_frames(uint8_t* obs, uint32_t n, const uint8_t* mask) {
-  const uint32_t e = blockIdx.y;
+// Reset of the envs selected by mask (all if null), one block per env: new state (init_state) and the 4 ring
+// frames zeroed (FrameRingBuffer::new).  Unselected envs return at once.
+__global__ __launch_bounds__(256) void k_env_reset(State* st, uint32_t* ep_steps, uint8_t* obs, uint32_t n, uint64_t seed,
+                                                   uint32_t id_offset, const uint8_t* mask, int bump) {
+  const uint32_t e = blockIdx.x;
   if (e >= n || (mask && !mask[e])) return;
+  if (threadIdx.x == 0) {
+    const uint32_t rc = bump ? st[e].reset_count + 1 : 0;
+    State s;
+    init_state(s, seed, id_offset + e, rc);
+    st[e] = s;
+    ep_steps[e] = 0;
+  }
   uint4* dst = reinterpret_cast<uint4*>(obs + (size_t)e * kSlots * kFramePix);
   const uint4 z = {0, 0, 0, 0};
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < kSlots * kFramePix / 16; i += gridDim.x * blockDim.x) dst[i] = z;
+  for (uint32_t i = threadIdx.x; i < kSlots * kFramePix / 16; i += 256) dst[i] = z;
 }
 
 // one wave per env (4 envs per 256-thread block)
@@ -483,9 +480,8 @@ void env_launch_step(qlx_env* env, const uint8_t* d_actions, float* d_rewards, u
 
 void env_launch_reset(qlx_env* env, const uint8_t* d_mask, int bump) {
   const uint32_t n = env->n;
-  hipLaunchKernelGGL(k_env_init, dim3((n + 255) / 256), dim3(256), 0, env->stream, env->d_state, env->d_ep_steps, n,
-                     env->seed, env->id_offset, d_mask, bump);
-  hipLaunchKernelGGL(k_env_clear_frames, dim3(2, n), dim3(256), 0, env->stream, env->d_obs, n, d_mask);
+  hipLaunchKernelGGL(k_env_reset, dim3(n), dim3(256), 0, env->stream, env->d_state, env->d_ep_steps, env->d_obs, n, env->seed,
+                     env->id_offset, d_mask, bump);
   QLX_HIP(hipGetLastError());
 }
 

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_action_counts(const uint8_t* actions, u
 void action_counts(hipStream_t s, const uint8_t* d_actions, uint64_t len, uint32_t n_actions, std::vector<uint64_t>& out) {
   QLX_CHECK(n_actions >= 1 && n_actions < 256, QLX_E_INVALID, "bad action space");
   unsigned long long* d = nullptr;
-  QLX_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), (n_actions + 1) * sizeof(unsigned long long), s));
+  QLX_HIP(hipMalloc(reinterpret_cast<void**>(&d), (n_actions + 1) * sizeof(unsigned long long)));
   QLX_HIP(hipMemsetAsync(d, 0, (n_actions + 1) * sizeof(unsigned long long), s));
   if (len) {
     const uint64_t blocks = std::min<uint64_t>(1024, std::max<uint64_t>(1, (len / 16 + 255) / 256));
