@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -218,6 +219,9 @@ struct qlx_learner {
   uint32_t last_updates = 0;
   // data parallel
   ncclComm_t comm = nullptr;
+  hipStream_t comm_stream = nullptr;   // the communicator's collectives (bucketed gradient all-reduce)
+  bool dp_overlap = true;              // QLX_DP_OVERLAP=0: one whole-gradient all-reduce after the backward
+  hipEvent_t ev_dense = nullptr, ev_reduced = nullptr;
   int world = 1, rank = 0;
   qlx::Profiler prof;
 };
@@ -265,13 +269,40 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
   const uint8_t* bact = L->d_bact + (size_t)u_local * B;
   // online: forward, Huber, backward
   model_forward_trunk(on, tab_s, (int)B, s);
-  model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s,
-                 L->per ? L->prio.d_w + (size_t)u_local * B : nullptr, L->per ? L->prio.d_td + (size_t)u_local * B : nullptr);
+  const float* isw = L->per ? L->prio.d_w + (size_t)u_local * B : nullptr;
+  float* td = L->per ? L->prio.d_td + (size_t)u_local * B : nullptr;
   float scale = 1.0f;
-  if (L->comm) {
+  if (!L->comm) {
+    model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td);
+  } else if (!L->dp_overlap) {   // one all-reduce of the whole gradient on the learner stream
+    model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td);
     ProfScope ps(&L->prof, "allreduce", s);
     const ncclResult_t r = ncclAllReduce(on->d_grads, on->d_grads, (size_t)kNumParams, ncclFloat, ncclSum, L->comm, s);
     QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    scale = 1.0f / (float)L->world;
+  } else {
+    // Data parallel, two gradient buckets: the dense one (W3, b3, W4, b4: 6.42 of 6.74 MB) is all-reduced on the
+    // communicator stream as soon as the fc1 backward produced it, overlapping the conv backward; the conv bucket
+    // follows on the learner stream once the dense reduction is done (so the two collectives of the communicator
+    // never run at the same time and keep one order on every rank).  Adam then sees both.
+    model_backward_dense(on, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td);
+    QLX_HIP(hipEventRecord(L->ev_dense, s));
+    QLX_HIP(hipStreamWaitEvent(L->comm_stream, L->ev_dense, 0));
+    const int64_t off_dense = kVarOffsetDense;
+    {
+      ProfScope ps(&L->prof, "allreduce_dense", L->comm_stream);
+      const ncclResult_t r = ncclAllReduce(on->d_grads + off_dense, on->d_grads + off_dense, (size_t)(kNumParams - off_dense),
+                                           ncclFloat, ncclSum, L->comm, L->comm_stream);
+      QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    }
+    QLX_HIP(hipEventRecord(L->ev_reduced, L->comm_stream));
+    model_backward_conv(on, tab_s, (int)B, s);
+    QLX_HIP(hipStreamWaitEvent(s, L->ev_reduced, 0));
+    {
+      ProfScope ps(&L->prof, "allreduce_conv", s);
+      const ncclResult_t r = ncclAllReduce(on->d_grads, on->d_grads, (size_t)off_dense, ncclFloat, ncclSum, L->comm, s);
+      QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    }
     scale = 1.0f / (float)L->world;
   }
   model_norms(on, s, scale);
@@ -462,7 +493,11 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
     if (!L) return;
     (void)hipSetDevice(L->device);
     (void)hipStreamSynchronize(L->stream);
+    if (L->comm_stream) (void)hipStreamSynchronize(L->comm_stream);
     if (L->comm) (void)ncclCommDestroy(L->comm);
+    if (L->comm_stream) (void)hipStreamDestroy(L->comm_stream);
+    for (hipEvent_t e : {L->ev_dense, L->ev_reduced})
+      if (e) (void)hipEventDestroy(e);
     qlx_env_destroy(L->env);
     qlx_replay_destroy(L->rb);
     qlx_model_destroy(L->online);
@@ -627,12 +662,18 @@ int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const
   return guard([&] {
     QLX_CHECK(L && uid && world >= 1 && rank >= 0 && rank < world, QLX_E_INVALID, "bad argument");
     QLX_CHECK(rank == L->rank, QLX_E_INVALID, "rank differs from qlx_params.rank");
-    if (world == 1) return;
+    QLX_CHECK(!L->comm, QLX_E_STATE, "communicator already initialised");
+    // world == 1 builds a single-rank communicator: the data-parallel update path (bucketed all-reduce on its
+    // own stream) with identity reductions, for tests on one GPU
     QLX_HIP(hipSetDevice(L->device));
     ncclUniqueId id;
     std::memcpy(&id, uid, 128);
     const ncclResult_t r = ncclCommInitRank(&L->comm, world, id, rank);
     QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    QLX_HIP(hipStreamCreateWithFlags(&L->comm_stream, hipStreamNonBlocking));
+    const char* ov = std::getenv("QLX_DP_OVERLAP");
+    L->dp_overlap = !(ov && ov[0] == '0');
+    for (hipEvent_t* e : {&L->ev_dense, &L->ev_reduced}) QLX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     L->world = world;
     L->rank = rank;
   });

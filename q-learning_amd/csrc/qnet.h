@@ -10,6 +10,7 @@
 namespace qlx {
 
 constexpr int kNumVars = 10;
+constexpr int64_t kVarOffsetDense = 77984;   // flat offset of W3 (conv variables before it, dense ones after)
 constexpr int64_t kNumParams = 1685667;   // sum of the 10 Keras variables (variables.index shapes)
 constexpr int kFc1Split = 7;              // split-K of the 3136-deep dense layer (14 MFMA k-steps each)
 // conv weight-gradient partial slabs, one region per layer (conv3 and conv2 share a launch)
@@ -103,9 +104,14 @@ void model_pack(qlx_model* m);
 // store_acts = false skips writing a1/a2 (only a3 is needed when no backward pass follows)
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts = true);
 // Huber head + backward after model_forward_trunk: loss -> *loss_dev, raw gradients -> m->d_grads
-// weights (optional): per-sample loss weights; td_abs (optional): |q_a - y| per sample out
+// weights (optional): per-sample loss weights; td_abs (optional): |q_a - y| per sample out.
+// = model_backward_dense (head, fc1: the dense gradients, 95 % of the bytes, are final after it) followed by
+// model_backward_conv (the conv trunk); a data-parallel caller all-reduces the dense bucket in between
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
                     hipStream_t s, const float* weights = nullptr, float* td_abs = nullptr);
+void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
+                          const float* weights = nullptr, float* td_abs = nullptr);
+void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
 // per-variable norm partials for Adam: with scale == 1 (no all-reduce since the backward) the producers'
 // fused partials are used as they are; otherwise per-range sums of squares of the scaled gradients
 void model_norms(qlx_model* m, hipStream_t s, float scale);

@@ -33,6 +33,8 @@ static int64_t var_offset(int v) {
   return o;
 }
 
+static_assert(8 * 8 * 4 * 32 + 32 + 4 * 4 * 32 * 64 + 64 + 3 * 3 * 64 * 64 + 64 == kVarOffsetDense, "dense bucket offset");
+
 // fused clip_by_norm partial slots per variable: conv W/b from the slab reduction blocks (64 outputs each),
 // W3/b3 from the 25 x 4 fc1 wgrad tiles (each writes one W3 and one b3 slot), W4 from the 64 dW4 blocks
 constexpr int kFc1WgradTiles = 25 * 4;
@@ -600,6 +602,13 @@ Fc2Args fc2_args(qlx_model* m, int B) {
 // model_forward_trunk on the same batch; actions / y are device arrays [B]
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
                     hipStream_t s, const float* weights, float* td_abs) {
+  model_backward_dense(m, B, actions, y, loss_dev, s, weights, td_abs);
+  model_backward_conv(m, table, B, s);
+}
+
+// the head and dense part of the backward: Huber (+ dz4), dW4 / db4 / loss, dW3 / db3 and dz3
+void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
+                          const float* weights, float* td_abs) {
   ModelWs& w = m->w;
   float* G = m->d_grads;
   {  // head: q, Huber, dz4 (one wave per sample)
@@ -635,6 +644,14 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
                         Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136),
            k_fc1_bwd<Epi4StoreF32, Epi4ReluMask>);
   }
+  QLX_HIP(hipGetLastError());
+}
+
+// the conv part of the backward (after model_backward_dense on the same batch): dz3 -> dz2 -> dz1 and the
+// three conv weight gradients into m->d_grads
+void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+  ModelWs& w = m->w;
+  float* G = m->d_grads;
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
     ProfScope ps(m->prof, "trunk_bwd_data", s, 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512));

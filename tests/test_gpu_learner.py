@@ -137,3 +137,25 @@ def test_learner_runs_many_steps_without_faults():
     assert (L.environment.mechanics()["fault"] == 0).all()
     w = L.model.get(6)
     assert np.isfinite(w).all()
+
+
+def test_data_parallel_path_single_rank_bit_identical():
+    """The data-parallel update path (dense gradient bucket all-reduced on the communicator's stream while the conv
+    backward runs, then the conv bucket, Adam after both) on a single-rank RCCL communicator equals the plain
+    single-GPU path bit for bit: the stream hand-offs order every read and write."""
+    qlx = _qlx()
+    p = dict(n_envs=64, batch_size=64, history_buffer_len=4000, update_after_actions=16, epsilon_pure_random_steps=1000,
+             max_steps_per_episode=300)
+    plain = qlx.SelfDrivingQLearner(qlx.Parameter(**p))
+    dp = qlx.SelfDrivingQLearner(qlx.Parameter(**p))
+    dp.dist_init(1, 0, qlx.dist_unique_id())
+    for v in range(25):
+        plain.vector_step()
+        dp.vector_step()
+        a, b = plain.last(), dp.last()
+        assert np.array_equal(a["actions"], b["actions"]) and np.array_equal(a["indices"], b["indices"]), v
+        assert np.array_equal(a["losses"], b["losses"]), v
+    for var in range(10):
+        for which in range(3):
+            assert np.array_equal(plain.model.get(var, which), dp.model.get(var, which)), (var, which)
+    assert plain.stats()["update_count"] == dp.stats()["update_count"] > 50
