@@ -223,6 +223,8 @@ int32_t qlx_learner_dist_init(qlx_learner* l, int32_t world, int32_t rank, const
  * HBM-bound ones).  filter = one scope name records only that scope (NULL = all). */
 int32_t qlx_learner_profile(qlx_learner* l, int32_t enable);
 int32_t qlx_learner_profile_filter(qlx_learner* l, const char* name_or_null);
+/* filter + sampling: record every stride-th launch of that scope (dispatch-bound events, see profiler.h) */
+int32_t qlx_learner_profile_sample(qlx_learner* l, const char* name_or_null, uint32_t stride);
 int32_t qlx_learner_profile_get(qlx_learner* l, const char* name, double* total_us, double* total_work,
                                 uint64_t* launches);
 int32_t qlx_learner_profile_names(qlx_learner* l, char* buf, size_t cap);

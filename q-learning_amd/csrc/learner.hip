@@ -690,12 +690,16 @@ int32_t qlx_learner_profile(qlx_learner* L, int32_t enable) {
   });
 }
 
-int32_t qlx_learner_profile_filter(qlx_learner* L, const char* name) {
+int32_t qlx_learner_profile_filter(qlx_learner* L, const char* name) { return qlx_learner_profile_sample(L, name, 1); }
+
+int32_t qlx_learner_profile_sample(qlx_learner* L, const char* name, uint32_t stride) {
   return guard([&] {
-    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_CHECK(L && stride >= 1, QLX_E_INVALID, "bad argument");
     QLX_HIP(hipStreamSynchronize(L->stream));
     L->prof.collect();
     L->prof.filter = name ? name : "";
+    L->prof.stride = stride;
+    L->prof.seen = 0;
   });
 }
 

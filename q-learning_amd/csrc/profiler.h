@@ -16,6 +16,9 @@ struct Profiler {
   struct Rec { const char* name; hipEvent_t a, b; double work; };
   bool enabled = false;
   std::string filter;   // empty = record every scope
+  unsigned stride = 1;  // with a filter: record every stride-th launch of that scope (sampling keeps the event cost
+                        // of a timed region small)
+  unsigned long long seen = 0;
   std::vector<Rec> pending;
   std::vector<hipEvent_t> pool;
   std::map<std::string, Acc> acc;
@@ -29,7 +32,7 @@ struct Profiler {
   }
   void begin(const char* name, hipStream_t s, double work) {
     if (!enabled) return;
-    if (!filter.empty() && filter != name) { open.push_back({name, nullptr, nullptr, 0.0}); return; }
+    if (!filter.empty() && (filter != name || (seen++ % stride) != 0)) { open.push_back({name, nullptr, nullptr, 0.0}); return; }
     hipEvent_t a = take();
     (void)hipEventRecord(a, s);
     open.push_back({name, a, nullptr, work});
@@ -49,6 +52,7 @@ struct Profiler {
   void ext(const char* name, double work, hipEvent_t* a, hipEvent_t* b) {
     *a = *b = nullptr;
     if (!enabled || (!filter.empty() && filter != name)) return;
+    if (!filter.empty() && (seen++ % stride) != 0) return;
     *a = take();
     *b = take();
     pending.push_back({name, *a, *b, work});

@@ -147,6 +147,7 @@ def lib():
         "qlx_learner_profile": ([vp, i32], i32),
         "qlx_learner_profile_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)], i32),
         "qlx_learner_profile_filter": ([vp, C.c_char_p], i32),
+        "qlx_learner_profile_sample": ([vp, C.c_char_p, u32], i32),
         "qlx_learner_profile_names": ([vp, C.c_char_p, C.c_size_t], i32),
         # BallGame
         "qlx_bg_env_create": ([u32, u64, i32, C.POINTER(vp)], i32), "qlx_bg_env_destroy": ([vp], i32),
@@ -496,8 +497,9 @@ class SelfDrivingQLearner(_LearningStats):
     def profile(self, enable=True):
         _check(lib().qlx_learner_profile(self.h, 1 if enable else 0))
 
-    def profile_filter(self, name=None):
-        _check(lib().qlx_learner_profile_filter(self.h, None if name is None else name.encode()))
+    def profile_filter(self, name=None, stride=1):
+        """Record only scope `name` (None = all), every `stride`-th launch of it."""
+        _check(lib().qlx_learner_profile_sample(self.h, None if name is None else name.encode(), stride))
 
     def profile_get(self, name):
         """(total_us, total_work, launches) of a profiler scope since profile() was enabled."""
