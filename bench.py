@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--replay", type=int, default=100_000, help="replay capacity per GPU (config C2: 100k)")
     ap.add_argument("--cpu-sample", type=int, default=2000, help="env-steps of the CPU baseline sample, ~15 s (0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--double-dqn", action="store_true", help="extension (config C5): double-DQN targets")
+    ap.add_argument("--per", action="store_true", help="extension (config C5): proportional prioritized replay")
     return ap.parse_args()
 
 
@@ -116,7 +118,9 @@ def main():
     N, B = args.envs, args.batch
     assert B % args.replay_ratio == 0
     ua = B // args.replay_ratio
-    p = qlx.Parameter(n_envs=N, batch_size=B, update_after_actions=ua, history_buffer_len=args.replay, rank=ctl.rank)
+    flags = (qlx.DOUBLE_DQN if args.double_dqn else 0) | (qlx.PER if args.per else 0)
+    p = qlx.Parameter(n_envs=N, batch_size=B, update_after_actions=ua, history_buffer_len=args.replay, rank=ctl.rank,
+                      flags=flags)
     L = qlx.SelfDrivingQLearner(p, device=ctl.local)
     if ctl.world > 1:
         uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
@@ -180,9 +184,10 @@ def main():
         "dtype": "bf16",
         "data": "synthetic: frames rendered by the batched Breakout env kernel from live play; "
                 "random-init (GlorotUniform) Nature-DQN",
-        "config": {"workload": f"C2: {N} Breakout envs per GPU, replay {args.replay} in HBM, Nature-DQN "
+        "config": {"workload": f"{'C5' if flags else 'C2'}: {N} Breakout envs per GPU, replay {args.replay} in HBM, Nature-DQN "
                                f"(3 conv + 2 dense), B={B}, update every {ua} env-steps (replay ratio "
-                               f"{args.replay_ratio} samples/env-step), epsilon-greedy acting",
+                               f"{args.replay_ratio} samples/env-step), epsilon-greedy acting"
+                               + (" + double-DQN" if args.double_dqn else "") + (" + prioritized replay" if args.per else ""),
                    "envs_per_gpu": N, "batch": B, "replay_capacity": args.replay, "update_after_actions": ua,
                    "parallelism": f"dp{ctl.world}" if ctl.world > 1 else "single", "env_dtype": "fp32",
                    "qnet_dtype": "bf16 MFMA, fp32 accumulate + master weights"},
