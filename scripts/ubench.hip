@@ -292,6 +292,20 @@ int main(int argc, char** argv) {
     report(nm, time_us([&] { hipLaunchKernelGGL(k, dim3(g), dim3(256), GemmCfg::LDS, g_s, Pw, Pd); }), 2 * fl, "TF/s");  \
   }
     }
+    if (B == 1024) {   // fc1 backward pair: dW3 as one K pass (16 k-steps per tile) vs split-K 2 into a slab (8 + 8)
+      float* slab2 = nullptr;
+      QLX_HIP(hipMalloc(&slab2, (size_t)2 * 3137 * 512 * 4));
+      const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
+      const auto Pw1 = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1, Epi4StoreF32{G + var_offset(6), 512, nullptr}, 3136);
+      const auto Pw2 = gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 2, Epi4Slab{slab2, 512, (size_t)3137 * 512}, 3136);
+      auto k1 = k_gemm_pair_v<true, true, Epi4StoreF32, false, false, Epi4ReluMask, 2, 2, false>;
+      auto k2 = k_gemm_pair_v<true, true, Epi4Slab, false, false, Epi4ReluMask, 2, 2, false>;
+      set_lds_attr(k1, GemmCfg::LDS);
+      set_lds_attr(k2, GemmCfg::LDS);
+      report("pair dW3 split=1 (dW3 tiles first)", time_us([&] { hipLaunchKernelGGL(k1, dim3(Pw1.tiles() + Pd.tiles()), dim3(256), GemmCfg::LDS, g_s, Pw1, Pd); }), 2 * fl, "TF/s");
+      report("pair dW3 split=2 (dW3 tiles first)", time_us([&] { hipLaunchKernelGGL(k2, dim3(Pw2.tiles() + Pd.tiles()), dim3(256), GemmCfg::LDS, g_s, Pw2, Pd); }), 2 * fl, "TF/s");
+      QLX_HIP(hipFree(slab2));
+    }
     for (int splits : {1, 7}) {
       if (B == 8192 && splits == 7) continue;
       if (B == 1024 && splits == 1) continue;
