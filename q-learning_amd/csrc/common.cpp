@@ -3,6 +3,9 @@
 
 #include <string>
 
+#include <mutex>
+#include <set>
+#include <tuple>
 #include "qlx_internal.h"
 
 namespace qlx {
@@ -10,6 +13,16 @@ namespace qlx {
 static thread_local std::string g_last_error;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+void set_lds_limit(const void* kernel, size_t bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<int, const void*, size_t>> done;   // the attribute is set per device
+  int dev = 0;
+  QLX_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  if (!done.insert({dev, kernel, bytes}).second) return;
+  QLX_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
 
 int current_device_checked(int device) {
   int count = 0;

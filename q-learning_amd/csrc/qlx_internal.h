@@ -148,5 +148,7 @@ __host__ __device__ inline uint64_t uniform_usize_single(RngStream& s, uint64_t 
 constexpr uint64_t kH1 = 0x9E3779B97F4A7C15ull, kH2 = 0xC2B2AE3D27D4EB4Full, kH3 = 0x100000001B3ull;
 
 int current_device_checked(int device);
+// hipFuncAttributeMaxDynamicSharedMemorySize for `kernel` on the current device, once per (device, kernel, size)
+void set_lds_limit(const void* kernel, size_t bytes);
 
 }  // namespace qlx

@@ -519,7 +519,7 @@ static int trunk_grid(int B) { return std::max(1, std::min(B, 256)); }
 
 template <class Kern>
 static void set_lds_attr(Kern k, size_t bytes) {
-  QLX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  set_lds_limit((const void*)k, bytes);
 }
 
 template <class Epi>
@@ -535,11 +535,7 @@ static GemmProblem<Epi> gemm_problem(bool row_major_operand, const bf16* A, int 
 template <bool AK, bool BK, class Epi>
 static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K, int splits, Epi epi, hipStream_t s,
                         int ones_m = -1, bool remap = false) {
-  static bool attr = false;
-  if (!attr) {
-    set_lds_attr(k_gemm<AK, BK, Epi>, GemmCfg::LDS);
-    attr = true;
-  }
+  set_lds_attr(k_gemm<AK, BK, Epi>, GemmCfg::LDS);
   const GemmProblem<Epi> P = gemm_problem(!(AK && BK), A, lda, Bm, ldb, M, N, K, splits, epi, ones_m, false, remap);
   hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), dim3(xcd_grid(P.tiles())), dim3(256), GemmCfg::LDS, s, P);
 }
@@ -555,12 +551,8 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
     if (m->prof)
       m->prof->ext(store_acts ? "trunk_fwd" : "trunk_fwd_nostore", 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 64 * 576),
                    &ea, &eb);
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
-      set_lds_attr(k_trunk_fwd<false>, kTrunkFwdLds);
-      attr = true;
-    }
+    set_lds_attr(k_trunk_fwd<true>, kTrunkFwdLds);
+    set_lds_attr(k_trunk_fwd<false>, kTrunkFwdLds);
     auto kern = store_acts ? k_trunk_fwd<true> : k_trunk_fwd<false>;
     hipExtLaunchKernelGGL(kern, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkFwdLds, s, ea, eb, 0u, table, B, m->wf0, m->wf1,
                           m->wf2, p + var_offset(1), p + var_offset(3), p + var_offset(5), w.a1, w.a2, w.a3,
@@ -632,11 +624,7 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
                          m->d_sqf + sq_first(8), m->d_sqf + sq_first(9)};
     auto launch = [&](const auto& Pw, auto kern) {
       QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
-      static bool attr = false;   // one per instantiation
-      if (!attr) {
-        set_lds_attr(kern, GemmCfg::LDS);
-        attr = true;
-      }
+      set_lds_attr(kern, GemmCfg::LDS);
       fc1_bwd_map(m, Pw, Pd, kFc2WgradBlocks, s);
       hipLaunchKernelGGL(kern, dim3(m->fc1bwd_grid), dim3(256), GemmCfg::LDS, s, Pw, Pd, F, (const int*)m->d_fc1bwd_map);
     };
@@ -655,11 +643,7 @@ void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipSt
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
   {
     ProfScope ps(m->prof, "trunk_bwd_data", s, 2.0 * B * (49.0 * 64 * 576 + 81.0 * 64 * 512));
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(k_trunk_bwd_data<false>, kTrunkBwdLds);
-      attr = true;
-    }
+    set_lds_attr(k_trunk_bwd_data<false>, kTrunkBwdLds);
     hipLaunchKernelGGL(k_trunk_bwd_data<false>, dim3(trunk_grid(B)), dim3(kTrunkThreads), kTrunkBwdLds, s, w.dz3, w.a2, w.a1, B,
                        m->wb2, m->wb1, w.dz2, w.dz1, nullptr);
   }
@@ -682,22 +666,14 @@ void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipSt
     ProfScope ps(m->prof, "conv23_wgrad", s, 2.0 * B * (49.0 * 576 * 64 + 81.0 * 512 * 64));
     constexpr size_t lds = std::max(CW3::LDS, CW2::LDS);
     auto kern = k_conv23_wgrad;
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(kern, lds);
-      attr = true;
-    }
+    set_lds_attr(kern, lds);
     hipLaunchKernelGGL(kern, dim3(wgrad_blocks(3, used3) + wgrad_blocks(2, used2)), dim3(kTrunkThreads), lds, s, w.a2, w.dz3, per3, used3,
                        w.slab + kSlabConv3, w.a1, w.dz2, per2, used2, w.slab + kSlabConv2, B);
   }
   const int grid1 = trunk_grid(B);
   {  // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames
     ProfScope ps(m->prof, "conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
-      attr = true;
-    }
+    set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
     hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid1), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B,
                        w.slab + kSlabConv1);
   }

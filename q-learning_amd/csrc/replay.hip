@@ -154,11 +154,7 @@ void launch_sample_distinct(hipStream_t s, uint64_t seed, uint32_t first_update,
   const uint32_t l2 = table_log2(batch);
   QLX_CHECK(len < 0xFFFFFFFFull, QLX_E_INVALID, "replay sampling keys are 32-bit: len must be < 2^32 - 1");
   QLX_CHECK(len >= batch, QLX_E_INVALID, "cannot draw more distinct indices than the replay holds");
-  static bool attr = false;
-  if (!attr) {   // up to 128 KB of hash set at B = 4096
-    QLX_HIP(hipFuncSetAttribute((const void*)k_sample_distinct, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-    attr = true;
-  }
+  set_lds_limit((const void*)k_sample_distinct, 128 * 1024);   // up to 128 KB of hash set at B = 4096
   hipLaunchKernelGGL(k_sample_distinct, dim3(n_updates), dim3(kSampleThreads), (size_t)8 << l2, s, seed, first_update, rank, len,
                      batch, l2, d_out);
   QLX_HIP(hipGetLastError());
