@@ -660,21 +660,26 @@ int32_t qlx_bg_env_create(uint32_t n_envs, uint64_t seed, int32_t device, qlx_bg
     QLX_CHECK(n_envs > 0 && out, QLX_E_INVALID, "n_envs must be > 0");
     current_device_checked(device);
     auto* e = new qlx_bg_env;
-    e->device = device;
-    e->n = n_envs;
-    e->seed = seed;
-    QLX_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    QLX_HIP(hipMalloc(&e->d_state, (size_t)n_envs * sizeof(qlx_ballgame_state)));
-    QLX_HIP(hipMalloc(&e->d_ep_steps, (size_t)n_envs * 4));
-    QLX_HIP(hipMalloc(&e->d_bad, 4));
-    QLX_HIP(hipMalloc(&e->d_tmp_u8, n_envs));
-    QLX_HIP(hipMalloc(&e->d_tmp_u8b, n_envs));
-    QLX_HIP(hipMalloc(&e->d_tmp_f32, (size_t)n_envs * 4));
-    QLX_HIP(hipMemsetAsync(e->d_bad, 0, 4, e->stream));
-    hipLaunchKernelGGL(k_env_init, dim3((n_envs + 255) / 256), dim3(256), 0, e->stream, e->d_state, e->d_ep_steps, n_envs, seed,
-                       0u, (const uint8_t*)nullptr, 0);
-    QLX_HIP(hipGetLastError());
-    QLX_HIP(hipStreamSynchronize(e->stream));
+    try {   // a failure part-way releases what was built
+      e->device = device;
+      e->n = n_envs;
+      e->seed = seed;
+      QLX_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+      QLX_HIP(hipMalloc(&e->d_state, (size_t)n_envs * sizeof(qlx_ballgame_state)));
+      QLX_HIP(hipMalloc(&e->d_ep_steps, (size_t)n_envs * 4));
+      QLX_HIP(hipMalloc(&e->d_bad, 4));
+      QLX_HIP(hipMalloc(&e->d_tmp_u8, n_envs));
+      QLX_HIP(hipMalloc(&e->d_tmp_u8b, n_envs));
+      QLX_HIP(hipMalloc(&e->d_tmp_f32, (size_t)n_envs * 4));
+      QLX_HIP(hipMemsetAsync(e->d_bad, 0, 4, e->stream));
+      hipLaunchKernelGGL(k_env_init, dim3((n_envs + 255) / 256), dim3(256), 0, e->stream, e->d_state, e->d_ep_steps, n_envs, seed,
+                         0u, (const uint8_t*)nullptr, 0);
+      QLX_HIP(hipGetLastError());
+      QLX_HIP(hipStreamSynchronize(e->stream));
+    } catch (...) {
+      qlx_bg_env_destroy(e);
+      throw;
+    }
     *out = e;
   });
 }
@@ -767,20 +772,25 @@ int32_t qlx_bg_model_create(uint64_t seed, int32_t device, qlx_bg_model** out) {
     QLX_CHECK(out, QLX_E_INVALID, "null argument");
     current_device_checked(device);
     auto* m = new qlx_bg_model;
-    m->device = device;
-    QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
-    const size_t pb = kParams * 4;
-    QLX_HIP(hipMalloc(&m->d_params, pb));
-    QLX_HIP(hipMalloc(&m->d_m, pb));
-    QLX_HIP(hipMalloc(&m->d_v, pb));
-    QLX_HIP(hipMalloc(&m->d_grads, pb));
-    QLX_HIP(hipMalloc(&m->d_norms, kVars * 4));
-    std::vector<float> params;
-    glorot_host(params, seed);
-    QLX_HIP(hipMemcpy(m->d_params, params.data(), pb, hipMemcpyHostToDevice));
-    QLX_HIP(hipMemset(m->d_m, 0, pb));
-    QLX_HIP(hipMemset(m->d_v, 0, pb));
-    QLX_HIP(hipMemset(m->d_grads, 0, pb));
+    try {   // a failure part-way releases what was built
+      m->device = device;
+      QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+      const size_t pb = kParams * 4;
+      QLX_HIP(hipMalloc(&m->d_params, pb));
+      QLX_HIP(hipMalloc(&m->d_m, pb));
+      QLX_HIP(hipMalloc(&m->d_v, pb));
+      QLX_HIP(hipMalloc(&m->d_grads, pb));
+      QLX_HIP(hipMalloc(&m->d_norms, kVars * 4));
+      std::vector<float> params;
+      glorot_host(params, seed);
+      QLX_HIP(hipMemcpy(m->d_params, params.data(), pb, hipMemcpyHostToDevice));
+      QLX_HIP(hipMemset(m->d_m, 0, pb));
+      QLX_HIP(hipMemset(m->d_v, 0, pb));
+      QLX_HIP(hipMemset(m->d_grads, 0, pb));
+    } catch (...) {
+      qlx_bg_model_destroy(m);
+      throw;
+    }
     *out = m;
   });
 }
@@ -903,68 +913,73 @@ int32_t qlx_bg_learner_create(const qlx_params* p, int32_t device, qlx_bg_learne
               QLX_E_INVALID, "prioritized replay needs alpha >= 0, beta >= 0, eps > 0");
     current_device_checked(device);
     auto* L = new qlx_bg_learner;
-    L->ddqn = (p->flags & QLX_LEARNER_DOUBLE_DQN) != 0;
-    L->per = (p->flags & QLX_LEARNER_PER) != 0;
-    L->p = *p;
-    L->device = device;
-    L->N = p->n_envs;
-    L->B = p->batch_size;
-    L->cap = p->history_buffer_len;
-    QLX_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
-    int32_t st = qlx_bg_env_create(L->N, p->env_seed, device, &L->env);
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    st = qlx_bg_model_create(p->init_seed, device, &L->online);
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    st = qlx_bg_model_create(p->init_seed, device, &L->target);   // same initial weights (:107-108)
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    L->env->stream = L->stream; L->env->own_stream = false;
-    L->online->stream = L->stream; L->online->own_stream = false;
-    L->target->stream = L->stream; L->target->own_stream = false;
-    if (p->rank != 0) {   // data-parallel ranks own env ids rank * N + e
-      L->env->id_offset = p->rank * L->N;
-      hipLaunchKernelGGL(k_env_init, dim3((L->N + 255) / 256), dim3(256), 0, L->stream, L->env->d_state, L->env->d_ep_steps, L->N,
-                         L->env->seed, L->env->id_offset, (const uint8_t*)nullptr, 0);
+    try {   // a failure part-way releases what was built
+      L->ddqn = (p->flags & QLX_LEARNER_DOUBLE_DQN) != 0;
+      L->per = (p->flags & QLX_LEARNER_PER) != 0;
+      L->p = *p;
+      L->device = device;
+      L->N = p->n_envs;
+      L->B = p->batch_size;
+      L->cap = p->history_buffer_len;
+      QLX_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+      int32_t st = qlx_bg_env_create(L->N, p->env_seed, device, &L->env);
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      st = qlx_bg_model_create(p->init_seed, device, &L->online);
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      st = qlx_bg_model_create(p->init_seed, device, &L->target);   // same initial weights (:107-108)
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      L->env->stream = L->stream; L->env->own_stream = false;
+      L->online->stream = L->stream; L->online->own_stream = false;
+      L->target->stream = L->stream; L->target->own_stream = false;
+      if (p->rank != 0) {   // data-parallel ranks own env ids rank * N + e
+        L->env->id_offset = p->rank * L->N;
+        hipLaunchKernelGGL(k_env_init, dim3((L->N + 255) / 256), dim3(256), 0, L->stream, L->env->d_state, L->env->d_ep_steps, L->N,
+                           L->env->seed, L->env->id_offset, (const uint8_t*)nullptr, 0);
+      }
+      const std::vector<double> eps = epsilon_table(*p);
+      L->eps_len = eps.size();
+      QLX_HIP(hipMalloc(&L->d_eps, eps.size() * 8));
+      QLX_HIP(hipMemcpy(L->d_eps, eps.data(), eps.size() * 8, hipMemcpyHostToDevice));
+      const uint32_t N = L->N, B = L->B;
+      L->max_updates = (uint32_t)(N / p->update_after_actions + 2);
+      const size_t UB = (size_t)L->max_updates * B;
+      QLX_HIP(hipMalloc(&L->d_rs, L->cap * sizeof(qlx_ballgame_state)));
+      QLX_HIP(hipMalloc(&L->d_rsn, L->cap * sizeof(qlx_ballgame_state)));
+      QLX_HIP(hipMalloc(&L->d_ra, L->cap));
+      QLX_HIP(hipMalloc(&L->d_rd, L->cap));
+      QLX_HIP(hipMalloc(&L->d_rr, L->cap * 4));
+      QLX_HIP(hipMalloc(&L->d_obs, (size_t)N * kObs));
+      QLX_HIP(hipMalloc(&L->d_actions, N));
+      QLX_HIP(hipMalloc(&L->d_dones, N));
+      QLX_HIP(hipMalloc(&L->d_reset, N));
+      QLX_HIP(hipMalloc(&L->d_rewards, (size_t)N * 4));
+      QLX_HIP(hipMalloc(&L->d_q, (size_t)N * kA * 4));
+      QLX_HIP(hipMalloc(&L->d_ep_reward, (size_t)N * 4));
+      QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * 4));
+      QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
+      QLX_HIP(hipMalloc(&L->d_idx, UB * 8));
+      QLX_HIP(hipMalloc(&L->d_xs, UB * kObs));
+      QLX_HIP(hipMalloc(&L->d_xn, UB * kObs));
+      QLX_HIP(hipMalloc(&L->d_bact, UB));
+      QLX_HIP(hipMalloc(&L->d_bdone, UB));
+      QLX_HIP(hipMalloc(&L->d_brew, UB * 4));
+      QLX_HIP(hipMalloc(&L->d_targets, UB * 4));
+      QLX_HIP(hipMalloc(&L->d_losses, L->max_updates * 4));
+      QLX_HIP(hipMemsetAsync(L->d_ep_reward, 0, (size_t)N * 4, L->stream));
+      QLX_HIP(hipMemsetAsync(L->d_book, 0, sizeof(Book), L->stream));
+      QLX_HIP(hipMemsetAsync(L->d_q, 0, (size_t)N * kA * 4, L->stream));
+      model_workspace(L->online, (int)std::max(N, B));
+      model_workspace(L->target, (int)UB);
+      if (L->ddqn) {
+        model_workspace(L->online, (int)UB);
+        QLX_HIP(hipMalloc(&L->d_qsel, UB * kA * 4));
+      }
+      if (L->per) L->prio.init(L->cap, UB);
+      QLX_HIP(hipStreamSynchronize(L->stream));
+    } catch (...) {
+      qlx_bg_learner_destroy(L);
+      throw;
     }
-    const std::vector<double> eps = epsilon_table(*p);
-    L->eps_len = eps.size();
-    QLX_HIP(hipMalloc(&L->d_eps, eps.size() * 8));
-    QLX_HIP(hipMemcpy(L->d_eps, eps.data(), eps.size() * 8, hipMemcpyHostToDevice));
-    const uint32_t N = L->N, B = L->B;
-    L->max_updates = (uint32_t)(N / p->update_after_actions + 2);
-    const size_t UB = (size_t)L->max_updates * B;
-    QLX_HIP(hipMalloc(&L->d_rs, L->cap * sizeof(qlx_ballgame_state)));
-    QLX_HIP(hipMalloc(&L->d_rsn, L->cap * sizeof(qlx_ballgame_state)));
-    QLX_HIP(hipMalloc(&L->d_ra, L->cap));
-    QLX_HIP(hipMalloc(&L->d_rd, L->cap));
-    QLX_HIP(hipMalloc(&L->d_rr, L->cap * 4));
-    QLX_HIP(hipMalloc(&L->d_obs, (size_t)N * kObs));
-    QLX_HIP(hipMalloc(&L->d_actions, N));
-    QLX_HIP(hipMalloc(&L->d_dones, N));
-    QLX_HIP(hipMalloc(&L->d_reset, N));
-    QLX_HIP(hipMalloc(&L->d_rewards, (size_t)N * 4));
-    QLX_HIP(hipMalloc(&L->d_q, (size_t)N * kA * 4));
-    QLX_HIP(hipMalloc(&L->d_ep_reward, (size_t)N * 4));
-    QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * 4));
-    QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
-    QLX_HIP(hipMalloc(&L->d_idx, UB * 8));
-    QLX_HIP(hipMalloc(&L->d_xs, UB * kObs));
-    QLX_HIP(hipMalloc(&L->d_xn, UB * kObs));
-    QLX_HIP(hipMalloc(&L->d_bact, UB));
-    QLX_HIP(hipMalloc(&L->d_bdone, UB));
-    QLX_HIP(hipMalloc(&L->d_brew, UB * 4));
-    QLX_HIP(hipMalloc(&L->d_targets, UB * 4));
-    QLX_HIP(hipMalloc(&L->d_losses, L->max_updates * 4));
-    QLX_HIP(hipMemsetAsync(L->d_ep_reward, 0, (size_t)N * 4, L->stream));
-    QLX_HIP(hipMemsetAsync(L->d_book, 0, sizeof(Book), L->stream));
-    QLX_HIP(hipMemsetAsync(L->d_q, 0, (size_t)N * kA * 4, L->stream));
-    model_workspace(L->online, (int)std::max(N, B));
-    model_workspace(L->target, (int)UB);
-    if (L->ddqn) {
-      model_workspace(L->online, (int)UB);
-      QLX_HIP(hipMalloc(&L->d_qsel, UB * kA * 4));
-    }
-    if (L->per) L->prio.init(L->cap, UB);
-    QLX_HIP(hipStreamSynchronize(L->stream));
     *out = L;
   });
 }

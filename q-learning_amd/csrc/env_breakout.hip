@@ -502,27 +502,32 @@ int32_t qlx_env_create(int32_t kind, uint32_t n_envs, uint64_t seed, int32_t dev
     QLX_CHECK(n_envs > 0 && out, QLX_E_INVALID, "n_envs must be > 0");
     current_device_checked(device);
     auto* e = new qlx_env;
-    e->device = device;
-    e->n = n_envs;
-    e->seed = seed;
-    e->acos_thr = acos_threshold_host();
-    QLX_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    QLX_HIP(hipMalloc(&e->d_state, sizeof(State) * n_envs));
-    QLX_HIP(hipMalloc(&e->d_obs, (size_t)n_envs * kSlots * kFramePix));
-    QLX_HIP(hipMalloc(&e->d_hash, sizeof(uint64_t) * n_envs));
-    QLX_HIP(hipMalloc(&e->d_ep_steps, sizeof(uint32_t) * n_envs));
-    QLX_HIP(hipMalloc(&e->d_flags, 16));
-    QLX_HIP(hipMalloc(&e->d_tmp_u8, n_envs));
-    QLX_HIP(hipMalloc(&e->d_tmp_u8b, n_envs));
-    QLX_HIP(hipMalloc(&e->d_tmp_f32, sizeof(float) * n_envs));
-    QLX_HIP(hipMemsetAsync(e->d_hash, 0, sizeof(uint64_t) * n_envs, e->stream));
-    QLX_HIP(hipMemsetAsync(e->d_flags, 0, 16, e->stream));
-    int8_t col[kFrame], row[kFrame];
-    brick_luts(col, row);
-    QLX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_brick_col), col, sizeof(col)));
-    QLX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_brick_row), row, sizeof(row)));
-    env_launch_reset(e, nullptr, 0);
-    QLX_HIP(hipStreamSynchronize(e->stream));
+    try {   // a failure part-way releases what was built
+      e->device = device;
+      e->n = n_envs;
+      e->seed = seed;
+      e->acos_thr = acos_threshold_host();
+      QLX_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+      QLX_HIP(hipMalloc(&e->d_state, sizeof(State) * n_envs));
+      QLX_HIP(hipMalloc(&e->d_obs, (size_t)n_envs * kSlots * kFramePix));
+      QLX_HIP(hipMalloc(&e->d_hash, sizeof(uint64_t) * n_envs));
+      QLX_HIP(hipMalloc(&e->d_ep_steps, sizeof(uint32_t) * n_envs));
+      QLX_HIP(hipMalloc(&e->d_flags, 16));
+      QLX_HIP(hipMalloc(&e->d_tmp_u8, n_envs));
+      QLX_HIP(hipMalloc(&e->d_tmp_u8b, n_envs));
+      QLX_HIP(hipMalloc(&e->d_tmp_f32, sizeof(float) * n_envs));
+      QLX_HIP(hipMemsetAsync(e->d_hash, 0, sizeof(uint64_t) * n_envs, e->stream));
+      QLX_HIP(hipMemsetAsync(e->d_flags, 0, 16, e->stream));
+      int8_t col[kFrame], row[kFrame];
+      brick_luts(col, row);
+      QLX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_brick_col), col, sizeof(col)));
+      QLX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_brick_row), row, sizeof(row)));
+      env_launch_reset(e, nullptr, 0);
+      QLX_HIP(hipStreamSynchronize(e->stream));
+    } catch (...) {
+      qlx_env_destroy(e);
+      throw;
+    }
     *out = e;
   });
 }

@@ -420,70 +420,75 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
               QLX_E_INVALID, "prioritized replay needs alpha >= 0, beta >= 0, eps > 0");
     current_device_checked(device);
     auto* L = new qlx_learner;
-    L->ddqn = (p->flags & QLX_LEARNER_DOUBLE_DQN) != 0;
-    L->per = (p->flags & QLX_LEARNER_PER) != 0;
-    L->p = *p;
-    L->device = device;
-    L->N = p->n_envs;
-    L->B = p->batch_size;
-    L->rank = (int)p->rank;
-    QLX_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
-    int32_t st;
-    st = qlx_env_create(QLX_ENV_BREAKOUT, L->N, p->env_seed, device, &L->env);
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    st = qlx_replay_create(p->history_buffer_len, L->N, device, &L->rb);
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->online);
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->target);   // same initial weights
-    QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-    // everything runs on the learner's stream
-    L->env->stream = L->stream; L->env->own_stream = false;
-    L->rb->stream = L->stream; L->rb->own_stream = false;
-    L->online->stream = L->stream; L->online->own_stream = false;
-    L->target->stream = L->stream; L->target->own_stream = false;
-    L->env->hashing = false;
-    // re-seat env ids for data-parallel ranks (ball launch streams are per global env id)
-    if (p->rank != 0) {
-      L->env->id_offset = p->rank * L->N;
-      env_launch_reset(L->env, nullptr, 0);
+    try {   // a failure part-way releases what was built
+      L->ddqn = (p->flags & QLX_LEARNER_DOUBLE_DQN) != 0;
+      L->per = (p->flags & QLX_LEARNER_PER) != 0;
+      L->p = *p;
+      L->device = device;
+      L->N = p->n_envs;
+      L->B = p->batch_size;
+      L->rank = (int)p->rank;
+      QLX_HIP(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+      int32_t st;
+      st = qlx_env_create(QLX_ENV_BREAKOUT, L->N, p->env_seed, device, &L->env);
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      st = qlx_replay_create(p->history_buffer_len, L->N, device, &L->rb);
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->online);
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->target);   // same initial weights
+      QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      // everything runs on the learner's stream
+      L->env->stream = L->stream; L->env->own_stream = false;
+      L->rb->stream = L->stream; L->rb->own_stream = false;
+      L->online->stream = L->stream; L->online->own_stream = false;
+      L->target->stream = L->stream; L->target->own_stream = false;
+      L->env->hashing = false;
+      // re-seat env ids for data-parallel ranks (ball launch streams are per global env id)
+      if (p->rank != 0) {
+        L->env->id_offset = p->rank * L->N;
+        env_launch_reset(L->env, nullptr, 0);
+      }
+      // epsilon table: eps_k after k decrements, k = 0.. until epsilon_min (repeated f64 subtraction)
+      const std::vector<double> eps = epsilon_table(*p);
+      L->eps_len = eps.size();
+      QLX_HIP(hipMalloc(&L->d_eps, eps.size() * sizeof(double)));
+      QLX_HIP(hipMemcpy(L->d_eps, eps.data(), eps.size() * sizeof(double), hipMemcpyHostToDevice));
+      const uint32_t N = L->N, B = L->B;
+      L->max_updates = (uint32_t)(N / p->update_after_actions + 2);
+      QLX_HIP(hipMalloc(&L->d_actions, N));
+      QLX_HIP(hipMalloc(&L->d_rewards, N * sizeof(float)));
+      QLX_HIP(hipMalloc(&L->d_dones, N));
+      QLX_HIP(hipMalloc(&L->d_reset, N));
+      QLX_HIP(hipMalloc(&L->d_obs_table, N * 4 * sizeof(void*)));
+      QLX_HIP(hipMalloc(&L->d_ep_reward, N * sizeof(float)));
+      QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * sizeof(float)));
+      QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
+      QLX_HIP(hipMalloc(&L->d_idx, (size_t)L->max_updates * B * sizeof(uint64_t)));
+      const size_t UB = (size_t)L->max_updates * B;   // all batches of one vector step
+      QLX_HIP(hipMalloc(&L->d_tab_s, UB * 4 * sizeof(void*)));
+      QLX_HIP(hipMalloc(&L->d_tab_sn, UB * 4 * sizeof(void*)));
+      QLX_HIP(hipMalloc(&L->d_bact, UB));
+      QLX_HIP(hipMalloc(&L->d_brew, UB * sizeof(float)));
+      QLX_HIP(hipMalloc(&L->d_bdone, UB));
+      QLX_HIP(hipMalloc(&L->d_losses, L->max_updates * sizeof(float)));
+      QLX_HIP(hipMalloc(&L->d_targets, (size_t)L->max_updates * B * sizeof(float)));
+      QLX_HIP(hipMemsetAsync(L->d_ep_reward, 0, N * sizeof(float), L->stream));
+      QLX_HIP(hipMemsetAsync(L->d_book, 0, sizeof(Book), L->stream));
+      QLX_HIP(hipMemsetAsync(L->d_actions, 0, N, L->stream));
+      QLX_HIP(hipMemsetAsync(L->d_rewards, 0, N * sizeof(float), L->stream));
+      QLX_HIP(hipMemsetAsync(L->d_dones, 0, N, L->stream));
+      hipLaunchKernelGGL(k_obs_table, dim3((N * 4 + 255) / 256), dim3(256), 0, L->stream, L->env->d_obs, N, L->d_obs_table);
+      QLX_HIP(hipGetLastError());
+      model_workspace(L->online, (int)std::max(N, B));
+      model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
+      if (L->ddqn) model_workspace(L->online, (int)(L->max_updates * B));   // + the online pass over s'
+      if (L->per) L->prio.init(p->history_buffer_len, UB);
+      QLX_HIP(hipStreamSynchronize(L->stream));
+    } catch (...) {
+      qlx_learner_destroy(L);
+      throw;
     }
-    // epsilon table: eps_k after k decrements, k = 0.. until epsilon_min (repeated f64 subtraction)
-    const std::vector<double> eps = epsilon_table(*p);
-    L->eps_len = eps.size();
-    QLX_HIP(hipMalloc(&L->d_eps, eps.size() * sizeof(double)));
-    QLX_HIP(hipMemcpy(L->d_eps, eps.data(), eps.size() * sizeof(double), hipMemcpyHostToDevice));
-    const uint32_t N = L->N, B = L->B;
-    L->max_updates = (uint32_t)(N / p->update_after_actions + 2);
-    QLX_HIP(hipMalloc(&L->d_actions, N));
-    QLX_HIP(hipMalloc(&L->d_rewards, N * sizeof(float)));
-    QLX_HIP(hipMalloc(&L->d_dones, N));
-    QLX_HIP(hipMalloc(&L->d_reset, N));
-    QLX_HIP(hipMalloc(&L->d_obs_table, N * 4 * sizeof(void*)));
-    QLX_HIP(hipMalloc(&L->d_ep_reward, N * sizeof(float)));
-    QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * sizeof(float)));
-    QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
-    QLX_HIP(hipMalloc(&L->d_idx, (size_t)L->max_updates * B * sizeof(uint64_t)));
-    const size_t UB = (size_t)L->max_updates * B;   // all batches of one vector step
-    QLX_HIP(hipMalloc(&L->d_tab_s, UB * 4 * sizeof(void*)));
-    QLX_HIP(hipMalloc(&L->d_tab_sn, UB * 4 * sizeof(void*)));
-    QLX_HIP(hipMalloc(&L->d_bact, UB));
-    QLX_HIP(hipMalloc(&L->d_brew, UB * sizeof(float)));
-    QLX_HIP(hipMalloc(&L->d_bdone, UB));
-    QLX_HIP(hipMalloc(&L->d_losses, L->max_updates * sizeof(float)));
-    QLX_HIP(hipMalloc(&L->d_targets, (size_t)L->max_updates * B * sizeof(float)));
-    QLX_HIP(hipMemsetAsync(L->d_ep_reward, 0, N * sizeof(float), L->stream));
-    QLX_HIP(hipMemsetAsync(L->d_book, 0, sizeof(Book), L->stream));
-    QLX_HIP(hipMemsetAsync(L->d_actions, 0, N, L->stream));
-    QLX_HIP(hipMemsetAsync(L->d_rewards, 0, N * sizeof(float), L->stream));
-    QLX_HIP(hipMemsetAsync(L->d_dones, 0, N, L->stream));
-    hipLaunchKernelGGL(k_obs_table, dim3((N * 4 + 255) / 256), dim3(256), 0, L->stream, L->env->d_obs, N, L->d_obs_table);
-    QLX_HIP(hipGetLastError());
-    model_workspace(L->online, (int)std::max(N, B));
-    model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
-    if (L->ddqn) model_workspace(L->online, (int)(L->max_updates * B));   // + the online pass over s'
-    if (L->per) L->prio.init(p->history_buffer_len, UB);
-    QLX_HIP(hipStreamSynchronize(L->stream));
     *out = L;
   });
 }

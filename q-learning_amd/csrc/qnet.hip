@@ -769,57 +769,62 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     QLX_CHECK(arch == QLX_ARCH_NATURE_DQN && out, QLX_E_INVALID, "unknown model arch");
     current_device_checked(device);
     auto* m = new qlx_model;
-    m->device = device;
-    QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
-    const size_t pb = kNumParams * sizeof(float);
-    QLX_HIP(hipMalloc(&m->d_params, pb));
-    QLX_HIP(hipMalloc(&m->d_m, pb));
-    QLX_HIP(hipMalloc(&m->d_v, pb));
-    QLX_HIP(hipMalloc(&m->d_grads, pb));
-    QLX_HIP(hipMalloc(&m->wf0, 32 * 256 * 2));
-    QLX_HIP(hipMalloc(&m->wf1, 64 * 512 * 2));
-    QLX_HIP(hipMalloc(&m->wb1, 32 * 1024 * 2));
-    QLX_HIP(hipMalloc(&m->wf2, 64 * 576 * 2));
-    QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
-    QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
-    // norm ranges: chunks of <= 2048 elements (~830 blocks) that never cross a variable
-    std::vector<int64_t> rb, re;
-    std::vector<int> vf(kNumVars + 1, 0);
-    int64_t off = 0;
-    for (int v = 0; v < kNumVars; ++v) {
-      vf[v] = (int)rb.size();
-      for (int64_t i = 0; i < kVarSize[v]; i += 2048) {
-        rb.push_back(off + i);
-        re.push_back(off + std::min<int64_t>(kVarSize[v], i + 2048));
+    try {   // a failure part-way releases what was built
+      m->device = device;
+      QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+      const size_t pb = kNumParams * sizeof(float);
+      QLX_HIP(hipMalloc(&m->d_params, pb));
+      QLX_HIP(hipMalloc(&m->d_m, pb));
+      QLX_HIP(hipMalloc(&m->d_v, pb));
+      QLX_HIP(hipMalloc(&m->d_grads, pb));
+      QLX_HIP(hipMalloc(&m->wf0, 32 * 256 * 2));
+      QLX_HIP(hipMalloc(&m->wf1, 64 * 512 * 2));
+      QLX_HIP(hipMalloc(&m->wb1, 32 * 1024 * 2));
+      QLX_HIP(hipMalloc(&m->wf2, 64 * 576 * 2));
+      QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
+      QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
+      // norm ranges: chunks of <= 2048 elements (~830 blocks) that never cross a variable
+      std::vector<int64_t> rb, re;
+      std::vector<int> vf(kNumVars + 1, 0);
+      int64_t off = 0;
+      for (int v = 0; v < kNumVars; ++v) {
+        vf[v] = (int)rb.size();
+        for (int64_t i = 0; i < kVarSize[v]; i += 2048) {
+          rb.push_back(off + i);
+          re.push_back(off + std::min<int64_t>(kVarSize[v], i + 2048));
+        }
+        off += kVarSize[v];
       }
-      off += kVarSize[v];
+      vf[kNumVars] = (int)rb.size();
+      for (int v = 0; v < kNumVars; ++v)
+        QLX_CHECK(vf[v + 1] - vf[v] <= kAdamMaxPartials && kSqSlots[v] <= kAdamMaxPartials, QLX_E_STATE, "k_adam partial bound");
+      m->n_ranges = (int)rb.size();
+      QLX_HIP(hipMalloc(&m->d_rbeg, rb.size() * 8));
+      QLX_HIP(hipMalloc(&m->d_rend, re.size() * 8));
+      QLX_HIP(hipMalloc(&m->d_partial, rb.size() * 4));
+      QLX_HIP(hipMalloc(&m->d_var_first, vf.size() * 4));
+      QLX_HIP(hipMalloc(&m->d_norms, 64));
+      std::vector<int> sf(kNumVars + 1);
+      for (int v = 0; v <= kNumVars; ++v) sf[v] = v < kNumVars ? sq_first(v) : sq_first(kNumVars - 1) + kSqSlots[kNumVars - 1];
+      QLX_HIP(hipMalloc(&m->d_sqf, sf[kNumVars] * 4));
+      QLX_HIP(hipMalloc(&m->d_sqf_first, sf.size() * 4));
+      QLX_HIP(hipMemcpy(m->d_sqf_first, sf.data(), sf.size() * 4, hipMemcpyHostToDevice));
+      QLX_HIP(hipMemset(m->d_sqf, 0, sf[kNumVars] * 4));
+      QLX_HIP(hipMemcpy(m->d_rbeg, rb.data(), rb.size() * 8, hipMemcpyHostToDevice));
+      QLX_HIP(hipMemcpy(m->d_rend, re.data(), re.size() * 8, hipMemcpyHostToDevice));
+      QLX_HIP(hipMemcpy(m->d_var_first, vf.data(), vf.size() * 4, hipMemcpyHostToDevice));
+      std::vector<float> params;
+      glorot_host(params, seed);
+      QLX_HIP(hipMemcpy(m->d_params, params.data(), pb, hipMemcpyHostToDevice));
+      QLX_HIP(hipMemset(m->d_m, 0, pb));
+      QLX_HIP(hipMemset(m->d_v, 0, pb));
+      QLX_HIP(hipMemset(m->d_grads, 0, pb));
+      model_pack(m);
+      QLX_HIP(hipStreamSynchronize(m->stream));
+    } catch (...) {
+      qlx_model_destroy(m);
+      throw;
     }
-    vf[kNumVars] = (int)rb.size();
-    for (int v = 0; v < kNumVars; ++v)
-      QLX_CHECK(vf[v + 1] - vf[v] <= kAdamMaxPartials && kSqSlots[v] <= kAdamMaxPartials, QLX_E_STATE, "k_adam partial bound");
-    m->n_ranges = (int)rb.size();
-    QLX_HIP(hipMalloc(&m->d_rbeg, rb.size() * 8));
-    QLX_HIP(hipMalloc(&m->d_rend, re.size() * 8));
-    QLX_HIP(hipMalloc(&m->d_partial, rb.size() * 4));
-    QLX_HIP(hipMalloc(&m->d_var_first, vf.size() * 4));
-    QLX_HIP(hipMalloc(&m->d_norms, 64));
-    std::vector<int> sf(kNumVars + 1);
-    for (int v = 0; v <= kNumVars; ++v) sf[v] = v < kNumVars ? sq_first(v) : sq_first(kNumVars - 1) + kSqSlots[kNumVars - 1];
-    QLX_HIP(hipMalloc(&m->d_sqf, sf[kNumVars] * 4));
-    QLX_HIP(hipMalloc(&m->d_sqf_first, sf.size() * 4));
-    QLX_HIP(hipMemcpy(m->d_sqf_first, sf.data(), sf.size() * 4, hipMemcpyHostToDevice));
-    QLX_HIP(hipMemset(m->d_sqf, 0, sf[kNumVars] * 4));
-    QLX_HIP(hipMemcpy(m->d_rbeg, rb.data(), rb.size() * 8, hipMemcpyHostToDevice));
-    QLX_HIP(hipMemcpy(m->d_rend, re.data(), re.size() * 8, hipMemcpyHostToDevice));
-    QLX_HIP(hipMemcpy(m->d_var_first, vf.data(), vf.size() * 4, hipMemcpyHostToDevice));
-    std::vector<float> params;
-    glorot_host(params, seed);
-    QLX_HIP(hipMemcpy(m->d_params, params.data(), pb, hipMemcpyHostToDevice));
-    QLX_HIP(hipMemset(m->d_m, 0, pb));
-    QLX_HIP(hipMemset(m->d_v, 0, pb));
-    QLX_HIP(hipMemset(m->d_grads, 0, pb));
-    model_pack(m);
-    QLX_HIP(hipStreamSynchronize(m->stream));
     *out = m;
   });
 }

@@ -176,17 +176,22 @@ int32_t qlx_replay_create(uint64_t capacity, uint32_t n_envs, int32_t device, ql
     QLX_CHECK(capacity > 0 && n_envs > 0 && out, QLX_E_INVALID, "capacity and n_envs must be > 0");
     current_device_checked(device);
     auto* r = new qlx_replay;
-    r->device = device;
-    r->cap = capacity;
-    r->n = n_envs;
-    r->F = capacity + 4ull * n_envs;
-    QLX_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-    const hipError_t e = hipMalloc(&r->d_frames, r->F * kFramePix);
-    if (e != hipSuccess) { delete r; throw Error{QLX_E_OOM, "replay frame store allocation failed"}; }
-    QLX_HIP(hipMalloc(&r->d_action, capacity));
-    QLX_HIP(hipMalloc(&r->d_reward, capacity * sizeof(float)));
-    QLX_HIP(hipMalloc(&r->d_done, capacity));
-    QLX_HIP(hipMalloc(&r->d_epstep, capacity * sizeof(uint32_t)));
+    try {   // a failure part-way releases what was built
+      r->device = device;
+      r->cap = capacity;
+      r->n = n_envs;
+      r->F = capacity + 4ull * n_envs;
+      QLX_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+      const hipError_t e = hipMalloc(&r->d_frames, r->F * kFramePix);
+      if (e != hipSuccess) { delete r; throw Error{QLX_E_OOM, "replay frame store allocation failed"}; }
+      QLX_HIP(hipMalloc(&r->d_action, capacity));
+      QLX_HIP(hipMalloc(&r->d_reward, capacity * sizeof(float)));
+      QLX_HIP(hipMalloc(&r->d_done, capacity));
+      QLX_HIP(hipMalloc(&r->d_epstep, capacity * sizeof(uint32_t)));
+    } catch (...) {
+      qlx_replay_destroy(r);
+      throw;
+    }
     *out = r;
   });
 }
