@@ -159,3 +159,24 @@ def test_data_parallel_path_single_rank_bit_identical():
         for which in range(3):
             assert np.array_equal(plain.model.get(var, which), dp.model.get(var, which)), (var, which)
     assert plain.stats()["update_count"] == dp.stats()["update_count"] > 50
+
+
+def test_invalid_parameters_fail_loudly():
+    """Bad parameters are rejected with the library's message (QlError), like the reference's Result errors; the
+    create path releases whatever it built before failing (repeated failures do not accumulate device memory)."""
+    qlx = _qlx()
+    bad = [dict(n_envs=0), dict(batch_size=0), dict(update_after_actions=0), dict(history_buffer_len=8, batch_size=32),
+           dict(episode_reward_history_buffer_len=0), dict(flags=8), dict(flags=qlx.PER, per_eps=0.0)]
+    for kw in bad:
+        p = dict(n_envs=16, batch_size=32, history_buffer_len=1000)
+        p.update(kw)
+        for cls in (qlx.SelfDrivingQLearner, qlx.BallGameLearner):
+            with pytest.raises(qlx.QlError):
+                cls(qlx.Parameter(**p))
+    import torch
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(20):   # fails after env, replay and both models were built
+        with pytest.raises(qlx.QlError):
+            qlx.SelfDrivingQLearner(qlx.Parameter(n_envs=16, batch_size=32, history_buffer_len=1000, flags=qlx.PER,
+                                                  per_eps=-1.0))
+    assert torch.cuda.mem_get_info()[0] >= free0 - (64 << 20)
