@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libqlx.so")
+LIB_PATH = os.environ.get("QLX_LIB_PATH") or os.path.join(_HERE, "lib", "libqlx.so")   # override: A/B builds
 
 ACTION_SPACE = 3           # BreakoutAction::ACTION_SPACE
 FRAME = 84
