@@ -42,22 +42,24 @@ def _batch(rank, B):
 def _worker(rank, world, port, B, out_path):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    ctl = bench.Control()                     # bench.py's control plane: gloo process group from the env
+    assert ctl.world == world and ctl.rank == rank and dist.is_initialized()
     net = O.QNet(seed=21)
     x, a, y = _batch(rank, B)
     _, grads, _ = net.train(x, a, y)          # local gradients (train also applies Adam locally; unused)
     flat = torch.from_numpy(np.concatenate([g.ravel() for g in grads]).astype(np.float64))
     dist.all_reduce(flat)                     # RCCL sum in the product
     mean = (flat / world).numpy()
-    # control plane used by bench.py
-    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    obj = [bytes(range(128)) if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    dist.barrier()
+    # control plane used by bench.py: max over ranks of the timed interval, unique-id broadcast, barrier
+    tmax = ctl.max(float(rank + 1))
+    uid = ctl.bcast_bytes(bytes(range(128)) if rank == 0 else bytes(128))
+    ctl.barrier()
     if rank == 0:
-        np.savez(out_path, mean=mean, tmax=t.item(), uid=np.frombuffer(obj[0], np.uint8))
+        np.savez(out_path, mean=mean, tmax=tmax, uid=np.frombuffer(uid, np.uint8))
     dist.destroy_process_group()
 
 
