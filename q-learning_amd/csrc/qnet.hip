@@ -624,9 +624,13 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
                          m->d_sqf + sq_first(8), m->d_sqf + sq_first(9)};
     auto launch = [&](const auto& Pw, auto kern) {
       QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
-      set_lds_attr(kern, GemmCfg::LDS);
       fc1_bwd_map(m, Pw, Pd, kFc2WgradBlocks, s);
-      hipLaunchKernelGGL(kern, dim3(m->fc1bwd_grid), dim3(256), GemmCfg::LDS, s, Pw, Pd, F, (const int*)m->d_fc1bwd_map);
+      // one block per CU (LDS request above half the CU's 160 KB): a 16-k-step dW3 tile sharing its CU with a
+      // second block lost more than the co-resident block gained (measured 28.3 -> 27.2 us per launch)
+      constexpr size_t lds_req = GemmCfg::LDS + 2048;
+      static_assert(2 * lds_req > 160 * 1024, "k_fc1_bwd: one block per CU");
+      set_lds_attr(kern, lds_req);
+      hipLaunchKernelGGL(kern, dim3(m->fc1bwd_grid), dim3(256), lds_req, s, Pw, Pd, F, (const int*)m->d_fc1bwd_map);
     };
     launch(gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1,
                         Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136),
