@@ -132,7 +132,10 @@ def pmc_traffic(scope):
     written by scripts/pmc.sh + scripts/pmc_traffic.py on the same build), or None."""
     import glob
     key = SCOPE_KERNEL.get(scope)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    import re
+    # natural order of the round / version directories (r01_v10 after r01_v9)
+    nat = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), key=nat)
     if not key or not files:
         return None, None
     data = json.load(open(files[-1]))["kernels"]
