@@ -66,6 +66,9 @@ struct qlx_model {
   int last_batch = 0;
   qlx::ModelWs w;
   qlx::Profiler* prof = nullptr;   // set by the learner while profiling
+  // conv1 weight gradient as channel-half blocks (k_conv1_wgrad_h); QLX_CONV1_HALVES=0 at create time selects the
+  // one-block-per-chunk k_conv1_wgrad (bit-identical gradients)
+  bool conv1_halves = true;
 };
 
 namespace qlx {

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -677,9 +678,15 @@ void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipSt
   const int grid1 = trunk_grid(B);
   {  // conv1: dW0 = im2col_s2d(x)^T dz1 per sample from the LDS-staged frames
     ProfScope ps(m->prof, "conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
-    set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
-    hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid1), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B,
-                       w.slab + kSlabConv1);
+    if (m->conv1_halves) {   // two channel-half blocks per sample chunk, two blocks per CU
+      set_lds_attr(k_conv1_wgrad_h, kConv1WgradHLds);
+      hipLaunchKernelGGL(k_conv1_wgrad_h, dim3(2 * grid1), dim3(kTrunkThreads), kConv1WgradHLds, s, table, w.dz1, B, grid1,
+                         w.slab + kSlabConv1);
+    } else {
+      set_lds_attr(k_conv1_wgrad, kConv1WgradLds);
+      hipLaunchKernelGGL(k_conv1_wgrad, dim3(grid1), dim3(kTrunkThreads), kConv1WgradLds, s, table, w.dz1, B,
+                         w.slab + kSlabConv1);
+    }
   }
   {
     ProfScope ps(m->prof, "wgrad_reduce", s);
@@ -773,6 +780,8 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     QLX_CHECK(arch == QLX_ARCH_NATURE_DQN && out, QLX_E_INVALID, "unknown model arch");
     current_device_checked(device);
     auto* m = new qlx_model;
+    const char* ch = std::getenv("QLX_CONV1_HALVES");
+    m->conv1_halves = !(ch && ch[0] == '0');
     try {   // a failure part-way releases what was built
       m->device = device;
       QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));

@@ -436,6 +436,121 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv1_wgrad(const uint8_t*
   }
 }
 
+// Channel-half variant of k_conv1_wgrad (the shipped one): block i = sample chunk i % G1 x half hh = i / G1 of the
+// 64 s2d channels (ring slots 2hh, 2hh + 1).  The half image X [441][kXHS] + DZ fit two blocks per CU, so two
+// per-sample chains interleave on every CU (the one-block kernel is latency-bound); each block stages half the
+// frames and all of dz1.  Wave w owns tap ij = w >> 1 and k tile a = w & 1 (16 channels) x both n tiles.  Every
+// dW element sees the same MFMA operands in the same order as in k_conv1_wgrad (bit-identical slab rows);
+// half 0 also sums the bias partial.
+constexpr int kXHS = 40;
+constexpr size_t kConv1WgradHLds = (size_t)(441 * kXHS + kLdsDZ) * 2;
+static_assert(2 * (kConv1WgradHLds + 16 * 32 * 4 + 64) <= 160 * 1024, "k_conv1_wgrad_h: two blocks per CU");
+__global__ __launch_bounds__(kTrunkThreads, 2) void k_conv1_wgrad_h(const uint8_t* const* __restrict__ table,
+                                                                    const bf16* __restrict__ dz1, int B, int G1,
+                                                                    float* slab) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* X = lds;
+  bf16* DZ = lds + 441 * kXHS;
+  __shared__ float bred[16][32];
+  __shared__ const uint8_t* sptr[2];
+  const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int chunk = (int)blockIdx.x % G1, hh = (int)blockIdx.x / G1;
+  const int ij = wave >> 1, ti = ij >> 1, tj = ij & 1, ka = wave & 1;
+  const int col0 = ka * 16 + 4 * p;
+  for (int i = tid; i < 16 * kDZS / 8; i += kTrunkThreads)
+    *reinterpret_cast<uint4*>(DZ + 400 * kDZS + i * 8) = uint4{0, 0, 0, 0};
+  f32x4 acc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+  float bsum = 0.0f;
+  const int bn = tid & 31, brg = tid >> 5;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  auto tr = [](const bf16* pp) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pp)); };
+  uint4 pf[2], dv[4];
+  auto dz_prefetch = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      dv[u] = uint4{0, 0, 0, 0};
+      if (b < B && c < 1600)
+        dv[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(dz1 + (size_t)b * 12800 + c * 8));
+    }
+  };
+  // this half's two frames (pointers from LDS, wave-uniform), thread pos < 441 owns s2d block pos
+  auto frames_prefetch = [&](bool valid) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      pf[u] = uint4{0, 0, 0, 0};
+      const unsigned long long fv = (unsigned long long)sptr[u];
+      const uint8_t* f = (const uint8_t*)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(fv >> 32)) << 32) |
+                                          (unsigned)__builtin_amdgcn_readfirstlane((int)fv));
+      if (valid && f && tid < 441) pf[u] = __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4*)(f + tid * 16));
+    }
+  };
+  const uint8_t* pnext = nullptr;
+  if (tid < 2) sptr[tid] = chunk < B ? table[chunk * 4 + 2 * hh + tid] : nullptr;
+  if (tid < 2 && chunk + G1 < B) pnext = table[(chunk + G1) * 4 + 2 * hh + tid];
+  lds_barrier();
+  frames_prefetch(chunk < B);
+  dz_prefetch(chunk);
+  for (int b = chunk; b < B; b += G1) {
+    lds_barrier();   // previous sample's readers are done
+    if (tid < 441) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        uint4 lo, hi;
+        u8x16_to_bf16(pf[u], lo, hi);
+        uint4* d = reinterpret_cast<uint4*>(X + tid * kXHS + u * 16);
+        d[0] = lo;
+        d[1] = hi;
+      }
+    }
+    if (tid < 2) sptr[tid] = pnext;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * kTrunkThreads;
+      if (c < 1600) *reinterpret_cast<uint4*>(DZ + (c >> 2) * kDZS + (c & 3) * 8) = dv[u];
+    }
+    lds_barrier();
+    frames_prefetch(b + G1 < B);
+    if (tid < 2 && b + 2 * G1 < B) pnext = table[(b + 2 * G1) * 4 + 2 * hh + tid];
+    dz_prefetch(b + G1);
+    for (int ms = 0; ms < 13; ++ms) {
+      const int m0 = ms * 32;
+      int mA = min(m0 + 4 * g + q, 399), mB = min(m0 + 16 + 4 * g + q, 399);
+      const int oxA = mA / 20, oyA = mA - oxA * 20, oxB = mB / 20, oyB = mB - oxB * 20;
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x4 x0 = tr(X + ((oxA + ti) * 21 + oyA + tj) * kXHS + col0);
+      const s16x4 x1 = tr(X + ((oxB + ti) * 21 + oyB + tj) * kXHS + col0);
+      const bf16x8 af = __builtin_bit_cast(bf16x8, (s16x8){x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]});
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const s16x4 v0 = tr(DZ + (m0 + 4 * g + q) * kDZS + c * 16 + 4 * p);
+        const s16x4 v1 = tr(DZ + (m0 + 16 + 4 * g + q) * kDZS + c * 16 + 4 * p);
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, (s16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[c], 0, 0, 0);
+      }
+    }
+    if (hh == 0)
+      for (int m = brg; m < 400; m += 16) bsum += (float)DZ[m * kDZS + bn];
+  }
+  // D tile (ka, c): row k = ij * 64 + hh * 32 + ka * 16 + 4g + e, col n = c * 16 + li (k_conv1_wgrad's rows)
+  float* out = slab + (size_t)chunk * kConv1SlabStride;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[(ij * 64 + hh * 32 + ka * 16 + 4 * g + e) * 32 + c * 16 + li] = acc[c][e];
+  if (hh == 0) {
+    bred[brg][bn] = bsum;
+    lds_barrier();
+    if (tid < 32) {
+      float t = 0.0f;
+      for (int i = 0; i < 16; ++i) t += bred[i][tid];
+      out[8192 + tid] = t;
+    }
+  }
+}
+
 // Backward data through conv3 and conv2, fused per sample:
 //   dz2 = convT(dz3, W2) * (a2 > 0)        M = 81 rows (ih, iw), N = 64, K = 576 = (kh*3+kw)*64 + oc
 //   dz1 = convT(dz2, W1) * (a1 > 0)        by output parity class p = (ih & 1, iw & 1): rows (i, j) of

@@ -195,3 +195,27 @@ def test_large_batch_forward_paths_agree():
     srt = np.sort(q_chunks, axis=1)
     sure = srt[:, -1] - srt[:, -2] > 2e-2 * top
     assert np.array_equal(a_big[sure], np.argmax(q_chunks, axis=1)[sure])
+
+
+@pytest.mark.parametrize("B", [32, 300, 1024])
+def test_conv1_wgrad_halves_bit_identical(B):
+    """conv1's weight gradient as channel-half blocks (default, k_conv1_wgrad_h) equals the one-block-per-chunk
+    kernel (QLX_CONV1_HALVES=0) bit for bit: every dW element sees the same MFMA operands in the same order."""
+    x = np.concatenate([env_states(B // 2), rand_states(B - B // 2, 11)])
+    rng = np.random.default_rng(B + 1)
+    a = rng.integers(0, 3, B).astype(np.uint8)
+    y = rng.normal(0, 2.0, B).astype(np.float32)
+    out = []
+    for halves in ("1", "0"):
+        os.environ["QLX_CONV1_HALVES"] = halves
+        try:
+            m = _qlx().DeepQLearningModel(seed=3)
+        finally:
+            os.environ.pop("QLX_CONV1_HALVES", None)
+        loss, grads, _ = m.train(x, a, y, want_grads=True)
+        out.append((loss, grads, [m.get(v) for v in range(10)]))
+    (l1, g1, w1), (l0, g0, w0) = out
+    assert l1 == l0
+    for v in range(10):
+        assert np.array_equal(g1[v], g0[v]), f"gradient of var {v} differs"
+        assert np.array_equal(w1[v], w0[v]), f"weights of var {v} differ after Adam"
