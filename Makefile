@@ -14,7 +14,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 STRICT := -ffp-contract=off
 LDFLAGS := -shared -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 
-OBJS := $(OUT)/obj/common.o $(OUT)/obj/env_breakout.o $(OUT)/obj/replay.o $(OUT)/obj/qnet.o $(OUT)/obj/learner.o \
+OBJS := $(OUT)/obj/common.o $(OUT)/obj/env_breakout.o $(OUT)/obj/replay.o $(OUT)/obj/qnet.o $(OUT)/obj/qnet32.o $(OUT)/obj/learner.o \
         $(OUT)/obj/ballgame.o $(OUT)/obj/tf_bundle.o $(OUT)/obj/per.o $(OUT)/obj/stats.o
 
 HDRS := include/qlx.h $(wildcard $(SRC)/*.h)
@@ -37,6 +37,10 @@ $(OUT)/obj/replay.o: $(SRC)/replay.hip $(HDRS) | $(OUT)/obj
 
 $(OUT)/obj/qnet.o: $(SRC)/qnet.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# fp32 Q-net: bit-exact against the oracle, so no contraction anywhere (every fma is an explicit fmaf / MFMA)
+$(OUT)/obj/qnet32.o: $(SRC)/qnet32.hip $(HDRS) | $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
 
 $(OUT)/obj/learner.o: $(SRC)/learner.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@

@@ -46,7 +46,15 @@ extern "C" {
 
 #define QLX_ENV_BREAKOUT 1
 #define QLX_ENV_BALLGAME 2
-#define QLX_ARCH_NATURE_DQN 1 /* Conv(32,8,s4)-Conv(64,4,s2)-Conv(64,3,s1)-Dense512-Dense3 */
+/* Conv(32,8,s4)-Conv(64,4,s2)-Conv(64,3,s1)-Dense512-Dense3 in fp32: the reference's arithmetic, every reduction a
+ * single fmaf chain in the order DESIGN.md §6 defines (bit-exact against the CPU oracle) */
+#define QLX_ARCH_NATURE_DQN 1
+/* the same net with bf16 MFMA operands, fp32 accumulation and fp32 master weights (the labelled fast path) */
+#define QLX_ARCH_NATURE_DQN_BF16 2
+/* fp32 weight gradients of the conv layers: per-chunk fmaf chains over this many samples, chunks summed in order */
+#define QLX_F32_WGRAD_CHUNK_CONV1 4
+#define QLX_F32_WGRAD_CHUNK_CONV2 16
+#define QLX_F32_WGRAD_CHUNK_CONV3 16
 
 const char* qlx_last_error(void);
 int32_t qlx_version(void);
@@ -114,8 +122,9 @@ int32_t qlx_replay_get_many(qlx_replay* rb, const uint64_t* indices, uint32_t ba
 
 typedef struct qlx_model qlx_model;
 
-/* Nature-DQN with GlorotUniform weights from stream (seed, var, 0) and zero biases; fp32 master
- * weights + Adam slots in HBM, bf16 MFMA copies. lr 2.5e-4, beta 0.9/0.999, eps 1e-7, clipnorm 1. */
+/* Nature-DQN (arch QLX_ARCH_NATURE_DQN = fp32, QLX_ARCH_NATURE_DQN_BF16 = bf16 MFMA operands) with GlorotUniform
+ * weights from stream (seed, var, 0) and zero biases; fp32 master weights + Adam slots in HBM.  lr 2.5e-4, beta
+ * 0.9/0.999, eps 1e-7, clipnorm 1. */
 int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out);
 int32_t qlx_model_destroy(qlx_model* m);
 int32_t qlx_model_num_vars(void);
@@ -169,8 +178,13 @@ typedef struct qlx_params { /* Parameter (self_driving_tf_q_learner.rs:20-67) + 
   float per_alpha;    /* prioritized replay: P(i) ~ p_i^alpha, p_i = |td_i| + per_eps */
   float per_beta;     /* importance-sampling exponent, w_i = (len P(i))^-beta / max_batch w */
   float per_eps;
-  uint32_t pad2;
+  uint32_t qnet_precision;     /* QLX_PREC_F32 (0, the reference's arithmetic) or QLX_PREC_BF16 */
+  uint64_t stats_after_steps;  /* every this many env-steps: checkpoint + learning_update_log (0 = never) */
+  char checkpoint_file[256];   /* write_checkpoint target of those events and of solved() (empty = not written) */
 } qlx_params;
+
+#define QLX_PREC_F32 0u
+#define QLX_PREC_BF16 1u
 
 /* qlx_params.flags */
 #define QLX_LEARNER_DOUBLE_DQN 1u  /* y = r + gamma Q_target(s', argmax_a Q_online(s')) (van Hasselt et al. 2016) */
@@ -192,6 +206,16 @@ int32_t qlx_learner_destroy(qlx_learner* l);
 /* One vector step (n_envs env-steps + the updates they trigger), enqueued asynchronously. */
 int32_t qlx_learner_vector_step(qlx_learner* l);
 int32_t qlx_learner_run(qlx_learner* l, uint64_t n_vector_steps);
+/* Vector steps without updates (act, env step, replay push, episode books; epsilon and step_count advance): fills the
+ * replay before a measurement or a parity check at a given replay occupancy.  Not in the reference loop. */
+int32_t qlx_learner_prefill(qlx_learner* l, uint64_t n_vector_steps);
+/* learn_till_mastered (self_driving_tf_q_learner.rs:127-132): vector steps until solved() or max_vector_steps. */
+int32_t qlx_learner_learn_till_mastered(qlx_learner* l, uint64_t max_vector_steps, uint64_t* steps_run);
+/* Statistics events so far (write_checkpoint + learning_update_log every stats_after_steps env-steps and on solved,
+ * :204-212,226-230); the last event's log text; a callback receiving each log text (the reference's log::info!). */
+uint64_t qlx_learner_stats_events(const qlx_learner* l);
+int32_t qlx_learner_last_log(qlx_learner* l, char* buf, size_t cap, size_t* len);
+int32_t qlx_learner_set_log_callback(qlx_learner* l, void (*cb)(const char* text, void* user), void* user);
 int32_t qlx_learner_sync(qlx_learner* l);
 int32_t qlx_learner_stats_get(qlx_learner* l, qlx_learner_stats* out);
 /* Outputs of the last vector step (host copies; synchronises): actions/rewards/dones [n_envs],

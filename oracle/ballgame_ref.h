@@ -94,7 +94,9 @@ struct BgParams {   // field layout = qlx_params (include/qlx.h)
   uint32_t rank;
   uint32_t flags;      // bit 0 double DQN, bit 1 prioritized replay (qlx.h QLX_LEARNER_*)
   float per_alpha, per_beta, per_eps;
-  uint32_t pad2;
+  uint32_t qnet_precision;     // 0 fp32 (qnet32_ref.cpp, bit-exact definition), 1 bf16 product (double-accumulating oracle)
+  uint64_t stats_after_steps;  // learning_update_log + write_checkpoint every this many env-steps (0 = never)
+  char checkpoint_file[256];
 };
 
 struct BgTransition { uint8_t action; BgState s, s_next; float reward; bool done; };

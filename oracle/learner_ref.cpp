@@ -40,6 +40,13 @@ void per_sample(const SumTree& st, uint64_t seed, uint32_t update_idx, uint32_t 
   for (int b = 0; b < B; ++b) weights[b] = weights[b] / wmax;
 }
 
+// the Q-net arithmetic of the product under test: fp32 fmaf chains (qnet32_ref.cpp, bit-exact definition) or the
+// double-accumulating restatement the bf16 product is held to within stated tolerances (qnet_ref.cpp)
+void Learner::fwd(const QNet& q, const uint8_t* x, int B, Acts& a) const {
+  if (p.qnet_precision == 0) qnet32_forward(q, x, B, a);
+  else qnet_forward(q, x, B, a);
+}
+
 static StateRef snapshot(const Env& e) {   // Environment::state_as_rc / step_as_rc (prelude.rs:36,52-58)
   auto s = std::make_shared<std::vector<uint8_t>>(kStateBytes);
   env_state_tensor(e, s->data());
@@ -60,7 +67,7 @@ Learner::Learner(const LearnerParams& prm) : p(prm), replay(prm.history_buffer_l
   epsilon = p.epsilon_max;
 }
 
-void Learner::vector_step() {
+void Learner::vector_step(bool train) {
   const uint32_t N = p.n_envs;
   last_actions.assign(N, 0);
   last_rewards.assign(N, 0.0f);
@@ -78,7 +85,7 @@ void Learner::vector_step() {
     std::vector<uint8_t> x((size_t)N * kStateBytes);
     for (uint32_t e = 0; e < N; ++e) std::memcpy(&x[(size_t)e * kStateBytes], state[e]->data(), kStateBytes);
     Acts a;
-    qnet_forward(online, x.data(), (int)N, a);
+    fwd(online, x.data(), (int)N, a);
     last_q = a.q;
   }
   const double interval = p.epsilon_max - p.epsilon_min;
@@ -100,6 +107,7 @@ void Learner::vector_step() {
     last_actions[e] = a;
   }
   // ---- env step + replay (learn_episode :169-178, :214-230) ----
+  bool episode_ended = false;
   for (uint32_t e = 0; e < N; ++e) {
     float r; bool done;
     env_step(envs[e], last_actions[e], &r, &done);
@@ -121,6 +129,7 @@ void Learner::vector_step() {
         running_reward = s / (float)episode_rewards.size();
       }
       episode_count += 1;
+      episode_ended = true;
       env_reset(envs[e]);
       state[e] = snapshot(envs[e]);
       ep_reward[e] = 0.0f;
@@ -129,7 +138,7 @@ void Learner::vector_step() {
   }
   // ---- training updates (:181-202) ----
   const uint64_t triggers = step_count / p.update_after_actions - step_before / p.update_after_actions;
-  if (replay.len() > p.batch_size && triggers > 0) {
+  if (train && replay.len() > p.batch_size && triggers > 0) {
     // every batch of the vector step is drawn from the replay (and priorities) as they stand after the pushes
     const int B = (int)p.batch_size;
     const uint64_t len = replay.len();
@@ -151,6 +160,11 @@ void Learner::vector_step() {
   }
   if (p.target_sync_steps > 0 && step_count / p.target_sync_steps != step_before / p.target_sync_steps)
     qnet_copy_weights(target, online);
+  // statistics events (:204-212, :226-230): write_checkpoint + learning_update_log once per vector step that crossed a
+  // multiple of stats_after_steps, and once more when an episode ended and the task is solved
+  const uint64_t S = p.stats_after_steps;
+  if (S > 0 && step_count / S != step_before / S) stats_events += 1;
+  if (episode_ended && solved()) stats_events += 1;
   vec_steps += 1;
 }
 
@@ -162,9 +176,9 @@ void Learner::targets(const uint64_t* idx, float* y) const {
   std::vector<uint8_t> xn((size_t)B * kStateBytes);
   for (int b = 0; b < B; ++b) std::memcpy(&xn[(size_t)b * kStateBytes], replay.buf[idx[b]].s_next->data(), kStateBytes);
   Acts at;
-  qnet_forward(target, xn.data(), B, at);   // batch_predict_max_future_reward
+  fwd(target, xn.data(), B, at);   // batch_predict_max_future_reward
   Acts an;
-  if (p.flags & 1u) qnet_forward(online, xn.data(), B, an);   // double DQN: the online net picks a*
+  if (p.flags & 1u) fwd(online, xn.data(), B, an);   // double DQN: the online net picks a*
   for (int b = 0; b < B; ++b) {
     const Transition& t = replay.buf[idx[b]];
     float v;
@@ -188,11 +202,17 @@ void Learner::update(const uint64_t* idx, const float* isw, const float* y) {
     act[b] = t.action;
   }
   Acts ao;
-  qnet_forward(online, xs.data(), B, ao);
+  fwd(online, xs.data(), B, ao);
   Grads g;
   std::vector<float> td(B);
-  const float loss = qnet_loss_backward(online, xs.data(), act.data(), y, B, ao, g, isw, td.data());
-  qnet_apply_adam(online, g, nullptr);
+  float loss;
+  if (p.qnet_precision == 0) {
+    loss = qnet32_loss_backward(online, xs.data(), act.data(), y, B, ao, g, isw, td.data());
+    qnet32_apply_adam(online, g, nullptr);
+  } else {
+    loss = qnet_loss_backward(online, xs.data(), act.data(), y, B, ao, g, isw, td.data());
+    qnet_apply_adam(online, g, nullptr);
+  }
   if (p.flags & 2u) {   // new priorities (|td| + eps)^alpha, in batch order (a repeated slot keeps its last value)
     const uint64_t start = (total_pushed - replay.len()) % p.history_buffer_len;
     for (int b = 0; b < B; ++b) {

@@ -49,7 +49,9 @@ struct LearnerParams {   // layout mirrored by tests/oracle.py (ctypes)
   uint32_t rank;
   uint32_t flags;      // bit 0 double DQN, bit 1 prioritized replay (qlx.h QLX_LEARNER_*)
   float per_alpha, per_beta, per_eps;
-  uint32_t pad2;
+  uint32_t qnet_precision;     // 0 fp32 (qnet32_ref.cpp, bit-exact definition), 1 bf16 product (double-accumulating oracle)
+  uint64_t stats_after_steps;  // learning_update_log + write_checkpoint every this many env-steps (0 = never)
+  char checkpoint_file[256];
 };
 
 using StateRef = std::shared_ptr<std::vector<uint8_t>>;   // Rc<BreakoutState> tensor view [x][y][slot]
@@ -126,8 +128,12 @@ struct Learner {
   std::vector<float> last_targets;      // [n_updates][B] y
   std::vector<float> last_weights;      // [n_updates][B] IS weights (1 without prioritized replay)
 
+  uint64_t stats_events = 0;            // write_checkpoint + learning_update_log events so far
+
   explicit Learner(const LearnerParams& prm);
-  void vector_step();
+  // train = false: act, step, push and keep the books only (replay prefill: no updates, no update_count)
+  void vector_step(bool train = true);
+  void fwd(const QNet& q, const uint8_t* x, int B, Acts& a) const;
   void targets(const uint64_t* idx, float* y) const;
   // logical indices of the batch, IS weights (or null), Bellman targets
   void update(const uint64_t* idx, const float* isw, const float* y);

@@ -191,10 +191,37 @@ float orc_qnet_train(void* h, const uint8_t* x, const uint8_t* actions, const fl
   return loss;
 }
 
+// the fp32 arithmetic of QLX_ARCH_NATURE_DQN (qnet32_ref.cpp)
+void orc_qnet32_forward(void* h, const uint8_t* x, int B, float* q, float* a1, float* a2, float* a3, float* a4) {
+  Acts a;
+  qnet32_forward(*(QNet*)h, x, B, a);
+  std::memcpy(q, a.q.data(), a.q.size() * 4);
+  if (a1) std::memcpy(a1, a.a1.data(), a.a1.size() * 4);
+  if (a2) std::memcpy(a2, a.a2.data(), a.a2.size() * 4);
+  if (a3) std::memcpy(a3, a.a3.data(), a.a3.size() * 4);
+  if (a4) std::memcpy(a4, a.a4.data(), a.a4.size() * 4);
+}
+float orc_qnet32_train(void* h, const uint8_t* x, const uint8_t* actions, const float* y, int B, float* grads_out,
+                       float* norms_out) {
+  QNet* q = (QNet*)h;
+  Acts a;
+  qnet32_forward(*q, x, B, a);
+  Grads g;
+  const float loss = qnet32_loss_backward(*q, x, actions, y, B, a, g);
+  if (grads_out) {
+    size_t off = 0;
+    for (int v = 0; v < kNumVars; ++v) { std::memcpy(grads_out + off, g.g[v].data(), kVarSize[v] * 4); off += kVarSize[v]; }
+  }
+  qnet32_apply_adam(*q, g, norms_out);
+  return loss;
+}
+
 // ---------------- learner ----------------
 void* orc_learner_new(const LearnerParams* p) { return new Learner(*p); }
 void orc_learner_free(void* h) { delete (Learner*)h; }
 void orc_learner_vector_step(void* h) { ((Learner*)h)->vector_step(); }
+void orc_learner_prefill(void* h, uint64_t n) { for (uint64_t i = 0; i < n; ++i) ((Learner*)h)->vector_step(false); }
+uint64_t orc_learner_stats_events(void* h) { return ((Learner*)h)->stats_events; }
 void* orc_learner_qnet(void* h, int which) { Learner* l = (Learner*)h; return which == 0 ? (void*)&l->online : (void*)&l->target; }
 void orc_learner_counters(void* h, uint64_t* out /*[6]*/, double* eps, float* running_reward) {
   Learner* l = (Learner*)h;

@@ -1,0 +1,323 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see rng_ref.h / qnet_ref.h headers).
+//
+// fp32 restatement of the reference Q-network and its train step with every reduction a single fmaf chain in the
+// order the build defines.  The reference graph is float32 Keras
+// (create_ql_model_breakout_84x84x4_3_32.py:20-33,37-61; tf.float32 TensorSpecs) run by TF 2.12, whose reduction
+// order is internal to its CPU kernels and pinned by no reference test: the order is therefore part of
+// this build's definition of the arithmetic, stated here once and followed by the GPU kernels
+// (q-learning_amd/csrc/qnet32_kernels.h).  tests/test_oracle_qnet.py pins this restatement against float64 torch.
+//   conv1 forward   z = sum over (kh, c, kw) of x[4oh+kh][4ow+kw][c] W0[kh][kw][c][oc]
+//   conv2 / conv3   z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
+//   dense           z = sum over k ascending (Flatten order h, w, c)
+//   every sum: acc = 0; acc = fmaf(x, w, acc) in that order; then + bias, ReLU (v > 0 ? v : 0)
+//   Huber head      e = q_a - y, h = w (|e| <= 1 ? (0.5 e) e : |e| - 0.5), g = (w clip(e, -1, 1)) / B,
+//                   loss = (sum over b ascending of h) / B
+//   dense-3 bwd     dz4[b][k] = a4 > 0 ? W4[k][a_b] g_b : 0; dW4[k][n] = chain over b of a4[b][k] dq[b][n]
+//   dense-512 bwd   dW3[k][n] = chain over b of a3[b][k] dz4[b][n]; db3 = sum over b; dz3 = a3 > 0 ? chain over n : 0
+//   conv dgrad      dz_in[b][ih][iw][c] = a_in > 0 ? chain over the valid taps (kh, kw, oc) lexicographic : 0
+//   conv wgrad      per sample chunk z of SC_l samples: P_z = chain over (b, oh, ow) ascending; dW = ((0 + P_0) + P_1) ..
+//   clip_by_norm    per variable: segments of 8192 elements; 256 lane chains fmaf(g, g, t) over i = lane mod 256;
+//                   4 x 64-lane xor butterflies (32 .. 1); ((w0 + w1) + w2) + w3; segments summed in order
+//   Adam            legacy ResourceApplyAdam with explicit roundings (qnet_ref.cpp)
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include <omp.h>
+
+#include "qnet_ref.h"
+
+namespace orc {
+
+// chunk sizes of the conv weight-gradient partials (include/qlx.h QLX_F32_WGRAD_CHUNK_CONV*; tests check equality)
+constexpr int kSC1 = 4, kSC2 = 16, kSC3 = 16;
+constexpr int kNormSeg = 8192;
+
+static inline float fma32(float a, float b, float c) { return std::fmaf(a, b, c); }
+static inline float relu(float v) { return v > 0.0f ? v : 0.0f; }
+
+// conv1 forward from the u8 tensor view [B][84][84][4]
+static void conv1_fwd(const uint8_t* x, int B, const float* W, const float* bias, float* out) {
+#pragma omp parallel for schedule(static)
+  for (int b = 0; b < B; ++b)
+    for (int oh = 0; oh < 20; ++oh)
+      for (int ow = 0; ow < 20; ++ow) {
+        float acc[32];
+        for (int oc = 0; oc < 32; ++oc) acc[oc] = 0.0f;
+        for (int kh = 0; kh < 8; ++kh)
+          for (int c = 0; c < 4; ++c)
+            for (int kw = 0; kw < 8; ++kw) {
+              const float v = (float)x[(((size_t)b * 84 + oh * 4 + kh) * 84 + ow * 4 + kw) * 4 + c];
+              if (v == 0.0f) continue;   // fmaf(0, w, acc) == acc (acc is never -0)
+              const float* wr = W + ((kh * 8 + kw) * 4 + c) * 32;
+              for (int oc = 0; oc < 32; ++oc) acc[oc] = fma32(v, wr[oc], acc[oc]);
+            }
+        float* o = out + (((size_t)b * 20 + oh) * 20 + ow) * 32;
+        for (int oc = 0; oc < 32; ++oc) o[oc] = relu(acc[oc] + bias[oc]);
+      }
+}
+
+struct Cfg { int H, W, C, K, S, OH, OW, OC; };
+static const Cfg kC2 = {20, 20, 32, 4, 2, 9, 9, 64}, kC3 = {9, 9, 64, 3, 1, 7, 7, 64};
+
+static void conv_fwd(const Cfg& c, const float* in, int B, const float* W, const float* bias, float* out) {
+#pragma omp parallel for schedule(static)
+  for (int b = 0; b < B; ++b)
+    for (int oh = 0; oh < c.OH; ++oh)
+      for (int ow = 0; ow < c.OW; ++ow) {
+        float acc[64];
+        for (int oc = 0; oc < c.OC; ++oc) acc[oc] = 0.0f;
+        for (int kh = 0; kh < c.K; ++kh)
+          for (int kw = 0; kw < c.K; ++kw) {
+            const float* src = in + (((size_t)b * c.H + oh * c.S + kh) * c.W + ow * c.S + kw) * c.C;
+            for (int ch = 0; ch < c.C; ++ch) {
+              const float v = src[ch];
+              if (v == 0.0f) continue;
+              const float* wr = W + ((size_t)(kh * c.K + kw) * c.C + ch) * c.OC;
+              for (int oc = 0; oc < c.OC; ++oc) acc[oc] = fma32(v, wr[oc], acc[oc]);
+            }
+          }
+        float* o = out + (((size_t)b * c.OH + oh) * c.OW + ow) * c.OC;
+        for (int oc = 0; oc < c.OC; ++oc) o[oc] = relu(acc[oc] + bias[oc]);
+      }
+}
+
+// y[b][n] = act(chain over k of x[b][k] W[k][n] + bias[n])
+static void dense_fwd(const float* x, int B, int K, int N, const float* W, const float* bias, bool relu_out, float* y) {
+#pragma omp parallel for schedule(static)
+  for (int b = 0; b < B; ++b) {
+    std::vector<float> acc(N, 0.0f);
+    for (int k = 0; k < K; ++k) {
+      const float v = x[(size_t)b * K + k];
+      if (v == 0.0f) continue;
+      const float* wr = W + (size_t)k * N;
+      for (int n = 0; n < N; ++n) acc[n] = fma32(v, wr[n], acc[n]);
+    }
+    for (int n = 0; n < N; ++n) {
+      const float t = acc[n] + bias[n];
+      y[(size_t)b * N + n] = relu_out ? relu(t) : t;
+    }
+  }
+}
+
+void qnet32_forward(const QNet& q, const uint8_t* x8, int B, Acts& a) {
+  a.a1.assign((size_t)B * 20 * 20 * 32, 0.0f);
+  a.a2.assign((size_t)B * 9 * 9 * 64, 0.0f);
+  a.a3.assign((size_t)B * 7 * 7 * 64, 0.0f);
+  a.a4.assign((size_t)B * 512, 0.0f);
+  a.q.assign((size_t)B * kActions, 0.0f);
+  conv1_fwd(x8, B, q.w[0].data(), q.w[1].data(), a.a1.data());
+  conv_fwd(kC2, a.a1.data(), B, q.w[2].data(), q.w[3].data(), a.a2.data());
+  conv_fwd(kC3, a.a2.data(), B, q.w[4].data(), q.w[5].data(), a.a3.data());
+  dense_fwd(a.a3.data(), B, 3136, 512, q.w[6].data(), q.w[7].data(), true, a.a4.data());
+  dense_fwd(a.a4.data(), B, 512, kActions, q.w[8].data(), q.w[9].data(), false, a.q.data());
+}
+
+// conv weight gradient of one layer, chunked: dW [K*K*C][OC] and db [OC] from input `in` (fp32 NHWC, or the u8
+// tensor view when in8 != null: conv1) and the ReLU-masked output gradient dz [B][OH][OW][OC]
+static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const float* dz, int B, int SC, float* dW, float* db) {
+  const int KK = c.K * c.K * c.C, nz = (B + SC - 1) / SC;
+  std::vector<float> part((size_t)nz * (KK + 1) * c.OC, 0.0f);
+#pragma omp parallel for schedule(dynamic)
+  for (int z = 0; z < nz; ++z) {
+    float* P = part.data() + (size_t)z * (KK + 1) * c.OC;
+    float* Pb = P + (size_t)KK * c.OC;
+    for (int b = z * SC; b < std::min(B, (z + 1) * SC); ++b)
+      for (int oh = 0; oh < c.OH; ++oh)
+        for (int ow = 0; ow < c.OW; ++ow) {
+          const float* d = dz + (((size_t)b * c.OH + oh) * c.OW + ow) * c.OC;
+          bool any = false;
+          for (int oc = 0; oc < c.OC; ++oc) {
+            Pb[oc] = Pb[oc] + d[oc];
+            any |= d[oc] != 0.0f;
+          }
+          if (!any) continue;   // fmaf(x, 0, acc) == acc
+          for (int kh = 0; kh < c.K; ++kh)
+            for (int kw = 0; kw < c.K; ++kw)
+              for (int ch = 0; ch < c.C; ++ch) {
+                const int ih = oh * c.S + kh, iw = ow * c.S + kw;
+                const float v = in8 ? (float)in8[(((size_t)b * c.H + ih) * c.W + iw) * c.C + ch]
+                                    : in[(((size_t)b * c.H + ih) * c.W + iw) * c.C + ch];
+                if (v == 0.0f) continue;
+                float* pr = P + ((size_t)(kh * c.K + kw) * c.C + ch) * c.OC;
+                for (int oc = 0; oc < c.OC; ++oc) pr[oc] = fma32(v, d[oc], pr[oc]);
+              }
+        }
+  }
+  for (int i = 0; i < KK * c.OC; ++i) {
+    float t = 0.0f;
+    for (int z = 0; z < nz; ++z) t = t + part[(size_t)z * (KK + 1) * c.OC + i];
+    dW[i] = t;
+  }
+  for (int oc = 0; oc < c.OC; ++oc) {
+    float t = 0.0f;
+    for (int z = 0; z < nz; ++z) t = t + part[((size_t)z * (KK + 1) + KK) * c.OC + oc];
+    db[oc] = t;
+  }
+}
+
+// conv backward-data: din[b][ih][iw][c] = mask(a_in) * chain over the valid (kh, kw, oc) of dz[..][oc] W[kh][kw][c][oc]
+static void conv_dgrad(const Cfg& c, const float* dz, int B, const float* W, const float* a_in, float* din) {
+  // W transposed to [kh][kw][oc][c] so the per-c chains run along contiguous memory
+  std::vector<float> WT((size_t)c.K * c.K * c.OC * c.C);
+  for (int t = 0; t < c.K * c.K; ++t)
+    for (int ch = 0; ch < c.C; ++ch)
+      for (int oc = 0; oc < c.OC; ++oc) WT[((size_t)t * c.OC + oc) * c.C + ch] = W[((size_t)t * c.C + ch) * c.OC + oc];
+#pragma omp parallel for schedule(static)
+  for (int b = 0; b < B; ++b)
+    for (int ih = 0; ih < c.H; ++ih)
+      for (int iw = 0; iw < c.W; ++iw) {
+        float acc[64];
+        for (int ch = 0; ch < c.C; ++ch) acc[ch] = 0.0f;
+        for (int kh = 0; kh < c.K; ++kh) {
+          const int th = ih - kh;
+          if (th < 0 || th % c.S != 0 || th / c.S >= c.OH) continue;
+          for (int kw = 0; kw < c.K; ++kw) {
+            const int tw = iw - kw;
+            if (tw < 0 || tw % c.S != 0 || tw / c.S >= c.OW) continue;
+            const float* d = dz + (((size_t)b * c.OH + th / c.S) * c.OW + tw / c.S) * c.OC;
+            for (int oc = 0; oc < c.OC; ++oc) {
+              const float v = d[oc];
+              if (v == 0.0f) continue;
+              const float* wr = WT.data() + ((size_t)(kh * c.K + kw) * c.OC + oc) * c.C;
+              for (int ch = 0; ch < c.C; ++ch) acc[ch] = fma32(v, wr[ch], acc[ch]);
+            }
+          }
+        }
+        const size_t o = (((size_t)b * c.H + ih) * c.W + iw) * c.C;
+        for (int ch = 0; ch < c.C; ++ch) din[o + ch] = a_in[o + ch] > 0.0f ? acc[ch] : 0.0f;
+      }
+}
+
+float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* actions, const float* y, int B, const Acts& a,
+                           Grads& g, const float* weights, float* td_abs) {
+  for (int v = 0; v < kNumVars; ++v) g.g[v].assign(kVarSize[v], 0.0f);
+  // Huber head
+  std::vector<float> gs(B), hs(B);
+  float lsum = 0.0f;
+  for (int b = 0; b < B; ++b) {
+    const float qa = a.q[(size_t)b * kActions + actions[b]];
+    const float e = qa - y[b];
+    const float ae = std::fabs(e);
+    const float w = weights ? weights[b] : 1.0f;
+    const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
+    gs[b] = (w * ge) / (float)B;
+    hs[b] = w * (ae <= 1.0f ? 0.5f * e * e : ae - 0.5f);
+    lsum = lsum + hs[b];
+    if (td_abs) td_abs[b] = ae;
+  }
+  const float loss = lsum / (float)B;
+  // dense 512 -> 3
+  const float* W4 = q.w[8].data();
+  std::vector<float> dz4((size_t)B * 512);
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < 512; ++k) {
+      const float av = a.a4[(size_t)b * 512 + k];
+      dz4[(size_t)b * 512 + k] = av > 0.0f ? W4[k * 3 + actions[b]] * gs[b] : 0.0f;
+    }
+  for (int k = 0; k < 512; ++k) {
+    float s[3] = {0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < B; ++b)
+      for (int n = 0; n < 3; ++n) s[n] = fma32(a.a4[(size_t)b * 512 + k], actions[b] == n ? gs[b] : 0.0f, s[n]);
+    for (int n = 0; n < 3; ++n) g.g[8][k * 3 + n] = s[n];
+  }
+  for (int n = 0; n < 3; ++n) {
+    float s = 0.0f;
+    for (int b = 0; b < B; ++b) s = s + (actions[b] == n ? gs[b] : 0.0f);
+    g.g[9][n] = s;
+  }
+  // dense 3136 -> 512
+  float* dW3 = g.g[6].data();
+#pragma omp parallel for schedule(static)
+  for (int k = 0; k < 3136; ++k) {
+    float* row = dW3 + (size_t)k * 512;
+    for (int b = 0; b < B; ++b) {
+      const float v = a.a3[(size_t)b * 3136 + k];
+      if (v == 0.0f) continue;
+      const float* d = dz4.data() + (size_t)b * 512;
+      for (int n = 0; n < 512; ++n) row[n] = fma32(v, d[n], row[n]);
+    }
+  }
+  for (int n = 0; n < 512; ++n) {
+    float s = 0.0f;
+    for (int b = 0; b < B; ++b) s = s + dz4[(size_t)b * 512 + n];
+    g.g[7][n] = s;
+  }
+  std::vector<float> W3T((size_t)512 * 3136);
+  for (int k = 0; k < 3136; ++k)
+    for (int n = 0; n < 512; ++n) W3T[(size_t)n * 3136 + k] = q.w[6][(size_t)k * 512 + n];
+  std::vector<float> dz3((size_t)B * 3136);
+#pragma omp parallel for schedule(static)
+  for (int b = 0; b < B; ++b) {
+    std::vector<float> acc(3136, 0.0f);
+    for (int n = 0; n < 512; ++n) {
+      const float v = dz4[(size_t)b * 512 + n];
+      if (v == 0.0f) continue;
+      const float* wr = W3T.data() + (size_t)n * 3136;
+      for (int k = 0; k < 3136; ++k) acc[k] = fma32(v, wr[k], acc[k]);
+    }
+    for (int k = 0; k < 3136; ++k) dz3[(size_t)b * 3136 + k] = a.a3[(size_t)b * 3136 + k] > 0.0f ? acc[k] : 0.0f;
+  }
+  // conv3, conv2, conv1
+  std::vector<float> dz2((size_t)B * 81 * 64), dz1((size_t)B * 400 * 32);
+  conv_wgrad(kC3, a.a2.data(), nullptr, dz3.data(), B, kSC3, g.g[4].data(), g.g[5].data());
+  conv_dgrad(kC3, dz3.data(), B, q.w[4].data(), a.a2.data(), dz2.data());
+  conv_wgrad(kC2, a.a1.data(), nullptr, dz2.data(), B, kSC2, g.g[2].data(), g.g[3].data());
+  conv_dgrad(kC2, dz2.data(), B, q.w[2].data(), a.a1.data(), dz1.data());
+  // conv1's wgrad chain runs over (b, oh, ow) with its rows in the order (kh, c, kw) on the GPU; per output element
+  // the chain order is the same (b, oh, ow) whatever the row order, so the HWIO restatement gives the same bits
+  const Cfg c1 = {84, 84, 4, 8, 4, 20, 20, 32};
+  conv_wgrad(c1, nullptr, x8, dz1.data(), B, kSC1, g.g[0].data(), g.g[1].data());
+  return loss;
+}
+
+// per-variable sums of squares in the build's order (header)
+static float sumsq32(const float* g, int64_t n) {
+  float total = 0.0f;
+  for (int64_t b = 0; b < n; b += kNormSeg) {
+    const int64_t e = std::min<int64_t>(n, b + kNormSeg);
+    float t[256];
+    for (int l = 0; l < 256; ++l) {
+      float s = 0.0f;
+      for (int64_t i = b + l; i < e; i += 256) s = fma32(g[i], g[i], s);
+      t[l] = s;
+    }
+    float w[4];
+    for (int wv = 0; wv < 4; ++wv) {
+      float v[64];
+      for (int l = 0; l < 64; ++l) v[l] = t[wv * 64 + l];
+      for (int off = 32; off > 0; off >>= 1) {
+        float nv[64];
+        for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+        std::memcpy(v, nv, sizeof(v));
+      }
+      w[wv] = v[0];
+    }
+    total = total + (((w[0] + w[1]) + w[2]) + w[3]);
+  }
+  return total;
+}
+
+void qnet32_apply_adam(QNet& q, const Grads& g, float* norms_out) {
+  const float t = (float)(q.iterations + 1);
+  const float b1p = std::pow(q.beta1, t), b2p = std::pow(q.beta2, t);
+  const float alpha = q.lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
+  for (int v = 0; v < kNumVars; ++v) {
+    const float l2sum = sumsq32(g.g[v].data(), kVarSize[v]);
+    const float l2norm = l2sum > 0.0f ? std::sqrt(l2sum) : l2sum;
+    if (norms_out) norms_out[v] = l2norm;
+    const float denom = std::max(l2norm, q.clipnorm);
+    float* w = q.w[v].data();
+    float* m = q.m[v].data();
+    float* vv = q.v[v].data();
+    for (int i = 0; i < kVarSize[v]; ++i) {
+      const float gc = (g.g[v][i] * q.clipnorm) / denom;
+      m[i] += (gc - m[i]) * (1.0f - q.beta1);
+      vv[i] += (gc * gc - vv[i]) * (1.0f - q.beta2);
+      w[i] -= (m[i] * alpha) / (std::sqrt(vv[i]) + q.eps);
+    }
+  }
+  q.iterations += 1;
+}
+
+}  // namespace orc

@@ -51,6 +51,13 @@ float qnet_loss_backward(const QNet& q, const uint8_t* x, const uint8_t* actions
 // clip_by_norm per variable + ResourceApplyAdam, iterations += 1
 void qnet_apply_adam(QNet& q, const Grads& grads, float* norms_out /*[10] or null*/);
 
+// The fp32 arithmetic of the product's QLX_ARCH_NATURE_DQN (qnet32_ref.cpp): the same math with every reduction a
+// single fmaf chain in the order the build defines, so the GPU results match bit for bit.
+void qnet32_forward(const QNet& q, const uint8_t* x, int B, Acts& acts);
+float qnet32_loss_backward(const QNet& q, const uint8_t* x, const uint8_t* actions, const float* y, int B,
+                           const Acts& acts, Grads& grads, const float* weights = nullptr, float* td_abs = nullptr);
+void qnet32_apply_adam(QNet& q, const Grads& grads, float* norms_out /*[10] or null*/);
+
 // reference helpers
 int argmax_first(const float* q, int n);
 

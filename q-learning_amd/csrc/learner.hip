@@ -224,6 +224,12 @@ struct qlx_learner {
   hipEvent_t ev_dense = nullptr, ev_reduced = nullptr;
   int world = 1, rank = 0;
   qlx::Profiler prof;
+  // statistics events (write_checkpoint + learning_update_log, self_driving_tf_q_learner.rs:204-212,226-230)
+  uint64_t stats_events = 0;
+  uint64_t seen_episodes = 0;
+  std::string last_log;
+  void (*log_cb)(const char*, void*) = nullptr;
+  void* log_user = nullptr;
 };
 
 namespace qlx {
@@ -310,7 +316,7 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
   L->update_count += 1;
 }
 
-static void learner_vector_step(qlx_learner* L) {
+static void learner_vector_step(qlx_learner* L, bool train = true) {
   hipStream_t s = L->stream;
   const uint32_t N = L->N;
   const uint64_t step_before = L->step_count;
@@ -348,7 +354,7 @@ static void learner_vector_step(qlx_learner* L) {
   const uint64_t ua = L->p.update_after_actions;
   const uint64_t triggers = L->step_count / ua - step_before / ua;
   L->last_updates = 0;
-  if (L->rb->len() > L->B && triggers > 0) {
+  if (train && L->rb->len() > L->B && triggers > 0) {
     const uint32_t U = (uint32_t)triggers;
     QLX_CHECK(U <= L->max_updates, QLX_E_STATE, "too many updates per vector step");
     const uint64_t cap = L->rb->cap, start = (L->rb->total - L->rb->len()) % cap;
@@ -407,6 +413,8 @@ void qlx_params_default(qlx_params* p) {
   p->per_alpha = 0.6f;   // Schaul et al. 2016 proportional variant
   p->per_beta = 0.4f;
   p->per_eps = 1e-6f;
+  p->qnet_precision = QLX_PREC_F32;   // the reference's arithmetic
+  p->stats_after_steps = 25000;       // Parameter::default (self_driving_tf_q_learner.rs:63)
 }
 
 int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** out) {
@@ -416,6 +424,9 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
     QLX_CHECK(p->update_after_actions > 0 && p->history_buffer_len >= p->batch_size, QLX_E_INVALID, "bad parameters");
     QLX_CHECK(p->episode_reward_history_buffer_len > 0, QLX_E_INVALID, "episode_reward_history_buffer_len must be > 0");
     QLX_CHECK((p->flags & ~(QLX_LEARNER_DOUBLE_DQN | QLX_LEARNER_PER)) == 0, QLX_E_INVALID, "unknown learner flags");
+    QLX_CHECK(p->qnet_precision == QLX_PREC_F32 || p->qnet_precision == QLX_PREC_BF16, QLX_E_INVALID, "unknown qnet_precision");
+    QLX_CHECK(p->qnet_precision == QLX_PREC_BF16 || p->batch_size <= (uint32_t)kF32FwdChunk, QLX_E_INVALID,
+              "fp32 batch_size above the forward chunk");
     QLX_CHECK(!(p->flags & QLX_LEARNER_PER) || (p->per_alpha >= 0.0f && p->per_beta >= 0.0f && p->per_eps > 0.0f),
               QLX_E_INVALID, "prioritized replay needs alpha >= 0, beta >= 0, eps > 0");
     current_device_checked(device);
@@ -434,9 +445,10 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       QLX_CHECK(st == QLX_OK, st, qlx_last_error());
       st = qlx_replay_create(p->history_buffer_len, L->N, device, &L->rb);
       QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-      st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->online);
+      const int32_t arch = p->qnet_precision == QLX_PREC_BF16 ? QLX_ARCH_NATURE_DQN_BF16 : QLX_ARCH_NATURE_DQN;
+      st = qlx_model_create(arch, p->init_seed, device, &L->online);
       QLX_CHECK(st == QLX_OK, st, qlx_last_error());
-      st = qlx_model_create(QLX_ARCH_NATURE_DQN, p->init_seed, device, &L->target);   // same initial weights
+      st = qlx_model_create(arch, p->init_seed, device, &L->target);   // same initial weights
       QLX_CHECK(st == QLX_OK, st, qlx_last_error());
       // everything runs on the learner's stream
       L->env->stream = L->stream; L->env->own_stream = false;
@@ -517,11 +529,13 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
   });
 }
 
+static void learner_step_full(qlx_learner* L, bool train);
+
 int32_t qlx_learner_vector_step(qlx_learner* L) {
   return guard([&] {
     QLX_CHECK(L, QLX_E_INVALID, "null learner");
     QLX_HIP(hipSetDevice(L->device));
-    learner_vector_step(L);
+    learner_step_full(L, true);
   });
 }
 
@@ -529,7 +543,48 @@ int32_t qlx_learner_run(qlx_learner* L, uint64_t n) {
   return guard([&] {
     QLX_CHECK(L, QLX_E_INVALID, "null learner");
     QLX_HIP(hipSetDevice(L->device));
-    for (uint64_t i = 0; i < n; ++i) learner_vector_step(L);
+    for (uint64_t i = 0; i < n; ++i) learner_step_full(L, true);
+  });
+}
+
+int32_t qlx_learner_prefill(qlx_learner* L, uint64_t n) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipSetDevice(L->device));
+    for (uint64_t i = 0; i < n; ++i) learner_step_full(L, false);
+  });
+}
+
+int32_t qlx_learner_learn_till_mastered(qlx_learner* L, uint64_t max_vector_steps, uint64_t* steps_run) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    QLX_HIP(hipSetDevice(L->device));
+    uint64_t i = 0;
+    qlx_learner_stats st{};
+    for (; i < max_vector_steps; ++i) {
+      learner_step_full(L, true);
+      const int32_t rc = qlx_learner_stats_get(L, &st);
+      QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+      if (st.solved) { ++i; break; }
+    }
+    if (steps_run) *steps_run = i;
+  });
+}
+
+uint64_t qlx_learner_stats_events(const qlx_learner* L) { return L ? L->stats_events : 0; }
+
+int32_t qlx_learner_set_log_callback(qlx_learner* L, void (*cb)(const char* text, void* user), void* user) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    L->log_cb = cb;
+    L->log_user = user;
+  });
+}
+
+int32_t qlx_learner_last_log(qlx_learner* L, char* buf, size_t cap, size_t* len) {
+  return guard([&] {
+    QLX_CHECK(L, QLX_E_INVALID, "null learner");
+    copy_text(L->last_log, buf, cap, len);
   });
 }
 
@@ -648,6 +703,52 @@ int32_t qlx_learner_update_log(qlx_learner* L, char* buf, size_t cap, size_t* le
     copy_text(learning_log(in), buf, cap, len);
   });
 }
+
+}  // extern "C"
+
+// One vector step, then the reference's statistics events (self_driving_tf_q_learner.rs:204-212, 226-230):
+// write_checkpoint (when checkpoint_file is set) + learning_update_log once per vector step that crossed a multiple of
+// stats_after_steps, and once more when an episode ended and solved() holds.  The log text goes to the callback (the
+// reference's log::info!) and stays readable through qlx_learner_last_log.  With stats_after_steps = 0 nothing runs.
+static void learner_stats_event(qlx_learner* L) {
+  if (L->p.checkpoint_file[0]) {
+    char path[257];
+    std::memcpy(path, L->p.checkpoint_file, 256);
+    path[256] = 0;
+    const int32_t rc = qlx_model_write_checkpoint(L->online, path);
+    QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+  }
+  size_t n = 0;
+  int32_t rc = qlx_learner_update_log(L, nullptr, 0, &n);
+  QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+  std::string text(n + 1, '\0');
+  rc = qlx_learner_update_log(L, &text[0], text.size(), &n);
+  QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+  text.resize(n);
+  L->last_log = text;
+  L->stats_events += 1;
+  if (L->log_cb) L->log_cb(L->last_log.c_str(), L->log_user);
+}
+
+static void learner_step_full(qlx_learner* L, bool train) {
+  const uint64_t before = L->step_count;
+  learner_vector_step(L, train);
+  const uint64_t S = L->p.stats_after_steps;
+  if (S == 0) return;
+  if (L->step_count / S != before / S) learner_stats_event(L);
+  Book b;   // solved() after an episode ended in this step (:226-230)
+  QLX_HIP(hipMemcpyAsync(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost, L->stream));
+  QLX_HIP(hipStreamSynchronize(L->stream));
+  if (b.episode_count != L->seen_episodes) {
+    L->seen_episodes = b.episode_count;
+    qlx_learner_stats st{};
+    const int32_t rc = qlx_learner_stats_get(L, &st);
+    QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+    if (st.solved) learner_stats_event(L);
+  }
+}
+
+extern "C" {
 
 qlx_env* qlx_learner_env(qlx_learner* L) { return L ? L->env : nullptr; }
 qlx_replay* qlx_learner_replay(qlx_learner* L) { return L ? L->rb : nullptr; }

@@ -32,12 +32,24 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float* slab = nullptr;
   float* bslab = nullptr;
   float* loss = nullptr;
+  // fp32 path (qnet32.hip): activations a1..a3 per forward chunk of `fchunk` samples, a4 for the whole batch; the
+  // gradient buffers (dz, weight-gradient chunk slabs) in their own allocation `fgrad`, sized for fgrad_batch
+  float *fa1 = nullptr, *fa2 = nullptr, *fa3 = nullptr, *fa4 = nullptr;
+  float *fdz1 = nullptr, *fdz2 = nullptr, *fdz3 = nullptr, *fdz4 = nullptr;
+  float *fslab1 = nullptr, *fslab2 = nullptr, *fslab3 = nullptr;
+  float* fpart = nullptr;   // clip_by_norm segment partials
+  int fchunk = 0;
+  void* fgrad = nullptr;
+  int fgrad_batch = 0;
 };
+
+constexpr int kF32FwdChunk = 8192;   // samples per fp32 forward pass (bounds the a1..a3 workspace)
 
 }  // namespace qlx
 
 struct qlx_model {
   int device = 0;
+  bool f32 = true;   // QLX_ARCH_NATURE_DQN: fp32 (the reference's arithmetic); QLX_ARCH_NATURE_DQN_BF16: bf16 MFMA operands
   hipStream_t stream = nullptr;
   bool own_stream = true;
   float* d_params = nullptr;   // fp32 master weights, Keras layouts, variables concatenated
@@ -74,6 +86,7 @@ struct qlx_model {
 namespace qlx {
 struct Fc2Args {
   const __bf16* a4;          // [B][512]
+  const float* a4f;          // fp32 model: [B][512]
   // pending split-K fc1 partials (splits > 0): the head finishes a4 = relu(sum_z slab[z] + b3) in fixed z order
   // and writes it to a4_out, so no separate reduction launch runs
   const float* slab;
@@ -119,4 +132,14 @@ void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipSt
 // fused partials are used as they are; otherwise per-range sums of squares of the scaled gradients
 void model_norms(qlx_model* m, hipStream_t s, float scale);
 void model_adam(qlx_model* m, hipStream_t s, float scale);
+
+// fp32 path (qnet32.hip), dispatched to by the model_* functions when m->f32
+void f32_workspace(qlx_model* m, int B);
+void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
+void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s);   // mode 3 = training head
+void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
+                        const float* weights, float* td_abs);
+void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
+void f32_norms(qlx_model* m, hipStream_t s, float scale);
+void f32_adam(qlx_model* m, hipStream_t s, float scale);
 }  // namespace qlx

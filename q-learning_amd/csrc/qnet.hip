@@ -366,6 +366,7 @@ static void fc1_bwd_map(qlx_model* m, const GemmProblem<E1>& Pw, const GemmProbl
 }
 
 void launch_fc2(int mode, const Fc2Args& a, int B, hipStream_t s) {
+  if (a.a4f) { f32_head(mode, a, B, s); return; }
   const dim3 g((B + 3) / 4), blk(256);
   switch (mode) {
     case 0: hipLaunchKernelGGL(k_fc2<0>, g, blk, 0, s, a); break;
@@ -468,6 +469,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 void model_workspace(qlx_model* m, int B) {
+  if (m->f32) { f32_workspace(m, B); return; }
   if (B <= m->ws_batch) return;
   QLX_HIP(hipStreamSynchronize(m->stream));
   if (m->ws) (void)hipFree(m->ws);
@@ -511,6 +513,7 @@ static PackPtrs pack_ptrs(qlx_model* m) {
 }
 
 void model_pack(qlx_model* m) {
+  if (m->f32) return;   // the fp32 path reads the master weights directly
   hipLaunchKernelGGL(k_pack_all, dim3(2048), dim3(256), 0, m->stream, m->d_params, (int64_t)kNumParams, pack_ptrs(m));
   QLX_HIP(hipGetLastError());
 }
@@ -542,6 +545,7 @@ static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, 
 }
 
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts) {
+  if (m->f32) { f32_forward(m, table, B, s); return; }
   ModelWs& w = m->w;
   m->last_batch = B;
   const float* p = m->d_params;
@@ -578,6 +582,7 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
 Fc2Args fc2_args(qlx_model* m, int B) {
   Fc2Args a{};
   a.a4 = m->w.a4;
+  a.a4f = m->f32 ? m->w.fa4 : nullptr;
   a.w4 = m->d_params + var_offset(8);
   a.b4 = m->d_params + var_offset(9);
   a.B = B;
@@ -602,6 +607,7 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
 // the head and dense part of the backward: Huber (+ dz4), dW4 / db4 / loss, dW3 / db3 and dz3
 void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
                           const float* weights, float* td_abs) {
+  if (m->f32) { f32_backward_dense(m, B, actions, y, loss_dev, s, weights, td_abs); return; }
   ModelWs& w = m->w;
   float* G = m->d_grads;
   {  // head: q, Huber, dz4 (one wave per sample)
@@ -643,6 +649,7 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
 // the conv part of the backward (after model_backward_dense on the same batch): dz3 -> dz2 -> dz1 and the
 // three conv weight gradients into m->d_grads
 void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+  if (m->f32) { f32_backward_conv(m, table, B, s); return; }
   ModelWs& w = m->w;
   float* G = m->d_grads;
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
@@ -712,6 +719,7 @@ void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipSt
 
 
 void model_norms(qlx_model* m, hipStream_t s, float scale) {
+  if (m->f32) { f32_norms(m, s, scale); return; }
   m->norms_fused = scale == 1.0f;   // the gradients are exactly what model_backward produced
   if (m->norms_fused) return;
   ProfScope ps(m->prof, "norms", s);
@@ -720,6 +728,7 @@ void model_norms(qlx_model* m, hipStream_t s, float scale) {
 }
 
 void model_adam(qlx_model* m, hipStream_t s, float scale) {
+  if (m->f32) { f32_adam(m, s, scale); return; }
   const int64_t t = m->iterations + 1;
   const float tf = (float)t;
   const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
@@ -777,9 +786,10 @@ int64_t qlx_model_var_size(int32_t v) { return (v >= 0 && v < kNumVars) ? kVarSi
 
 int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out) {
   return guard([&] {
-    QLX_CHECK(arch == QLX_ARCH_NATURE_DQN && out, QLX_E_INVALID, "unknown model arch");
+    QLX_CHECK((arch == QLX_ARCH_NATURE_DQN || arch == QLX_ARCH_NATURE_DQN_BF16) && out, QLX_E_INVALID, "unknown model arch");
     current_device_checked(device);
     auto* m = new qlx_model;
+    m->f32 = arch == QLX_ARCH_NATURE_DQN;
     const char* ch = std::getenv("QLX_CONV1_HALVES");
     m->conv1_halves = !(ch && ch[0] == '0');
     try {   // a failure part-way releases what was built
@@ -790,12 +800,14 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
       QLX_HIP(hipMalloc(&m->d_m, pb));
       QLX_HIP(hipMalloc(&m->d_v, pb));
       QLX_HIP(hipMalloc(&m->d_grads, pb));
-      QLX_HIP(hipMalloc(&m->wf0, 32 * 256 * 2));
-      QLX_HIP(hipMalloc(&m->wf1, 64 * 512 * 2));
-      QLX_HIP(hipMalloc(&m->wb1, 32 * 1024 * 2));
-      QLX_HIP(hipMalloc(&m->wf2, 64 * 576 * 2));
-      QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
-      QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
+      if (!m->f32) {   // bf16 MFMA operand copies
+        QLX_HIP(hipMalloc(&m->wf0, 32 * 256 * 2));
+        QLX_HIP(hipMalloc(&m->wf1, 64 * 512 * 2));
+        QLX_HIP(hipMalloc(&m->wb1, 32 * 1024 * 2));
+        QLX_HIP(hipMalloc(&m->wf2, 64 * 576 * 2));
+        QLX_HIP(hipMalloc(&m->wb2, 64 * 576 * 2));
+        QLX_HIP(hipMalloc(&m->wb3, 3136 * 512 * 2));
+      }
       // norm ranges: chunks of <= 2048 elements (~830 blocks) that never cross a variable
       std::vector<int64_t> rb, re;
       std::vector<int> vf(kNumVars + 1, 0);
@@ -848,7 +860,8 @@ int32_t qlx_model_destroy(qlx_model* m) {
     (void)hipSetDevice(m->device);
     (void)hipStreamSynchronize(m->stream);
     void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wb3,
-                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->d_sqf, m->d_sqf_first, m->ws, m->d_fc1bwd_map};
+                    m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->d_sqf, m->d_sqf_first, m->ws, m->d_fc1bwd_map,
+                    m->w.fgrad};
     for (void* p : ptrs) (void)hipFree(p);
     if (m->own_stream) (void)hipStreamDestroy(m->stream);
     delete m;
@@ -897,8 +910,7 @@ int32_t qlx_model_predict(qlx_model* m, const uint8_t* obs, uint32_t n, float* q
     model_forward_trunk(m, m->w.table, (int)n, m->stream);
     Fc2Args a = fc2_args(m, (int)n);
     a.argmax = m->w.argmax;
-    hipLaunchKernelGGL(k_fc2<1>, dim3((n + 3) / 4), dim3(256), 0, m->stream, a);
-    QLX_HIP(hipGetLastError());
+    launch_fc2(1, a, (int)n, m->stream);
     if (q_out) QLX_HIP(hipMemcpyAsync(q_out, m->w.q, n * 3 * sizeof(float), hipMemcpyDeviceToHost, m->stream));
     if (actions) QLX_HIP(hipMemcpyAsync(actions, m->w.argmax, n, hipMemcpyDeviceToHost, m->stream));
     QLX_HIP(hipStreamSynchronize(m->stream));
@@ -916,8 +928,7 @@ int32_t qlx_model_batch_max_q(qlx_model* m, const uint8_t* obs, uint32_t n, floa
     QLX_HIP(hipMemsetAsync(m->w.done, 0, n, m->stream));
     Fc2Args a = fc2_args(m, (int)n);
     a.rewards = m->w.rew; a.dones = m->w.done; a.gamma = 1.0f; a.y_out = m->w.y;
-    hipLaunchKernelGGL(k_fc2<2>, dim3((n + 3) / 4), dim3(256), 0, m->stream, a);
-    QLX_HIP(hipGetLastError());
+    launch_fc2(2, a, (int)n, m->stream);
     QLX_HIP(hipMemcpyAsync(out, m->w.y, n * sizeof(float), hipMemcpyDeviceToHost, m->stream));
     QLX_HIP(hipStreamSynchronize(m->stream));
   });
@@ -948,6 +959,14 @@ int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
   return guard([&] {
     QLX_CHECK(m && out && layer >= 1 && layer <= 4 && m->ws_batch > 0, QLX_E_INVALID, "bad argument");
     QLX_HIP(hipSetDevice(m->device));
+    if (m->f32) {   // a1..a3 of the last forward chunk (the whole batch up to kF32FwdChunk samples), a4 of all
+      QLX_CHECK(layer == 4 || m->last_batch <= m->w.fchunk, QLX_E_STATE, "activations of a chunked forward");
+      QLX_HIP(hipStreamSynchronize(m->stream));
+      const size_t per[5] = {0, 12800, 5184, 3136, 512};
+      const float* src = layer == 1 ? m->w.fa1 : layer == 2 ? m->w.fa2 : layer == 3 ? m->w.fa3 : m->w.fa4;
+      QLX_HIP(hipMemcpy(out, src, per[layer] * (size_t)m->last_batch * 4, hipMemcpyDeviceToHost));
+      return;
+    }
     if (layer == 4 && m->w.a4_splits > 0) {   // forward without a head yet: finish a4 from the fc1 partials
       const int B = m->last_batch;
       hipLaunchKernelGGL(k_slab_reduce_bias_relu, dim3(std::min(2048, (B * 512 + 255) / 256)), dim3(256), 0, m->stream,

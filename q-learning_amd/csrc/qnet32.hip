@@ -1,0 +1,500 @@
+// fp32 DeepQLearningModel path (the reference's arithmetic): Nature-DQN forward / Huber / backward /
+// clip_by_norm / Adam on v_mfma_f32_16x16x4_f32, bit-exact against oracle/qnet32_ref.cpp.
+//
+// Reference (restated): create_ql_model_breakout_84x84x4_3_32.py:20-33 (float32 Keras graph), :36-55 (predict_action,
+// batch_predict_max_future_reward), :63-82 (train_model; intended q_a = Q(s)[a] of
+// create_ql_model_ballgame_3x3x4_5_512.py:71-78), legacy Keras Adam(lr 2.5e-4, clipnorm 1.0) = tf.clip_by_norm per
+// variable + ResourceApplyAdam, Huber(delta = 1) mean over the batch.  Orders of every reduction: DESIGN.md §6.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "objects.h"
+#include "profiler.h"
+#include "qnet.h"
+#include "qnet32_kernels.h"
+
+namespace qlx {
+
+using namespace q32;
+
+static int64_t voff(int v) {
+  int64_t o = 0;
+  for (int i = 0; i < v; ++i) o += kVarSize[i];
+  return o;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// dense 512 -> 3 head, one thread per sample: q[n] = (fmaf chain over k ascending of a4[k] W4[k][n]) + b4[n]
+//   MODE 0: q;  1: q + argmax (predict_action);  2: Bellman target y = r + max_a q * gamma (or q at the online net's
+//   argmax, double DQN), y = r if done;  3: training head (Huber value h, dloss/dq_a g, |e|)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
+  __shared__ float w4s[512 * 3];
+  for (int i = threadIdx.x; i < 512 * 3; i += 256) w4s[i] = A.w4[i];
+  __syncthreads();
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= A.B) return;
+  const float* x = A.a4f + (size_t)b * 512;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 4
+  for (int k = 0; k < 512; k += 4) {
+    const f32x4 v = ld4(x + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s0 = fmaf(v[j], w4s[(k + j) * 3 + 0], s0);
+      s1 = fmaf(v[j], w4s[(k + j) * 3 + 1], s1);
+      s2 = fmaf(v[j], w4s[(k + j) * 3 + 2], s2);
+    }
+  }
+  const float q0 = __fadd_rn(s0, A.b4[0]), q1 = __fadd_rn(s1, A.b4[1]), q2 = __fadd_rn(s2, A.b4[2]);
+  if (A.q) { A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2; }
+  if (MODE == 1) {   // tf.argmax: first maximal index
+    int best = 0;
+    float bv = q0;
+    if (q1 > bv) { best = 1; bv = q1; }
+    if (q2 > bv) best = 2;
+    A.argmax[b] = (uint8_t)best;
+  } else if (MODE == 2) {
+    float mx;
+    if (A.q_select) {
+      const float* qs = A.q_select + b * 3;
+      int best = 0;
+      float bv = qs[0];
+      if (qs[1] > bv) { best = 1; bv = qs[1]; }
+      if (qs[2] > bv) best = 2;
+      mx = best == 0 ? q0 : (best == 1 ? q1 : q2);
+    } else {
+      mx = fmaxf(fmaxf(q0, q1), q2);
+    }
+    const float r = A.rewards[b];
+    // add_arrays(reward, array_mul(max_future, gamma)) (self_driving_tf_q_learner.rs:189-199,298-315): two roundings
+    A.y_out[b] = A.dones[b] ? r : __fadd_rn(r, __fmul_rn(mx, A.gamma));
+  } else if (MODE == 3) {
+    const int a = A.actions[b];
+    const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
+    const float e = __fsub_rn(qa, A.y[b]);
+    const float ae = fabsf(e);
+    const float wgt = A.weights ? A.weights[b] : 1.0f;   // prioritized replay: the IS weight scales h and dloss/dq
+    const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
+    A.gsample[b] = __fmul_rn(wgt, ge) / (float)A.B;
+    A.hsample[b] = __fmul_rn(wgt, ae <= 1.0f ? __fmul_rn(__fmul_rn(0.5f, e), e) : __fsub_rn(ae, 0.5f));
+    if (A.td_abs) A.td_abs[b] = ae;
+  }
+}
+
+// dz4[b][k] = (a4 > 0) ? W4[k][a_b] * g_b : 0  (the dense-3 backward: dq is g_b at a_b and 0 elsewhere, so the
+// fmaf chain over n of W4[k][n] dq[b][n] is the single rounded product)
+__global__ __launch_bounds__(256) void k_dz4_32(const float* a4, const float* w4, const uint8_t* act, const float* gs, int B,
+                                                float* dz4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // float4 index
+  if (i >= B * 128) return;
+  const int b = i >> 7, k = (i & 127) * 4;
+  const f32x4 x = ld4(a4 + (size_t)i * 4);
+  const int a = act[b];
+  const float g = gs[b];
+  f32x4 d;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) d[j] = x[j] > 0.0f ? __fmul_rn(w4[(k + j) * 3 + a], g) : 0.0f;
+  *reinterpret_cast<f32x4*>(dz4 + (size_t)i * 4) = d;
+}
+
+// dW4[k][n] = fmaf chain over b of a4[b][k] dq[b][n]; db4[n] = sum over b of dq[b][n]; loss = (sum over b of h_b) / B.
+// Leading blocks of the fc1 backward launch (independent of its GEMM tiles).
+struct SideFc2 {
+  static constexpr int BLOCKS = 3;
+  const float* a4;
+  const uint8_t* act;
+  const float* gs;
+  const float* hs;
+  int B;
+  float* dw4;
+  float* db4;
+  float* loss;
+  __device__ void run(int blk, float*) const {
+    const int t = threadIdx.x;
+    if (blk < 2) {
+      const int k = blk * 256 + t;
+      float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 8
+      for (int b = 0; b < B; ++b) {
+        const float x = a4[(size_t)b * 512 + k];
+        const int a = act[b];
+        const float g = gs[b];
+        s0 = fmaf(x, a == 0 ? g : 0.0f, s0);
+        s1 = fmaf(x, a == 1 ? g : 0.0f, s1);
+        s2 = fmaf(x, a == 2 ? g : 0.0f, s2);
+      }
+      dw4[k * 3 + 0] = s0;
+      dw4[k * 3 + 1] = s1;
+      dw4[k * 3 + 2] = s2;
+    } else if (t < 3) {
+      float s = 0.0f;
+#pragma unroll 8
+      for (int b = 0; b < B; ++b) s = __fadd_rn(s, act[b] == t ? gs[b] : 0.0f);
+      db4[t] = s;
+    } else if (t == 3) {
+      float s = 0.0f;
+#pragma unroll 8
+      for (int b = 0; b < B; ++b) s = __fadd_rn(s, hs[b]);
+      *loss = s / (float)B;
+    }
+  }
+};
+
+// Conv weight gradients: dW = sum over sample chunks z in order of the chunk partials (t = 0; t = t + P_z), written into
+// the flat gradient.  Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32] with its rows (kh, c, kw)
+// mapped to HWIO (kh, kw, c).  The last row of each is the bias.
+struct WRed {
+  const float* slab[3];
+  int nz[3];
+  int count[3];   // (M + 1) * OC
+  int oc[3];
+  float* gw[3];   // W gradient
+  float* gb[3];   // b gradient
+};
+__global__ __launch_bounds__(256) void k_wreduce32(WRed R) {
+  int e = blockIdx.x * 256 + threadIdx.x;
+  int L = 0;
+  while (L < 3 && e >= R.count[L]) { e -= R.count[L]; ++L; }
+  if (L >= 3) return;
+  const float* p = R.slab[L] + e;
+  const size_t stride = (size_t)R.count[L];
+  const int nz = R.nz[L];
+  float t = 0.0f;
+  int z = 0;
+  for (; z + 8 <= nz; z += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[(size_t)(z + j) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t = __fadd_rn(t, v[j]);
+  }
+  for (; z < nz; ++z) t = __fadd_rn(t, p[(size_t)z * stride]);
+  const int oc = R.oc[L], m = e / oc, n = e - m * oc;
+  const int M = R.count[L] / oc - 1;
+  if (m == M) { R.gb[L][n] = t; return; }
+  int row = m;
+  if (L == 2) {   // conv1: (kh, c, kw) -> (kh, kw, c)
+    const int kh = m >> 5, c = (m >> 3) & 3, kw = m & 7;
+    row = (kh * 8 + kw) * 4 + c;
+  }
+  R.gw[L][(size_t)row * oc + n] = t;
+}
+
+// clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg;
+// lane chain t = fmaf(x, x, t) over i = tid, tid + 256, ...; wave xor butterfly (32, 16, .., 1); then
+// ((w0 + w1) + w2) + w3.  Norm_v = sum over its segments in order (k_adam32).
+constexpr int kNormSeg = 8192;
+struct NormArgs {
+  const float* g;
+  float scale;
+  float* partial;
+  int seg_first[kNumVars + 1];
+  int64_t off[kNumVars + 1];
+};
+__global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
+  __shared__ float wsum[4];
+  int v = 0;
+  while (v < kNumVars - 1 && (int)blockIdx.x >= A.seg_first[v + 1]) ++v;
+  const int j = blockIdx.x - A.seg_first[v];
+  const int64_t n = A.off[v + 1] - A.off[v];
+  const int64_t b = (int64_t)j * kNormSeg, e = std::min<int64_t>(n, b + kNormSeg);
+  const float* g = A.g + A.off[v];
+  float t = 0.0f;
+  for (int64_t i = b + threadIdx.x; i < e; i += 256) {
+    const float x = __fmul_rn(g[i], A.scale);
+    t = fmaf(x, x, t);
+  }
+  for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) A.partial[blockIdx.x] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]);
+}
+
+struct Adam32Args {
+  float* w;
+  float* m;
+  float* v;
+  const float* g;
+  const float* partial;
+  int seg_first[kNumVars + 1];
+  int64_t off[kNumVars + 1];
+  float* norms;
+  float scale, alpha, beta1, beta2, eps, clipnorm;
+};
+
+// tf.clip_by_norm + ResourceApplyAdam per element, explicit roundings in the oracle's order
+__device__ __forceinline__ float adam32_elem(float g, float scale, float clipnorm, float denom, float alpha, float beta1,
+                                             float beta2, float eps, float& m, float& v, float w) {
+  const float gc = __fmul_rn(__fmul_rn(g, scale), clipnorm) / denom;
+  m = __fadd_rn(m, __fmul_rn(__fsub_rn(gc, m), 1.0f - beta1));
+  v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(gc, gc), v), 1.0f - beta2));
+  return __fsub_rn(w, __fmul_rn(m, alpha) / __fadd_rn(sqrtf(v), eps));
+}
+
+__global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
+  __shared__ float nrm[kNumVars];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int v = wave; v < kNumVars; v += 4) {
+    const int first = A.seg_first[v], cnt = A.seg_first[v + 1] - first;
+    float t = 0.0f;
+    for (int c = 0; c < cnt; c += 64) {
+      const float x = c + lane < cnt ? A.partial[first + c + lane] : 0.0f;
+      const int m = cnt - c < 64 ? cnt - c : 64;
+      for (int j = 0; j < m; ++j)
+        t = __fadd_rn(t, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), j)));
+    }
+    if (lane == 0) {
+      nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
+      if (blockIdx.x == 0) A.norms[v] = nrm[v];
+    }
+  }
+  __syncthreads();
+  const int64_t count = A.off[kNumVars];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    int var = 0;
+    while (i >= A.off[var + 1]) ++var;
+    const float denom = fmaxf(nrm[var], A.clipnorm);
+    float m = A.m[i], v = A.v[i];
+    A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
+    A.m[i] = m;
+    A.v[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// host side
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
+using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3>;
+using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
+using PConv1WgradT = PConv1Wgrad<kSC1>;
+
+static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
+
+void f32_workspace(qlx_model* m, int B) {
+  if (B <= m->ws_batch) return;
+  QLX_HIP(hipStreamSynchronize(m->stream));
+  if (m->ws) (void)hipFree(m->ws);
+  m->ws = nullptr;
+  ModelWs& w = m->w;
+  const int C = std::min(B, kF32FwdChunk);   // conv activations are held per forward chunk
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off = align_up(off + bytes, 256); return o; };
+  const size_t o_frames = take((size_t)B * 4 * kFramePix);
+  const size_t o_table = take((size_t)B * 4 * sizeof(void*));
+  const size_t o_a1 = take((size_t)C * 12800 * 4), o_a2 = take((size_t)C * 5184 * 4), o_a3 = take((size_t)C * 3136 * 4);
+  const size_t o_a4 = take((size_t)B * 512 * 4), o_q = take((size_t)B * 3 * 4);
+  const size_t o_gs = take((size_t)B * 4), o_hs = take((size_t)B * 4), o_y = take((size_t)B * 4);
+  const size_t o_act = take((size_t)B), o_argmax = take((size_t)B), o_rew = take((size_t)B * 4), o_done = take((size_t)B);
+  int nseg = 0;
+  for (int v = 0; v < kNumVars; ++v) nseg += segs_of(v);
+  const size_t o_part = take((size_t)nseg * 4);
+  const size_t o_loss = take(64);
+  QLX_HIP(hipMalloc(&m->ws, off));
+  char* base = (char*)m->ws;
+  w.frames = (uint8_t*)(base + o_frames);
+  w.table = (const uint8_t**)(base + o_table);
+  w.fa1 = (float*)(base + o_a1); w.fa2 = (float*)(base + o_a2); w.fa3 = (float*)(base + o_a3); w.fa4 = (float*)(base + o_a4);
+  w.q = (float*)(base + o_q);
+  w.gs = (float*)(base + o_gs); w.hs = (float*)(base + o_hs); w.y = (float*)(base + o_y);
+  w.act = (uint8_t*)(base + o_act); w.argmax = (uint8_t*)(base + o_argmax); w.rew = (float*)(base + o_rew);
+  w.done = (uint8_t*)(base + o_done);
+  w.fpart = (float*)(base + o_part);
+  w.loss = (float*)(base + o_loss);
+  w.fchunk = C;
+  m->ws_batch = B;
+}
+
+// gradient workspace (dz buffers, weight-gradient slabs) for training batches up to B (<= the forward chunk)
+static void f32_grad_workspace(qlx_model* m, int B) {
+  ModelWs& w = m->w;
+  if (B <= w.fgrad_batch) return;
+  QLX_HIP(hipStreamSynchronize(m->stream));
+  if (w.fgrad) (void)hipFree(w.fgrad);
+  w.fgrad = nullptr;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off = align_up(off + bytes, 256); return o; };
+  const size_t o_dz1 = take((size_t)B * 12800 * 4), o_dz2 = take((size_t)B * 5184 * 4), o_dz3 = take((size_t)B * 3136 * 4);
+  const size_t o_dz4 = take((size_t)B * 512 * 4);
+  const size_t o_s1 = take((size_t)((B + kSC1 - 1) / kSC1) * 257 * 32 * 4);
+  const size_t o_s2 = take((size_t)((B + kSC2 - 1) / kSC2) * 513 * 64 * 4);
+  const size_t o_s3 = take((size_t)((B + kSC3 - 1) / kSC3) * 577 * 64 * 4);
+  void* p = nullptr;
+  QLX_HIP(hipMalloc(&p, off));
+  w.fgrad = p;
+  char* base = (char*)p;
+  w.fdz1 = (float*)(base + o_dz1); w.fdz2 = (float*)(base + o_dz2); w.fdz3 = (float*)(base + o_dz3);
+  w.fdz4 = (float*)(base + o_dz4);
+  w.fslab1 = (float*)(base + o_s1); w.fslab2 = (float*)(base + o_s2); w.fslab3 = (float*)(base + o_s3);
+  w.fgrad_batch = B;
+}
+
+template <class P>
+static void launch(const P& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), s, p);
+  QLX_HIP(hipGetLastError());
+}
+
+template <class P1, class P2, class S>
+static void launch_pair(const P1& p1, const P2& p2, const S& side, hipStream_t s) {
+  const size_t lds = std::max(gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>());
+  hipLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, p1, p2,
+                     side);
+  QLX_HIP(hipGetLastError());
+}
+
+static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
+
+// forward over B samples in chunks of the workspace's forward chunk: a1..a3 hold the last chunk (the whole batch when
+// B <= chunk, as training needs), a4 all B samples
+void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+  ModelWs& w = m->w;
+  QLX_CHECK(m->ws_batch >= B, QLX_E_STATE, "f32 forward: workspace too small");
+  m->last_batch = B;
+  const float* p = m->d_params;
+  for (int c0 = 0; c0 < B; c0 += w.fchunk) {
+    const int n = std::min(w.fchunk, B - c0);
+    {
+      ProfScope ps(m->prof, "f32_conv1_fwd", s, 2.0 * n * 400 * 32 * 256);
+      PConv1Fwd P{grid(n * 400, PConv1Fwd::BM, 32, 32, 1), table + (size_t)c0 * 4, p + voff(0), p + voff(1), w.fa1, n * 400};
+      launch(P, s);
+    }
+    {
+      ProfScope ps(m->prof, "f32_conv2_fwd", s, 2.0 * n * 81 * 64 * 512);
+      PConv2Fwd P{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81};
+      launch(P, s);
+    }
+    {
+      ProfScope ps(m->prof, "f32_conv3_fwd", s, 2.0 * n * 49 * 64 * 576);
+      PConv3Fwd P{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49};
+      launch(P, s);
+    }
+    {
+      ProfScope ps(m->prof, "f32_fc1_fwd", s, 2.0 * n * 3136 * 512);
+      PFc1Fwd P{grid(n, PFc1Fwd::BM, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n};
+      launch(P, s);
+    }
+  }
+}
+
+void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s) {
+  const dim3 g((B + 255) / 256), blk(256);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(k_head32<0>, g, blk, 0, s, a); break;
+    case 1: hipLaunchKernelGGL(k_head32<1>, g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_head32<2>, g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_head32<3>, g, blk, 0, s, a); break;
+  }
+  QLX_HIP(hipGetLastError());
+}
+
+void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
+                        const float* weights, float* td_abs) {
+  QLX_CHECK(B <= m->w.fchunk && B == m->last_batch, QLX_E_STATE, "f32 backward: batch must follow its forward");
+  f32_grad_workspace(m, B);
+  ModelWs& w = m->w;
+  float* G = m->d_grads;
+  const float* p = m->d_params;
+  {
+    ProfScope ps(m->prof, "f32_head", s);
+    Fc2Args a = fc2_args(m, B);
+    a.actions = actions;
+    a.y = y;
+    a.gsample = w.gs;
+    a.hsample = w.hs;
+    a.weights = weights;
+    a.td_abs = td_abs;
+    f32_head(3, a, B, s);
+    hipLaunchKernelGGL(k_dz4_32, dim3((B * 128 + 255) / 256), dim3(256), 0, s, w.fa4, p + voff(8), actions, w.gs, B, w.fdz4);
+    QLX_HIP(hipGetLastError());
+  }
+  {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its three leading blocks
+    ProfScope ps(m->prof, "f32_fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
+    PFc1Wgrad Pw{grid(3136, 64, 512, 64, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
+    PFc1Dgrad Pd{grid(B, 64, 3136, 64, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
+    SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
+    launch_pair(Pw, Pd, S, s);
+  }
+}
+
+void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+  ModelWs& w = m->w;
+  const float* p = m->d_params;
+  float* G = m->d_grads;
+  const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
+  {  // conv3: dz2 tiles + weight-gradient chunk tiles
+    ProfScope ps(m->prof, "f32_conv3_bwd", s, 2.0 * 2.0 * B * 49 * 64 * 576);
+    PConv3Dgrad Pd{grid(B * 81, 64, 64, 64, 1), w.fdz3, p + voff(4), w.fa2, w.fdz2, B * 81};
+    PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
+    launch_pair(Pw, Pd, NoSide{}, s);
+  }
+  {  // conv2: dz1 tiles (4 parity classes) + weight-gradient chunk tiles
+    ProfScope ps(m->prof, "f32_conv2_bwd", s, 2.0 * B * 81 * 64 * 512 + 2.0 * B * 400 * 32 * 256);
+    PConv2Dgrad Pd{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), w.fdz2, p + voff(2), w.fa1, w.fdz1, B * 100};
+    PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
+    launch_pair(Pw, Pd, NoSide{}, s);
+  }
+  {
+    ProfScope ps(m->prof, "f32_conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
+    PConv1WgradT P{grid(256, PConv1WgradT::BM, 32, 32, z1), table, w.fdz1, w.fslab1, B};
+    launch(P, s);
+  }
+  {
+    ProfScope ps(m->prof, "f32_wgrad_reduce", s);
+    WRed R;
+    R.slab[0] = w.fslab3; R.nz[0] = z3; R.count[0] = 577 * 64; R.oc[0] = 64; R.gw[0] = G + voff(4); R.gb[0] = G + voff(5);
+    R.slab[1] = w.fslab2; R.nz[1] = z2; R.count[1] = 513 * 64; R.oc[1] = 64; R.gw[1] = G + voff(2); R.gb[1] = G + voff(3);
+    R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
+    const int total = R.count[0] + R.count[1] + R.count[2];
+    hipLaunchKernelGGL(k_wreduce32, dim3((total + 255) / 256), dim3(256), 0, s, R);
+    QLX_HIP(hipGetLastError());
+  }
+}
+
+static void seg_tables(int* seg_first, int64_t* off) {
+  int sf = 0;
+  int64_t o = 0;
+  for (int v = 0; v < kNumVars; ++v) {
+    seg_first[v] = sf;
+    off[v] = o;
+    sf += segs_of(v);
+    o += kVarSize[v];
+  }
+  seg_first[kNumVars] = sf;
+  off[kNumVars] = o;
+}
+
+void f32_norms(qlx_model* m, hipStream_t s, float scale) {
+  ProfScope ps(m->prof, "f32_norms", s, 4.0 * kNumParams);
+  NormArgs A;
+  A.g = m->d_grads;
+  A.scale = scale;
+  A.partial = m->w.fpart;
+  seg_tables(A.seg_first, A.off);
+  hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
+  QLX_HIP(hipGetLastError());
+}
+
+void f32_adam(qlx_model* m, hipStream_t s, float scale) {
+  const int64_t t = m->iterations + 1;
+  const float tf = (float)t;
+  const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
+  Adam32Args a;
+  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.partial = m->w.fpart; a.norms = m->d_norms;
+  seg_tables(a.seg_first, a.off);
+  a.scale = scale;
+  a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
+  a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
+  ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
+  hipLaunchKernelGGL(k_adam32, dim3(2048), dim3(256), 0, s, a);
+  QLX_HIP(hipGetLastError());
+  m->iterations = t;
+}
+
+}  // namespace qlx

@@ -1,0 +1,510 @@
+// fp32 Nature-DQN kernels for gfx950: the reference's arithmetic (Keras float32 graph,
+// create_ql_model_breakout_84x84x4_3_32.py:20-33,37-61) on v_mfma_f32_16x16x4_f32.
+//
+// Every GEMM-shaped op is one LDS-tiled implicit-GEMM kernel (gemm_body) driven by a per-layer operand policy.
+// v_mfma_f32_16x16x4_f32 is bit-for-bit a k-ordered fmaf chain over its four k (lane group 0 first; measured on
+// MI355X, scripts/mfma_f32_probe.hip), and each output element keeps ONE accumulator over the whole reduction,
+// consumed in ascending k.  So every output is exactly
+//     acc = 0; for k in the layer's order: acc = fmaf(x_k, w_k, acc)
+// in the order DESIGN.md §6 defines per layer (and oracle/qnet32_ref.cpp restates): the fp32 Q-net is
+// bit-exact against the CPU oracle.  The only reductions split across blocks are the conv weight gradients
+// (sample chunks of a fixed size, partials summed in chunk order) and the clip_by_norm sums of squares.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qlx_internal.h"
+
+namespace qlx {
+namespace q32 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;   // reduction depth staged per LDS slab
+
+// Operand tile in LDS.  RMAJ: t[row][k] (pitch BK + 4: the 16 rows x 4 k of a fragment read hit 64 distinct
+// banks); KMAJ: t[k][row] (pitch = rows padded to 16 mod 64, same property).  Writes are 16-byte float4 along the
+// operand's contiguous source dimension.
+__host__ __device__ constexpr int kmaj_pitch(int rows) { return rows + (((16 - rows % 64) % 64) + 64) % 64; }
+
+template <int ROWS, bool KMAJ>
+struct Opnd {
+  static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS) : BK + 4;
+  static constexpr int FLOATS = KMAJ ? BK * PITCH : ROWS * PITCH;
+  static constexpr int F4 = ROWS * BK / 4;   // float4 per slab
+  __device__ static void coord(int idx, int& row, int& k) {
+    if (KMAJ) { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
+    else { row = idx >> 3; k = (idx & 7) * 4; }
+  }
+  __device__ static void put(float* t, int row, int k, f32x4 v) {
+    *reinterpret_cast<f32x4*>(t + (KMAJ ? k * PITCH + row : row * PITCH + k)) = v;
+  }
+  __device__ static float at(const float* t, int row, int k) { return KMAJ ? t[k * PITCH + row] : t[row * PITCH + k]; }
+  // MFMA 16x16x4 operand of the 16 rows from r0, k step kk: lane l holds (r0 + (l & 15), 4 kk + (l >> 4))
+  __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & 15), 4 * kk + (lane >> 4)); }
+};
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 u8x4(uint32_t w) {
+  return f32x4{(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu), (float)((w >> 16) & 0xFFu), (float)(w >> 24)};
+}
+__device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
+
+// workgroup barrier ordering LDS only (keeps register prefetches in flight)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// XCD-aware block order: hardware block b runs on XCD b % 8; logical blocks [x * G / 8, ...) are all given to XCD x,
+// so consecutive logical tiles (neighbouring im2col rows, the tiles of one weight-gradient chunk) share an L2.
+__device__ __forceinline__ int xcd_logical(int b, int G) {
+  const int x = b & 7, i = b >> 3, q = G >> 3, r = G & 7;
+  return x * q + (x < r ? x : r) + i;
+}
+
+// One output tile of a policy P (see the policies below for the members it provides):
+//   acc[row][col] = sum over the slabs s = 0 .. nslabs(z) - 1 and k = 0 .. 31 of A(z, s, row, k) * B(z, s, col, k),
+// one fmaf chain per output in (s, k) order; then P::epi stores it.  With P::BIAS the tiles of row-tile 0 also
+// sum B's column over the same order (bias gradient = the all-ones row of A).
+template <class P>
+__device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
+  using OA = Opnd<P::BM, P::A_KMAJ>;
+  using OB = Opnd<P::BN, P::B_KMAJ>;
+  constexpr int T = P::WM * P::WN * 64;
+  constexpr int TM = P::BM / (P::WM * 16), TN = P::BN / (P::WN * 16);
+  static_assert(TM * P::WM * 16 == P::BM && TN * P::WN * 16 == P::BN, "tile shape");
+  constexpr int NA = (OA::F4 + T - 1) / T, NB = (OB::F4 + T - 1) / T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % P::WM, wn = wave / P::WM;
+  int tm, tn, z;
+  p.decode(lb, tm, tn, z);
+  const int row0 = tm * P::BM, col0 = tn * P::BN;
+  const int ns = p.nslabs(z);
+  float* As0 = lds;
+  float* As1 = lds + OA::FLOATS;
+  float* Bs0 = lds + 2 * OA::FLOATS;
+  float* Bs1 = Bs0 + OB::FLOATS;
+  f32x4 ra[NA], rb[NB];
+  auto load = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T;
+      if (OA::F4 % T == 0 || idx < OA::F4) {
+        int r, k;
+        OA::coord(idx, r, k);
+        ra[i] = p.ldA(z, s, row0 + r, k);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + i * T;
+      if (OB::F4 % T == 0 || idx < OB::F4) {
+        int r, k;
+        OB::coord(idx, r, k);
+        rb[i] = p.ldB(z, s, col0 + r, k);
+      }
+    }
+  };
+  auto store = [&](float* as, float* bs) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T;
+      if (OA::F4 % T == 0 || idx < OA::F4) {
+        int r, k;
+        OA::coord(idx, r, k);
+        OA::put(as, r, k, ra[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + i * T;
+      if (OB::F4 % T == 0 || idx < OB::F4) {
+        int r, k;
+        OB::coord(idx, r, k);
+        OB::put(bs, r, k, rb[i]);
+      }
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  float bsum = 0.0f;
+  const bool do_bias = P::BIAS && tm == 0 && tid < P::BN;
+  if (ns > 0) {
+    load(0);
+    store(As0, Bs0);
+  }
+  lds_barrier();
+  for (int s = 0; s < ns; ++s) {
+    const bool next = s + 1 < ns;
+    if (next) load(s + 1);
+    const float* a = (s & 1) ? As1 : As0;
+    const float* b = (s & 1) ? Bs1 : Bs0;
+    if (P::BIAS && do_bias)
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) bsum = bsum + OB::at(b, tid, k);
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (next) store((s & 1) ? As0 : As1, (s & 1) ? Bs0 : Bs1);
+    lds_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
+  if constexpr (P::BIAS) {
+    if (do_bias) p.epi_bias(z, col0 + tid, bsum);
+  }
+}
+
+template <class P>
+constexpr size_t gemm_lds_bytes() {
+  return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ>::FLOATS + Opnd<P::BN, P::B_KMAJ>::FLOATS) * sizeof(float);
+}
+
+// grid layout shared by the policies: tile index fastest (col tile, then row tile), then z
+struct Grid {
+  int tiles_m, tiles_n, nz;
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const {
+    tn = lb % tiles_n;
+    const int q = lb / tiles_n;
+    tm = q % tiles_m;
+    z = q / tiles_m;
+  }
+  __host__ __device__ int blocks() const { return tiles_m * tiles_n * nz; }
+};
+
+template <class P>
+__global__ __launch_bounds__(256) void k_gemm32(const P p) {
+  extern __shared__ float lds[];
+  gemm_body(p, xcd_logical(blockIdx.x, gridDim.x), lds);
+}
+
+// two independent GEMMs in one grid (logical blocks [0, G1) run P1), plus `side` leading blocks running S
+template <class P1, class P2, class S>
+__global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, const S side) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  if (b < S::BLOCKS) { side.run(b, lds); return; }
+  const int G = gridDim.x - S::BLOCKS;
+  const int lb = xcd_logical(b - S::BLOCKS, G);
+  const int g1 = p1.g.blocks();
+  if (lb < g1) gemm_body(p1, lb, lds);
+  else gemm_body(p2, lb - g1, lds);
+}
+
+struct NoSide {
+  static constexpr int BLOCKS = 0;
+  __device__ void run(int, float*) const {}
+};
+
+// ---------------------------------------------------------------------------------------------------------------
+// Layer policies.  Chain orders (oracle/qnet32_ref.cpp):
+//   conv1 forward   k = (kh, c, kw)            conv2 / conv3 forward  k = (kh, kw, c)      fc1 forward k = h, w, c
+//   conv dgrad      k = (kh, kw, oc) over the valid taps                                   fc1 dgrad   k = n
+//   weight grads    r = (b, oh, ow) ascending inside a sample chunk; fc1 / fc2 over b ascending, no chunks
+
+// conv1 forward: frames (u8, s2d layout, table[b * 4 + slot]) -> a1 [B][20][20][32] = relu(z + b0).
+// Slab s = kh; k = c * 8 + kw.  A row (b, oh, ow): 4 pixels kw = 4h .. 4h+3 of slot c are one aligned u32.
+struct PConv1Fwd {
+  static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
+  static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
+  Grid g;
+  const uint8_t* const* table;
+  const float* w0;   // [8][8][4][32] HWIO
+  const float* b0;
+  float* a1;
+  int M;             // B * 400
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return 8; }
+  __device__ f32x4 ldA(int, int kh, int row, int k) const {
+    if (row >= M) return zero4();
+    const int b = row / 400, p = row - b * 400, oh = p / 20, ow = p - oh * 20;
+    const int c = k >> 3, h = (k >> 2) & 1;
+    const uint8_t* f = table[b * 4 + c];
+    return u8x4(*reinterpret_cast<const uint32_t*>(f + ((oh + (kh >> 2)) * kBlocks + ow + h) * 16 + (kh & 3) * 4));
+  }
+  __device__ f32x4 ldB(int, int kh, int col, int k) const {   // W0[kh][kw][c][oc], k = c * 8 + kw
+    const int c = k >> 3, kw = k & 7;
+    return ld4(w0 + ((kh * 8 + kw) * 4 + c) * 32 + col);
+  }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) a1[(size_t)(row + r) * 32 + col] = relu(v[r] + b0[col]);
+  }
+};
+
+// conv2 / conv3 forward on fp32 NHWC input: out = relu(conv + bias); slab s: tap = 32 s / C, c0 = 32 s % C
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC>
+struct PConvFwd {
+  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
+  Grid g;
+  const float* in;
+  const float* w;    // [KS][KS][C][OC]
+  const float* bias;
+  float* out;        // [M][OC]
+  int M;             // B * OH * OW
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return KS * KS * C / BK; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const {
+    if (row >= M) return zero4();
+    const int tap = (s * BK) / C, c0 = (s * BK) % C, kh = tap / KS, kw = tap % KS;
+    const int b = row / (OH * OW), p = row - b * (OH * OW), oh = p / OW, ow = p - oh * OW;
+    return ld4(in + ((size_t)(b * H + oh * S + kh) * W + ow * S + kw) * C + c0 + k);
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w + (size_t)(s * BK + k) * OC + col); }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) out[(size_t)(row + r) * OC + col] = relu(v[r] + bias[col]);
+  }
+};
+using PConv2Fwd = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>;
+using PConv3Fwd = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>;
+
+// fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3)
+struct PFc1Fwd {
+  static constexpr int BM = 32, BN = 64, WM = 2, WN = 2;
+  static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
+  Grid g;
+  const float* a3;
+  const float* w3;
+  const float* b3;
+  float* a4;
+  int M;
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return 3136 / BK; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const {
+    return row < M ? ld4(a3 + (size_t)row * 3136 + s * BK + k) : zero4();
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w3 + (size_t)(s * BK + k) * 512 + col); }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) a4[(size_t)(row + r) * 512 + col] = relu(v[r] + b3[col]);
+  }
+};
+
+// fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
+struct PFc1Dgrad {
+  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
+  Grid g;
+  const float* dz4;
+  const float* w3;
+  const float* a3;
+  float* dz3;
+  int M;
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return 512 / BK; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const {
+    return row < M ? ld4(dz4 + (size_t)row * 512 + s * BK + k) : zero4();
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w3 + (size_t)col * 512 + s * BK + k); }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) {
+        const size_t o = (size_t)(row + r) * 3136 + col;
+        dz3[o] = a3[o] > 0.0f ? v[r] : 0.0f;
+      }
+  }
+};
+
+// fc1 weight gradient: dW3 [3136][512] = a3^T dz4 over b ascending; db3 = column sums of dz4 (row-tile 0 blocks)
+struct PFc1Wgrad {
+  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
+  Grid g;
+  const float* a3;
+  const float* dz4;
+  float* dw3;
+  float* db3;
+  int B;
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return (B + BK - 1) / BK; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const {
+    const int b = s * BK + k;
+    return (b < B && row < 3136) ? ld4(a3 + (size_t)b * 3136 + row) : zero4();
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const {
+    const int b = s * BK + k;
+    return b < B ? ld4(dz4 + (size_t)b * 512 + col) : zero4();
+  }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < 3136) dw3[(size_t)(row + r) * 512 + col] = v[r];
+  }
+  __device__ void epi_bias(int, int col, float v) const { db3[col] = v; }
+};
+
+// conv3 backward-data: dz2 [B][9][9][64] = convT(dz3, W2) * (a2 > 0); rows (b, ih, iw), k = (kh, kw, oc)
+struct PConv3Dgrad {
+  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
+  Grid g;
+  const float* dz3;   // [B][7][7][64]
+  const float* w2;    // [3][3][64][64]
+  const float* a2;
+  float* dz2;
+  int M;              // B * 81
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return 18; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const {
+    if (row >= M) return zero4();
+    const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3, oc0 = (s & 1) * 32;
+    const int b = row / 81, p = row - b * 81, ih = p / 9, iw = p - ih * 9;
+    const int oh = ih - kh, ow = iw - kw;
+    if (oh < 0 || oh >= 7 || ow < 0 || ow >= 7) return zero4();
+    return ld4(dz3 + ((size_t)(b * 7 + oh) * 7 + ow) * 64 + oc0 + k);
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const {   // W2[kh][kw][c = col][oc]
+    return ld4(w2 + ((size_t)(s >> 1) * 64 + col) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) {
+        const size_t o = (size_t)(row + r) * 64 + col;
+        dz2[o] = a2[o] > 0.0f ? v[r] : 0.0f;
+      }
+  }
+};
+
+// conv2 backward-data by output parity class z = (py, px): rows (b, i, j) with ih = 2 i + py, iw = 2 j + px
+// (10 x 10 per class); taps t = (th, tw): kh = py + 2 th, kw = px + 2 tw, source dz2[b][i - th][j - tw];
+// k = (t, oc): the valid taps of the lexicographic (kh, kw, oc) order
+struct PConv2Dgrad {
+  static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
+  Grid g;
+  const float* dz2;   // [B][9][9][64]
+  const float* w1;    // [4][4][32][64]
+  const float* a1;
+  float* dz1;         // [B][20][20][32]
+  int M;              // B * 100
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int nslabs(int) const { return 8; }
+  __device__ f32x4 ldA(int z, int s, int row, int k) const {
+    if (row >= M) return zero4();
+    const int t = s >> 1, th = t >> 1, tw = t & 1, oc0 = (s & 1) * 32;
+    const int b = row / 100, p = row - b * 100, i = p / 10, j = p - i * 10;
+    const int oh = i - th, ow = j - tw;
+    if (oh < 0 || oh >= 9 || ow < 0 || ow >= 9) return zero4();
+    (void)z;
+    return ld4(dz2 + ((size_t)(b * 9 + oh) * 9 + ow) * 64 + oc0 + k);
+  }
+  __device__ f32x4 ldB(int z, int s, int col, int k) const {   // W1[kh][kw][c = col][oc]
+    const int t = s >> 1, kh = (z >> 1) + 2 * (t >> 1), kw = (z & 1) + 2 * (t & 1);
+    return ld4(w1 + ((size_t)(kh * 4 + kw) * 32 + col) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ void epi(int z, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) {
+        const int rr = row + r, b = rr / 100, p = rr - b * 100, i = p / 10, j = p - i * 10;
+        const int ih = 2 * i + (z >> 1), iw = 2 * j + (z & 1);
+        const size_t o = ((size_t)(b * 20 + ih) * 20 + iw) * 32 + col;
+        dz1[o] = a1[o] > 0.0f ? v[r] : 0.0f;
+      }
+  }
+};
+
+// conv2 / conv3 weight gradient over sample chunk z (samples [z SC, min(B, (z + 1) SC))): rows m = (kh, kw, c),
+// cols oc, r = (b, oh, ow) ascending; partial slab[z][M + 1][OC] (row M = bias partial)
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC>
+struct PConvWgrad {
+  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
+  static constexpr int MROWS = KS * KS * C, P = OH * OW, CHUNK = SC;
+  Grid g;
+  const float* in;
+  const float* dz;   // [B][OH][OW][OC]
+  float* slab;
+  int B;
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int rows_in(int z) const {
+    const int b0 = z * SC, b1 = b0 + SC < B ? b0 + SC : B;
+    return (b1 - b0) * P;
+  }
+  __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
+  __device__ f32x4 ldA(int z, int s, int row, int k) const {
+    const int r = s * BK + k;
+    if (r >= rows_in(z)) return zero4();
+    const int tap = row / C, c = row - tap * C, kh = tap / KS, kw = tap - kh * KS;
+    const int bl = r / P, p = r - bl * P, oh = p / OW, ow = p - oh * OW, b = z * SC + bl;
+    return ld4(in + ((size_t)(b * H + oh * S + kh) * W + ow * S + kw) * C + c);
+  }
+  __device__ f32x4 ldB(int z, int s, int col, int k) const {
+    const int r = s * BK + k;
+    if (r >= rows_in(z)) return zero4();
+    return ld4(dz + ((size_t)z * SC * P + r) * OC + col);
+  }
+  __device__ void epi(int z, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[((size_t)z * (MROWS + 1) + row + r) * OC + col] = v[r];
+  }
+  __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * OC + col] = v; }
+};
+
+// conv1 weight gradient over sample chunk z: rows m = (kh, c, kw) (the forward's k order), cols oc, r = (b, oh, ow);
+// A (frames) is 4 consecutive kw per aligned u32.  The slab reduction maps m back to HWIO.
+template <int SC>
+struct PConv1Wgrad {
+  static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
+  static constexpr int MROWS = 256, P = 400, CHUNK = SC;
+  Grid g;
+  const uint8_t* const* table;
+  const float* dz1;   // [B][20][20][32]
+  float* slab;
+  int B;
+  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __device__ int rows_in(int z) const {
+    const int b0 = z * SC, b1 = b0 + SC < B ? b0 + SC : B;
+    return (b1 - b0) * P;
+  }
+  __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
+  __device__ f32x4 ldA(int z, int s, int row, int k) const {
+    const int r = s * BK + k;
+    if (r >= rows_in(z)) return zero4();
+    const int kh = row >> 5, c = (row >> 3) & 3, h = (row >> 2) & 1;
+    const int bl = r / P, p = r - bl * P, oh = p / 20, ow = p - oh * 20, b = z * SC + bl;
+    const uint8_t* f = table[b * 4 + c];
+    return u8x4(*reinterpret_cast<const uint32_t*>(f + ((oh + (kh >> 2)) * kBlocks + ow + h) * 16 + (kh & 3) * 4));
+  }
+  __device__ f32x4 ldB(int z, int s, int col, int k) const {
+    const int r = s * BK + k;
+    if (r >= rows_in(z)) return zero4();
+    return ld4(dz1 + ((size_t)z * SC * P + r) * 32 + col);
+  }
+  __device__ void epi(int z, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[((size_t)z * (MROWS + 1) + row + r) * 32 + col] = v[r];
+  }
+  __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * 32 + col] = v; }
+};
+
+}  // namespace q32
+}  // namespace qlx

@@ -66,11 +66,17 @@ class Params(C.Structure):
         ("per_alpha", C.c_float),
         ("per_beta", C.c_float),
         ("per_eps", C.c_float),
-        ("pad2", C.c_uint32),
+        ("qnet_precision", C.c_uint32),
+        ("stats_after_steps", C.c_uint64),
+        ("checkpoint_file", C.c_char * 256),
     ]
 
 DOUBLE_DQN = 1
 PER = 2
+PREC_F32 = 0    # QLX_PREC_F32: the reference's fp32 arithmetic (bit-exact against the oracle)
+PREC_BF16 = 1   # QLX_PREC_BF16: bf16 MFMA operands, fp32 accumulation (the labelled fast path)
+ARCH_F32 = 1    # QLX_ARCH_NATURE_DQN
+ARCH_BF16 = 2   # QLX_ARCH_NATURE_DQN_BF16
 
 
 class LearnerStats(C.Structure):
@@ -85,8 +91,11 @@ def Parameter(**kw):
                epsilon_greedy_steps=1_000_000.0, max_steps_per_episode=10_000, epsilon_pure_random_steps=50_000,
                history_buffer_len=1_000_000, update_after_actions=4, target_sync_steps=0,
                episode_reward_history_buffer_len=100, n_envs=1, batch_size=32, env_seed=0x51A5EED, learner_seed=1,
-               init_seed=2, rank=0, flags=0, per_alpha=0.6, per_beta=0.4, per_eps=1e-6, pad2=0)
+               init_seed=2, rank=0, flags=0, per_alpha=0.6, per_beta=0.4, per_eps=1e-6, qnet_precision=PREC_F32,
+               stats_after_steps=25_000, checkpoint_file=b"")
     for k, v in kw.items():
+        if k == "checkpoint_file" and isinstance(v, str):
+            v = v.encode()
         setattr(p, k, v)
     return p
 
@@ -128,6 +137,9 @@ def lib():
         "qlx_params_default": ([vp], None),
         "qlx_learner_create": ([C.POINTER(Params), i32, C.POINTER(vp)], i32), "qlx_learner_destroy": ([vp], i32),
         "qlx_learner_vector_step": ([vp], i32), "qlx_learner_run": ([vp, u64], i32), "qlx_learner_sync": ([vp], i32),
+        "qlx_learner_prefill": ([vp, u64], i32), "qlx_learner_stats_events": ([vp], u64),
+        "qlx_learner_learn_till_mastered": ([vp, u64, C.POINTER(u64)], i32),
+        "qlx_learner_last_log": ([vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)], i32),
         "qlx_learner_stats_get": ([vp, C.POINTER(LearnerStats)], i32),
         "qlx_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_learner_env": ([vp], vp), "qlx_learner_replay": ([vp], vp), "qlx_learner_model": ([vp, i32], vp),
@@ -337,13 +349,14 @@ class ReplayBuffer:
 
 
 class DeepQLearningModel:
-    """Nature-DQN on MI355X: bf16 MFMA contractions, fp32 accumulation and fp32 master weights."""
+    """Nature-DQN on MI355X: fp32 (the reference's arithmetic, fp32 MFMA, bit-exact against the oracle) or, with
+    precision=PREC_BF16, bf16 MFMA operands with fp32 accumulation and fp32 master weights."""
 
-    def __init__(self, seed=2, device=0, handle=None):
+    def __init__(self, seed=2, device=0, handle=None, precision=PREC_F32):
         self._owned = handle is None
         if handle is None:
             h = C.c_void_p()
-            _check(lib().qlx_model_create(1, seed, device, C.byref(h)))
+            _check(lib().qlx_model_create(ARCH_BF16 if precision == PREC_BF16 else ARCH_F32, seed, device, C.byref(h)))
             handle = h.value
         self.h = handle
 
@@ -453,6 +466,21 @@ class SelfDrivingQLearner(_LearningStats):
 
     def run(self, n):
         _check(lib().qlx_learner_run(self.h, n))
+
+    def prefill(self, n):
+        """n vector steps without updates (replay fill before a measurement / parity check)"""
+        _check(lib().qlx_learner_prefill(self.h, n))
+
+    def learn_till_mastered(self, max_vector_steps):
+        n = C.c_uint64()
+        _check(lib().qlx_learner_learn_till_mastered(self.h, max_vector_steps, C.byref(n)))
+        return n.value
+
+    def stats_events(self):
+        return int(lib().qlx_learner_stats_events(self.h))
+
+    def last_log(self):
+        return _text(lib().qlx_learner_last_log, self.h)
 
     def sync(self):
         _check(lib().qlx_learner_sync(self.h))

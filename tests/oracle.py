@@ -45,7 +45,9 @@ class LearnerParams(C.Structure):
         ("per_alpha", C.c_float),
         ("per_beta", C.c_float),
         ("per_eps", C.c_float),
-        ("pad2", C.c_uint32),
+        ("qnet_precision", C.c_uint32),
+        ("stats_after_steps", C.c_uint64),
+        ("checkpoint_file", C.c_char * 256),
     ]
 
 
@@ -59,7 +61,7 @@ def default_params(**kw):
                       epsilon_pure_random_steps=50_000, history_buffer_len=1_000_000, update_after_actions=4,
                       target_sync_steps=0, episode_reward_history_buffer_len=100, n_envs=1, batch_size=32,
                       env_seed=0x51A5EED, learner_seed=1, init_seed=2, rank=0, flags=0, per_alpha=0.6,
-                      per_beta=0.4, per_eps=1e-6, pad2=0)
+                      per_beta=0.4, per_eps=1e-6, qnet_precision=0, stats_after_steps=25_000, checkpoint_file=b"")
     for k, v in kw.items():
         setattr(p, k, v)
     return p
@@ -126,6 +128,12 @@ def lib():
         L.orc_qnet_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.orc_qnet_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
         L.orc_qnet_train.restype = f32
+        L.orc_qnet32_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+        L.orc_qnet32_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
+        L.orc_qnet32_train.restype = f32
+        L.orc_learner_prefill.argtypes = [vp, u64]
+        L.orc_learner_stats_events.argtypes = [vp]
+        L.orc_learner_stats_events.restype = u64
         L.orc_learner_new.argtypes = [C.POINTER(LearnerParams)]
         L.orc_learner_new.restype = vp
         L.orc_learner_free.argtypes = [vp]
@@ -273,7 +281,12 @@ def envs_run(env_seed, n_envs, n_steps, action_seed, max_steps=10_000, want_tens
 
 
 class QNet:
-    def __init__(self, seed=2, handle=None, owned=True):
+    """Q-net restatement.  f32=True: the fp32 arithmetic of QLX_ARCH_NATURE_DQN (oracle/qnet32_ref.cpp, every
+    reduction one fmaf chain in the build's order: the product matches it bit for bit); f32=False: the
+    double-accumulating restatement (oracle/qnet_ref.cpp) the bf16 product is held to within stated tolerances."""
+
+    def __init__(self, seed=2, handle=None, owned=True, f32=False):
+        self.f32 = f32
         self.owned = handle is None and owned
         self.h = handle if handle is not None else lib().orc_qnet_new(seed)
 
@@ -315,7 +328,8 @@ class QNet:
         q = np.zeros((B, 3), dtype=np.float32)
         a = [np.zeros((B, 20, 20, 32), np.float32), np.zeros((B, 9, 9, 64), np.float32),
              np.zeros((B, 7, 7, 64), np.float32), np.zeros((B, 512), np.float32)] if acts else [None] * 4
-        lib().orc_qnet_forward(self.h, _p(x), B, _p(q), *[_p(t) for t in a])
+        fn = lib().orc_qnet32_forward if self.f32 else lib().orc_qnet_forward
+        fn(self.h, _p(x), B, _p(q), *[_p(t) for t in a])
         return (q, a) if acts else q
 
     def train(self, x, actions, y):
@@ -324,7 +338,8 @@ class QNet:
         y = np.ascontiguousarray(y, dtype=np.float32)
         grads = np.zeros(sum(VAR_SIZES), dtype=np.float32)
         norms = np.zeros(10, dtype=np.float32)
-        loss = lib().orc_qnet_train(self.h, _p(x), _p(a), _p(y), x.shape[0], _p(grads), _p(norms))
+        fn = lib().orc_qnet32_train if self.f32 else lib().orc_qnet_train
+        loss = fn(self.h, _p(x), _p(a), _p(y), x.shape[0], _p(grads), _p(norms))
         out, off = [], 0
         for v in range(10):
             out.append(grads[off:off + VAR_SIZES[v]].reshape(VAR_SHAPES[v]))
@@ -386,6 +401,13 @@ class Learner:
     def vector_step(self):
         lib().orc_learner_vector_step(self.h)
 
+    def prefill(self, n_vector_steps):
+        """vector steps without updates (act, env step, replay push, episode books)"""
+        lib().orc_learner_prefill(self.h, n_vector_steps)
+
+    def stats_events(self):
+        return int(lib().orc_learner_stats_events(self.h))
+
     def counters(self):
         out = np.zeros(6, dtype=np.uint64)
         eps = C.c_double()
@@ -420,7 +442,7 @@ class Learner:
         return w[:n * self.B].reshape(n, self.B), leaves, pmax.value
 
     def qnet(self, which=0):
-        return QNet(handle=lib().orc_learner_qnet(self.h, which), owned=False)
+        return QNet(handle=lib().orc_learner_qnet(self.h, which), owned=False, f32=self.params.qnet_precision == 0)
 
     def env_state(self, e):
         s = np.zeros(1, dtype=STATE_DTYPE)

@@ -1,9 +1,15 @@
 """GPU SelfDrivingQLearner (vector steps) vs the oracle's sequential restatement.
 
-Bit-exact: actions drawn at random (pure-random warm-up and epsilon-greedy random draws), env rewards /
-dones / final mechanics, replay contents, sampled indices, episode bookkeeping.
-Within tolerance: Bellman targets y = r + gamma max Q_target(s') (3e-2 of max|y|) and losses.
+fp32 (qnet_precision = QLX_PREC_F32, the reference's arithmetic; the default): EVERYTHING is bit-exact - actions
+(random and greedy), env rewards / dones / mechanics, replay contents, sampled indices, Bellman targets, losses, the
+online weights and Adam slots after any number of updates (the Q-net is one fmaf chain per output in the order
+DESIGN.md §6 defines, tests/test_gpu_qnet32.py).
+bf16 (QLX_PREC_BF16, the labelled fast path): env / replay / indices exact; targets and losses within the stated
+bf16 tolerances (3e-2 of max|y|; lockstep losses 10 %).
 """
+import hashlib
+import os
+
 import numpy as np
 import pytest
 
@@ -17,17 +23,185 @@ def _qlx():
     return qlx
 
 
-def make(N, B, **kw):
+def make(N, B, prec=0, **kw):
     qlx = _qlx()
     p = dict(n_envs=N, batch_size=B, history_buffer_len=3000, update_after_actions=4,
-             epsilon_pure_random_steps=50_000, max_steps_per_episode=10_000)
+             epsilon_pure_random_steps=50_000, max_steps_per_episode=10_000, qnet_precision=prec)
     p.update(kw)
     return qlx.SelfDrivingQLearner(qlx.Parameter(**p)), O.Learner(O.default_params(**p))
 
 
-def test_pure_random_phase_parity():
+def same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def assert_step_equal(g, r, v):
+    for k in ("actions", "rewards", "dones", "indices", "targets", "losses"):
+        assert same(g[k], r[k]), f"{k} differ @ vector step {v}"
+
+
+def assert_models_equal(gpu_model, ref_qnet):
+    for var in range(10):
+        for which in range(3):
+            assert same(gpu_model.get(var, which), ref_qnet.get(var, which)), (var, which)
+
+
+def test_f32_pure_random_phase_bit_exact():
     N, B = 16, 32
     gpu, ref = make(N, B, max_steps_per_episode=45)
+    n_updates = 0
+    for v in range(30):
+        gpu.vector_step()
+        ref.vector_step()
+        g, r = gpu.last(), ref.last()
+        assert_step_equal(g, r, v)
+        n_updates += len(r["losses"])
+    assert n_updates > 50
+    assert_models_equal(gpu.model, ref.qnet(0))
+    sg, sr = gpu.stats(), ref.counters()
+    for k in ("step_count", "update_count", "episode_count", "replay_len"):
+        assert sg[k] == sr[k], k
+    assert sg["running_reward"] == sr["running_reward"] and sg["epsilon"] == sr["epsilon"]
+
+
+def test_f32_greedy_phase_bit_exact():
+    """Greedy acting from the online net while it learns: the acting forward, argmax, every update and the
+    resulting trajectories stay identical (epsilon 0.3 -> 0.05 over the run, one update per 16 env-steps)."""
+    N, B = 64, 32
+    gpu, ref = make(N, B, epsilon_pure_random_steps=200, epsilon_max=0.3, epsilon_min=0.05, epsilon_greedy_steps=2000.0,
+                    update_after_actions=16, max_steps_per_episode=200)
+    greedy = 0
+    for v in range(24):
+        gpu.vector_step()
+        ref.vector_step()
+        g, r = gpu.last(), ref.last()
+        assert_step_equal(g, r, v)
+        greedy += int(len(r["q"]) > 0)
+    assert greedy >= 20
+    assert_models_equal(gpu.model, ref.qnet(0))
+    mech = gpu.environment.mechanics()
+    for e in range(N):
+        ro = ref.env_state(e)
+        for k in O.STATE_DTYPE.names:
+            assert mech[k][e] == ro[k], (e, k)
+
+
+def test_f32_c2_config_bit_exact():
+    """Config C2: 1,024 envs, replay 100,000 filled to capacity (98 prefill vector steps, the FIFO
+    wraps), B = 1,024, replay ratio 8 (update every 128 env-steps); then 2 full vector steps (16 updates, greedy
+    acting at epsilon ~0.1) compared bit for bit."""
+    N, B = 1024, 1024
+    kw = dict(history_buffer_len=100_000, update_after_actions=128, epsilon_pure_random_steps=98 * 1024,
+              epsilon_greedy_steps=100_000.0, stats_after_steps=0)
+    gpu, ref = make(N, B, **kw)
+    gpu.prefill(98)
+    ref.prefill(98)
+    assert gpu.stats()["replay_len"] == ref.counters()["replay_len"] == 100_000
+    for v in range(2):
+        gpu.vector_step()
+        ref.vector_step()
+        g, r = gpu.last(), ref.last()
+        assert len(r["losses"]) == 8
+        assert_step_equal(g, r, v)
+    assert_models_equal(gpu.model, ref.qnet(0))
+
+
+def test_f32_c3_config():
+    """Config C3: 8,192 envs, replay 1,000,000 filled to capacity, B = 1,024 (64 updates per vector step).  The
+    oracle cannot hold 1M state pairs, so: sampled indices of all 64 updates = the sequential sampler at len 1M
+    (bit-exact); the Bellman targets of the first two updates and the first update's loss, gradients and weights =
+    the fp32 oracle fed the product's own gathered transitions and pre-step weights (bit-exact)."""
+    qlx = _qlx()
+    N, B = 8192, 1024
+    p = qlx.Parameter(n_envs=N, batch_size=B, history_buffer_len=1_000_000, update_after_actions=128,
+                      epsilon_pure_random_steps=123 * N, epsilon_greedy_steps=1_000_000.0, stats_after_steps=0)
+    L = qlx.SelfDrivingQLearner(p)
+    L.prefill(123)
+    st = L.stats()
+    assert st["replay_len"] == 1_000_000 and st["update_count"] == 0
+    w0 = [[L.model.get(v, which) for which in range(3)] for v in range(10)]
+    tw = [L.stabilized_model.get(v) for v in range(10)]
+    L.vector_step()
+    g = L.last()
+    assert g["losses"].shape[0] == 64
+    for u in range(64):
+        ref_idx = O.sample_distinct(p.learner_seed, u, 0, 1_000_000, B)
+        assert same(g["indices"][u], ref_idx), f"update {u} indices"
+    tnet = O.QNet(seed=1, f32=True)
+    for v in range(10):
+        tnet.set(v, tw[v])
+    for u in range(2):
+        batch = L.replay_buffer.get_many(g["indices"][u])
+        q = tnet.forward(batch["state_next"])
+        y = np.where(batch["done"], batch["reward"],
+                     (batch["reward"] + (q.max(axis=1) * np.float32(p.gamma)).astype(np.float32)).astype(np.float32))
+        assert same(g["targets"][u], y.astype(np.float32)), f"targets of update {u}"
+    online = O.QNet(seed=1, f32=True)
+    for v in range(10):
+        for which in range(3):
+            online.set(v, w0[v][which], which)
+    batch = L.replay_buffer.get_many(g["indices"][0])
+    loss, _, _ = online.train(batch["state"], batch["action"], g["targets"][0])
+    assert same(np.float32(loss), g["losses"][0])
+
+
+C1_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c1_learner_f32.npz")
+
+
+def test_f32_c1_reference_loop_golden():
+    """Config C1 (SURVEY §8d): the reference loop itself - 1 env, Parameter::default(), B = 32, 10,000 env-steps
+    (all random: 50k pure-random steps), 2,492 updates - on the GPU learner, against the fp32 oracle's run of the
+    same loop committed as tests/golden/c1_learner_f32.npz (tests/golden/make_c1_golden.py): actions, rewards,
+    dones and all 2,492 losses bit-exact; targets, indices and the final weights / Adam slots by SHA-256."""
+    qlx = _qlx()
+    gold = np.load(C1_GOLDEN, allow_pickle=False)
+    L = qlx.SelfDrivingQLearner(qlx.Parameter(n_envs=1, batch_size=32))
+    acts, rews, dones, losses = [], [], [], []
+    h_idx, h_tg = hashlib.sha256(), hashlib.sha256()
+    for _ in range(10_000):
+        L.vector_step()
+        g = L.last()
+        acts.append(g["actions"][0]); rews.append(g["rewards"][0]); dones.append(g["dones"][0])
+        if len(g["losses"]):
+            losses.extend(g["losses"].tolist())
+            h_idx.update(g["indices"].astype(np.uint64).tobytes())
+            h_tg.update(g["targets"].astype(np.float32).tobytes())
+    assert same(np.array(acts, np.uint8), gold["actions"])
+    assert same(np.array(rews, np.float32), gold["rewards"])
+    assert same(np.array(dones, np.uint8), gold["dones"])
+    assert len(losses) == 2492
+    assert same(np.array(losses, np.float32), gold["losses"])
+    assert h_idx.hexdigest() == str(gold["indices_sha256"]) and h_tg.hexdigest() == str(gold["targets_sha256"])
+    hw = hashlib.sha256()
+    for v in range(10):
+        for which in range(3):
+            hw.update(L.model.get(v, which).astype(np.float32).tobytes())
+    assert hw.hexdigest() == str(gold["model_sha256"])
+
+
+def test_stats_events_and_checkpoint(tmp_path):
+    """stats_after_steps (self_driving_tf_q_learner.rs:204-212): the learner writes its checkpoint and the
+    learning_update_log once per vector step that crosses a multiple - same event count as the oracle; the file
+    holds the online weights of that moment and the log text equals the oracle's formatting of the same state."""
+    qlx = _qlx()
+    path = str(tmp_path / "ql.ckpt")
+    gpu, ref = make(32, 32, stats_after_steps=100, checkpoint_file=path, max_steps_per_episode=60, update_after_actions=8)
+    for v in range(20):
+        gpu.vector_step()
+        ref.vector_step()
+    assert gpu.stats_events() == ref.stats_events() >= 6
+    m2 = qlx.DeepQLearningModel(seed=99)
+    m2.read_checkpoint(path)
+    for var in range(10):
+        assert same(m2.get(var), gpu.model.get(var))
+    log = gpu.last_log()
+    assert log == gpu.learning_update_log() and "reward_distribution" in log
+
+
+def test_bf16_pure_random_phase_parity():
+    N, B = 16, 32
+    gpu, ref = make(N, B, prec=1, max_steps_per_episode=45)
     n_updates = 0
     rel_errs = []
     for v in range(30):
@@ -70,11 +244,11 @@ def test_pure_random_phase_parity():
     assert np.array_equal(got["done"].astype(np.uint8), d)
 
 
-def test_lockstep_update_losses():
+def test_bf16_lockstep_update_losses():
     """One update per vector step; before each step the oracle's online net is re-synced to the product's
     weights + Adam slots, so every loss is compared from identical state (Q-forward tolerance)."""
     N, B = 32, 32
-    gpu, ref = make(N, B, update_after_actions=N)
+    gpu, ref = make(N, B, prec=1, update_after_actions=N)
     ref_online = ref.qnet(0)
     n = 0
     for v in range(12):
@@ -99,8 +273,8 @@ def test_epsilon_random_branch_is_exact():
         assert np.array_equal(gpu.last()["actions"], ref.last()["actions"])
 
 
-def test_greedy_actions_match_where_margin_is_clear():
-    gpu, ref = make(128, 32, epsilon_pure_random_steps=0, epsilon_max=0.0, epsilon_min=0.0)
+def test_bf16_greedy_actions_match_where_margin_is_clear():
+    gpu, ref = make(128, 32, prec=1, epsilon_pure_random_steps=0, epsilon_max=0.0, epsilon_min=0.0)
     checked = 0
     for _ in range(4):       # early steps: weights identical or one update apart
         obs = gpu.environment.state()

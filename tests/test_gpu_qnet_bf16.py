@@ -1,4 +1,5 @@
-"""GPU Q-network (bf16 MFMA, fp32 accumulation / master weights) vs the fp32 oracle.
+"""GPU Q-network, the bf16 fast path (QLX_ARCH_NATURE_DQN_BF16: bf16 MFMA operands, fp32 accumulation / master
+weights) vs the fp32 oracle.  The fp32 path (the reference's arithmetic) is bit-exact: tests/test_gpu_qnet32.py.
 
 Stated tolerances (bf16 operands carry 8 significant bits):
   Q values / activations : max|gpu - ref| <= 3e-2 * max|ref| (+ tiny absolute floor)
@@ -25,6 +26,11 @@ pytestmark = pytest.mark.gpu
 def _qlx():
     import qlx
     return qlx
+
+
+def _bf16(seed):
+    qlx = _qlx()
+    return qlx.DeepQLearningModel(seed=seed, precision=qlx.PREC_BF16)
 
 
 def rand_states(B, seed, sparse=False):
@@ -57,7 +63,7 @@ def close(a, ref, rel):
 
 
 def test_init_weights_bit_identical():
-    m = _qlx().DeepQLearningModel(seed=2)
+    m = _bf16(seed=2)
     ref = O.QNet(seed=2)
     for v in range(10):
         assert np.array_equal(m.get(v), ref.get(v)), f"var {v}"
@@ -66,7 +72,7 @@ def test_init_weights_bit_identical():
 
 @pytest.mark.parametrize("B,kind", [(1, "env"), (32, "rand"), (100, "sparse"), (256, "env"), (520, "sparse")])
 def test_forward_parity(B, kind):
-    m = _qlx().DeepQLearningModel(seed=2)
+    m = _bf16(seed=2)
     ref = O.QNet(seed=2)
     x = env_states(B) if kind == "env" else rand_states(B, B, sparse=kind == "sparse")
     q, a = m.q_values(x)
@@ -84,7 +90,7 @@ def test_forward_parity(B, kind):
 
 
 def test_batch_max_q_and_predict_action():
-    m = _qlx().DeepQLearningModel(seed=4)
+    m = _bf16(seed=4)
     ref = O.QNet(seed=4)
     x = env_states(32)
     mx = m.batch_predict_max_future_reward(x)
@@ -96,7 +102,7 @@ def test_batch_max_q_and_predict_action():
 
 @pytest.mark.parametrize("B", [32, 256, 320])
 def test_train_step_parity(B):
-    m = _qlx().DeepQLearningModel(seed=7)
+    m = _bf16(seed=7)
     ref = O.QNet(seed=7)
     w0 = ref.weights()
     x = np.concatenate([env_states(B // 2), rand_states(B - B // 2, 3, sparse=True)])
@@ -141,13 +147,13 @@ def test_train_step_parity(B):
 
 def test_checkpoint_roundtrip():
     qlx = _qlx()
-    m = qlx.DeepQLearningModel(seed=9)
+    m = _bf16(seed=9)
     x = env_states(8)
     m.train(x, np.zeros(8, np.uint8), np.ones(8, np.float32))
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "ckpt.qlx")
         m.write_checkpoint(path)
-        m2 = qlx.DeepQLearningModel(seed=1)
+        m2 = _bf16(seed=1)
         m2.read_checkpoint(path)
         for v in range(10):
             for which in range(3):
@@ -160,7 +166,7 @@ def test_checkpoint_roundtrip():
 
 def test_multi_step_training_stays_close():
     """5 consecutive updates on the same data: drift stays within the per-step bound."""
-    m = _qlx().DeepQLearningModel(seed=11)
+    m = _bf16(seed=11)
     ref = O.QNet(seed=11)
     B = 64
     x = env_states(B)
@@ -183,7 +189,7 @@ def test_large_batch_forward_paths_agree():
     two paths differ only in fc1's fp32 summation order, which can move an a4 element across a bf16 rounding
     boundary (one bf16 ulp = 2^-8 relative): max |dQ| <= 1e-2 * max|Q|, mean |dQ| <= 1e-4 * max|Q|.  A slice of
     the big batch is checked against the fp32 oracle with the module's tolerance."""
-    m = _qlx().DeepQLearningModel(seed=3)
+    m = _bf16(seed=3)
     x = rand_states(8192, 17, sparse=True)
     q_big, a_big = m.q_values(x)
     q_chunks = np.concatenate([m.q_values(x[i:i + 1024])[0] for i in range(0, 8192, 1024)])
@@ -209,7 +215,7 @@ def test_conv1_wgrad_halves_bit_identical(B):
     for halves in ("1", "0"):
         os.environ["QLX_CONV1_HALVES"] = halves
         try:
-            m = _qlx().DeepQLearningModel(seed=3)
+            m = _bf16(seed=3)
         finally:
             os.environ.pop("QLX_CONV1_HALVES", None)
         loss, grads, _ = m.train(x, a, y, want_grads=True)
