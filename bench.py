@@ -8,13 +8,23 @@ env-steps trigger (update every `update_after_actions` env-steps with batch B, r
 forward, online forward, Huber, backward, [RCCL all-reduce], clip_by_norm + Adam.
 
     python bench.py --gpus N --steps K --warmup W
-Multi-GPU: launched by torch.distributed.run, one process per GPU; envs are sharded (weak scaling) and
-gradients are all-reduced over RCCL inside libqlx.  torch.distributed (gloo) is only the control plane.
+
+Default workload (N = 1): config C3 of SURVEY.md §8(d) - 8,192 envs per GPU, replay 1,000,000 in HBM, B = 1024,
+fp32 Q-net (the reference's arithmetic).  Steady state regardless of --warmup: before anything is timed the replay
+is prefilled to capacity, which also runs the loop past the 50k-step pure-random phase, so the timed vector steps
+include the greedy acting forward, brick contacts and episode ends.  Then W untimed training vector steps, then K
+timed ones.  The bf16 fast path (labelled, not the headline) is measured beside it on the same workload.
+
+Multi-GPU: with --gpus N > 1 and no WORLD_SIZE in the environment, this process starts
+`torch.distributed.run --nproc-per-node N` on itself before touching the GPU and exits with its code; each rank owns
+one GPU, envs and replay are sharded (weak scaling), gradients are all-reduced over RCCL inside libqlx, rank 0's
+initial weights are broadcast over RCCL.  torch.distributed (gloo) is only the control plane.
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -23,33 +33,53 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
-PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
-PEAK_HBM_GBS = 8000.0         # HBM3E spec
-GEMM_SCOPES = ("trunk_fwd", "trunk_fwd_nostore", "trunk_bwd_data", "fc1_fwd", "fc1_bwd", "conv23_wgrad", "conv1_wgrad")
-# profiler scope -> the rocprofv3 kernel symbol it launches (for the committed PMC traffic lookup)
-SCOPE_KERNEL = {"trunk_fwd": "k_trunk_fwdILb1E", "trunk_fwd_nostore": "k_trunk_fwdILb0E", "trunk_bwd_data": "k_trunk_bwd_data",
-                "conv1_wgrad": "k_conv1_wgrad", "conv23_wgrad": "k_conv23_wgrad", "fc1_bwd": "k_fc1_bwd"}
-HBM_SCOPES = ("adam", "env_step", "replay_push")
-# per-sample algorithmic work of the scopes the roofline can name: (FLOP, HBM bytes).  trunk_fwd (the online forward
-# that keeps its activations for the backward): 2 (400*32*256 + 81*64*512 + 49*64*576) FLOP; 4 x 7,056 B frames
-# in + a1 25,600 + a2 10,368 + a3 6,272 B out.  219.6 FLOP/B is below the bf16 ridge (2,500 / 8 = 312.5): HBM class.
-SCOPE_ALGO = {"trunk_fwd": (15_474_688.0, 70_464.0), "trunk_fwd_nostore": (15_474_688.0, 28_224.0 + 6_272.0)}
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md: f32-input MFMA, bf16)
+PEAK_HBM_GBS = 8000.0                            # HBM3E
+# per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
+FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
+TRANSITION_BYTES = 56_454          # logical (a, s, s', r, done) of one sampled transition
+ADAM_BYTES = 53_941_344            # clip_by_norm + Adam per update: g read twice, w / m / v read and written
+# profiler scopes of each precision: the GEMM-shaped kernels (FLOP work) and their per-layer grouping
+GEMM_SCOPES = {
+    "fp32": ("f32_conv1_fwd", "f32_conv2_fwd", "f32_conv3_fwd", "f32_fc1_fwd", "f32_fc1_bwd", "f32_conv3_bwd",
+             "f32_conv2_bwd", "f32_conv1_wgrad"),
+    "bf16": ("trunk_fwd", "trunk_fwd_nostore", "trunk_bwd_data", "fc1_fwd", "fc1_bwd", "conv23_wgrad", "conv1_wgrad"),
+}
+ADAM_SCOPES = {"fp32": ("f32_norms", "f32_adam"), "bf16": ("sumsq", "adam")}
+# the kernels that deliver sampled transitions into the net: index draw, gather, and the conv1 frame fetch of the
+# online and target passes (fp32: conv1 is its own launch)
+SAMPLE_SCOPES = {"fp32": ("sample", "gather", "f32_conv1_fwd"), "bf16": ("sample", "gather")}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=55, help="vector steps before timing (covers the 50k pure-random phase)")
-    ap.add_argument("--envs", type=int, default=1024, help="envs per GPU (config C2: 1024)")
+    ap.add_argument("--steps", type=int, default=10, help="timed vector steps")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed training vector steps after the replay prefill")
+    ap.add_argument("--envs", type=int, default=8192, help="envs per GPU (C3: 8192; C2: 1024; C4: 4096 x 8)")
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--replay-ratio", type=int, default=8, help="samples per env-step (reference: 32 per 4 steps)")
-    ap.add_argument("--replay", type=int, default=100_000, help="replay capacity per GPU (config C2: 100k)")
-    ap.add_argument("--cpu-sample", type=int, default=2000, help="env-steps of the CPU baseline sample, ~15 s (0 = skip)")
-    ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--replay", type=int, default=1_000_000, help="replay capacity per GPU (C3: 1M; C2: 100k)")
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32", help="headline Q-net arithmetic")
+    ap.add_argument("--beside-steps", type=int, default=5, help="timed vector steps of the other precision (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=10_000, help="env-steps of the CPU baseline (C1: 10,000; 0 = skip)")
+    ap.add_argument("--profile-steps", type=int, default=1)
     ap.add_argument("--double-dqn", action="store_true", help="extension (config C5): double-DQN targets")
     ap.add_argument("--per", action="store_true", help="extension (config C5): proportional prioritized replay")
+    ap.add_argument("--control-only", action="store_true",
+                    help="exercise the rank spawn + gloo control plane only (no GPU; CPU test of the N > 1 path)")
     return ap.parse_args()
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a torch.distributed.run environment: start N rank processes on this bench (before
+    any GPU call in this process) and return their exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 class Control:
@@ -77,6 +107,14 @@ class Control:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def sum(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
     def bcast_bytes(self, b):
         if not self.dist:
             return b
@@ -85,155 +123,272 @@ class Control:
         return obj[0]
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(sample_steps):
+    """C1 on the host: the oracle's restatement of the reference loop (1 env, Parameter::default(), B = 32).  The loop
+    runs on one pinned core (the OpenMP master thread, OMP_PROC_BIND=close on an explicit place list); the Q-net's
+    OpenMP regions use up to 16 of the cores this process may run on."""
     exe = os.path.join(ROOT, "oracle", "cpu_baseline")
     if sample_steps <= 0 or not os.path.exists(exe):
         return None
-    threads = min(16, os.cpu_count() or 1)
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    out = subprocess.run([exe, str(sample_steps)], capture_output=True, text=True, env=env, timeout=600, check=True)
+    cpus = sorted(os.sched_getaffinity(0))[:16]
+    env = dict(os.environ, OMP_NUM_THREADS=str(len(cpus)), OMP_PROC_BIND="close",
+               OMP_PLACES=",".join("{%d}" % c for c in cpus))
+    out = subprocess.run([exe, str(sample_steps)], capture_output=True, text=True, env=env, timeout=900, check=True)
     r = json.loads(out.stdout.strip().splitlines()[-1])
     return {"value": round(r["env_steps_per_sec"], 3), "unit": "env-steps/s", "cores": r["threads"], "kind": "port",
-            "sample": f"{r['env_steps']} env-steps of the C++ restatement of the reference loop (oracle/): 1 env, "
-                      f"Parameter::default(), B=32, {r['updates']} fp32 Q-net train_model updates, "
-                      f"{r['seconds']:.1f} s; env+replay single-threaded, Q-net OpenMP",
+            "sample": f"C1: {r['env_steps']} env-steps of the C++ restatement of the reference loop (oracle/): 1 env, "
+                      f"Parameter::default(), B=32, {r['updates']} fp32 Q-net updates, {r['seconds']:.1f} s; env loop "
+                      f"single-threaded on one pinned core, Q-net OpenMP on {r['threads']} cores ({cpu_model()})",
             "grad_updates_per_sec": round(r["updates_per_sec"], 3)}
 
 
-def roofline(scope, work, launches, avg_us, tflops, traffic, traffic_src):
-    """Roofline entry for the dominant kernel: the bound follows its arithmetic intensity (algorithmic FLOP per
-    algorithmic HBM byte against the ridge PEAK_BF16 / PEAK_HBM); achieved = algorithmic work per launch / the
-    live average launch duration.  Both rates are kept for the record."""
-    flops_launch = work / max(launches, 1)
-    fl, by = SCOPE_ALGO.get(scope, (None, None))
-    r = {"kernel": scope, "avg_us": round(avg_us, 2), "launches": launches, "flops_per_launch": round(flops_launch),
-         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-         "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4)}
-    if fl is None:
-        r.update({"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                  "frac": round(tflops / PEAK_BF16_TFLOPS, 4)})
-        return r
-    bytes_launch = flops_launch / fl * by
-    gbs = bytes_launch / (avg_us * 1e-6) / 1e9 if avg_us > 0 else 0.0
-    intensity = fl / by
-    r["algorithmic_bytes_per_launch"] = round(bytes_launch)
-    r["flop_per_byte"] = round(intensity, 1)
-    if intensity < PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9):
-        r.update({"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                  "frac": round(gbs / PEAK_HBM_GBS, 4)})
-    else:
-        r.update({"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                  "frac": round(tflops / PEAK_BF16_TFLOPS, 4)})
-    return r
+def config_label(N, replay, flags, world):
+    if flags == 0 and world == 1 and N == 1024 and replay == 100_000:
+        return "C2"
+    if flags == 0 and world == 1 and N == 8192 and replay == 1_000_000:
+        return "C3"
+    if flags == 0 and world == 8 and N == 4096:
+        return "C4"
+    if flags == 3 and world == 8 and N == 8192:
+        return "C5"
+    if flags == 3 and world == 1 and N == 8192:
+        return "C5 (one GPU's shard)"
+    return f"custom ({world} GPU)"
 
 
-def pmc_traffic(scope):
-    """HBM bytes per launch of the scope's kernel from the newest committed PMC pass (profiles/*/pmc_traffic.json,
-    written by scripts/pmc.sh + scripts/pmc_traffic.py on the same build), or None."""
+def log(msg):
+    """progress on stderr (one line per phase, so a long run shows it is alive)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def rate(work, us, div):
+    return work / us / div if us > 0 else 0.0
+
+
+class Run:
+    """One learner measured on the steady-state workload."""
+
+    def __init__(self, args, ctl, precision, steps, warmup, flags):
+        import qlx
+        self.args, self.ctl, self.precision = args, ctl, precision
+        N, B = args.envs, args.batch
+        self.ua = B // args.replay_ratio
+        prec = qlx.PREC_F32 if precision == "fp32" else qlx.PREC_BF16
+        p = qlx.Parameter(n_envs=N, batch_size=B, update_after_actions=self.ua, history_buffer_len=args.replay,
+                          rank=ctl.rank, flags=flags, qnet_precision=prec)
+        L = qlx.SelfDrivingQLearner(p, device=ctl.local)
+        self.L = L
+        try:
+            if ctl.world > 1:
+                uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
+                L.dist_init(ctl.world, ctl.rank, uid)
+            # steady state: replay at capacity and past the pure-random phase, whatever --warmup is
+            prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
+            log(f"{precision}: prefill {prefill} vector steps")
+            L.prefill(prefill)
+            log(f"{precision}: warmup {max(warmup, 1)} vector steps")
+            L.run(max(warmup, 1))
+            L.sync()
+            s = L.stats()
+            assert s["replay_len"] == args.replay, s
+            assert s["step_count"] >= p.epsilon_pure_random_steps, s
+            self.prefill = prefill
+            log(f"{precision}: profile pass")
+            self.comps = self._profile()
+            log(f"{precision}: timed {steps} vector steps")
+            self._timed(steps)
+            log(f"{precision}: {self.value():.1f} env-steps/s")
+        finally:
+            L.close()
+
+    def _profile(self):
+        """Event-timed per-scope device time over profile_steps vector steps (every launch bracketed by events, so
+        the sum exceeds the un-instrumented step; for attribution only)."""
+        L, n = self.L, self.args.profile_steps
+        L.profile(True)
+        L.run(n)
+        L.sync()
+        comps = {}
+        for name in L.profile_names():
+            us, work, k = L.profile_get(name)
+            if k:
+                comps[name] = {"avg_us": us / k, "launches_per_step": k / n, "total_us_per_step": us / n, "work": work / n}
+        L.profile(False)
+        return comps
+
+    def _timed(self, steps):
+        L, ctl, gemm = self.L, self.ctl, GEMM_SCOPES[self.precision]
+        self.dominant = max((c for c in self.comps if c in gemm), key=lambda c: self.comps[c]["total_us_per_step"])
+        # events only around the dominant kernel, on every 7th launch (keeps the event cost off the clock)
+        L.profile(True)
+        L.profile_filter(self.dominant, stride=7)
+        s0 = L.stats()
+        ctl.barrier()
+        L.sync()
+        t0 = time.perf_counter()
+        L.run(steps)
+        L.sync()
+        ctl.barrier()
+        dt = ctl.max(time.perf_counter() - t0)
+        s1 = L.stats()
+        self.dom_us, self.dom_work, self.dom_launches = L.profile_get(self.dominant)
+        L.profile(False)
+        self.steps, self.dt = steps, dt
+        self.env_steps = self.args.envs * steps * ctl.world
+        self.updates = s1["update_count"] - s0["update_count"]
+        self.episodes = int(ctl.sum(s1["episode_count"] - s0["episode_count"]))
+        self.episodes_total = int(ctl.sum(s1["episode_count"]))
+        self.last_loss = s1["last_loss"]
+        self.running_reward = s1["running_reward"]
+        self.epsilon = s1["epsilon"]
+
+    def roofline(self):
+        """The dominant kernel against the MFMA peak of this precision (the Q-net is MFMA class):
+        achieved = algorithmic FLOP per launch / live average launch duration (HIP events bound to the kernel's own
+        dispatch on the learner stream, every 7th launch of the timed region)."""
+        peak = PEAK_TFLOPS[self.precision]
+        avg_us = self.dom_us / max(self.dom_launches, 1)
+        tflops = rate(self.dom_work, self.dom_us, 1e6)
+        traffic, src = pmc_traffic(self.precision, self.dominant)
+        return {"kernel": self.dominant, "bound": "mfma", "achieved": round(tflops, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(tflops / peak, 4), "traffic": traffic, "traffic_unit": "HBM bytes/launch",
+                "traffic_source": src, "avg_us": round(avg_us, 2), "launches_timed": self.dom_launches,
+                "flops_per_launch": round(self.dom_work / max(self.dom_launches, 1))}
+
+    def report(self):
+        """north_star's extra rates from the event-timed profile pass: per-layer MFMA utilisation, replay-sampling
+        and clip+Adam HBM fractions."""
+        c, peak = self.comps, PEAK_TFLOPS[self.precision]
+        layers = {}
+        for k in GEMM_SCOPES[self.precision]:
+            if k in c and c[k]["total_us_per_step"] > 0:
+                t = rate(c[k]["work"], c[k]["total_us_per_step"], 1e6)
+                layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
+        upd = self.updates / max(self.steps, 1) / max(self.ctl.world, 1)   # updates per vector step on one GPU
+        B = self.args.batch
+        t_samp = sum(c[k]["total_us_per_step"] for k in SAMPLE_SCOPES[self.precision] if k in c)
+        samp_gbs = rate(upd * B * TRANSITION_BYTES, t_samp, 1e3)
+        t_adam = sum(c[k]["total_us_per_step"] for k in ADAM_SCOPES[self.precision] if k in c)
+        adam_gbs = rate(upd * ADAM_BYTES, t_adam, 1e3)
+        return {
+            "mfma_per_layer": layers,
+            "replay_sampling": {"gbs": round(samp_gbs, 1), "frac": round(samp_gbs / PEAK_HBM_GBS, 4),
+                                "bytes_per_transition": TRANSITION_BYTES, "scopes": list(SAMPLE_SCOPES[self.precision]),
+                                "note": "logical transition bytes (a, s, s', r, done) delivered into the net / time of "
+                                        "index draw + gather + conv1 frame-fetch launches"},
+            "clip_adam": {"gbs": round(adam_gbs, 1), "frac": round(adam_gbs / PEAK_HBM_GBS, 4),
+                          "bytes_per_update": ADAM_BYTES, "scopes": list(ADAM_SCOPES[self.precision])},
+        }
+
+    def value(self):
+        return self.env_steps / self.dt
+
+
+def pmc_traffic(precision, scope):
+    """HBM bytes per launch of the scope's kernel from the newest committed PMC pass of this precision
+    (profiles/*/pmc_traffic_<precision>.json, written by scripts/pmc.sh + scripts/pmc_traffic.py), or None."""
     import glob
-    key = SCOPE_KERNEL.get(scope)
     import re
-    # natural order of the round / version directories (r01_v10 after r01_v9)
     nat = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), key=nat)
-    if not key or not files:
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_traffic_{precision}.json")), key=nat)
+    if not files:
         return None, None
-    data = json.load(open(files[-1]))["kernels"]
-    hits = [v for k, v in data.items() if key in k]
-    if len(hits) != 1:
+    d = json.load(open(files[-1]))
+    hit = d.get("scopes", {}).get(scope)
+    if hit is None:
         return None, None
-    return hits[0]["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return hit["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+
+
+def control_check(ctl):
+    """The control plane bench.py relies on, without the GPU: barrier, max / sum over ranks, rank 0's unique id on
+    every rank.  Rank 0 prints one JSON line."""
+    uid = ctl.bcast_bytes(bytes(range(128)) if ctl.rank == 0 else bytes(128))
+    ctl.barrier()
+    out = {"world": ctl.world, "max_rank": ctl.max(float(ctl.rank)), "sum_ones": ctl.sum(1.0),
+           "uid_ok": ctl.sum(1.0 if uid == bytes(range(128)) else 0.0) == ctl.world}
+    ctl.barrier()
+    if ctl.rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     ctl = Control()
+    assert ctl.world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {ctl.world}"
+    if args.control_only:
+        control_check(ctl)
+        return
+    assert args.batch % args.replay_ratio == 0
     import qlx
-    N, B = args.envs, args.batch
-    assert B % args.replay_ratio == 0
-    ua = B // args.replay_ratio
     flags = (qlx.DOUBLE_DQN if args.double_dqn else 0) | (qlx.PER if args.per else 0)
-    p = qlx.Parameter(n_envs=N, batch_size=B, update_after_actions=ua, history_buffer_len=args.replay, rank=ctl.rank,
-                      flags=flags)
-    L = qlx.SelfDrivingQLearner(p, device=ctl.local)
-    if ctl.world > 1:
-        uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
-        L.dist_init(ctl.world, ctl.rank, uid)
-
-    L.run(args.warmup)
-    L.sync()
-    # short profiled pass: per-kernel device time, pick the dominant GEMM kernel
-    L.profile(True)
-    L.run(args.profile_steps)
-    L.sync()
-    comps = {}
-    for name in L.profile_names():
-        us, work, n = L.profile_get(name)
-        if n:
-            comps[name] = {"avg_us": us / n, "launches_per_step": n / args.profile_steps, "total_us_per_step":
-                           us / args.profile_steps}
-            if name in GEMM_SCOPES and us > 0:
-                comps[name]["tflops"] = work / us / 1e6
-            if name in HBM_SCOPES and us > 0:
-                comps[name]["gbs"] = work / us / 1e3
-    dominant = max((n for n in comps if n in GEMM_SCOPES), key=lambda n: comps[n]["total_us_per_step"])
-    L.profile(False)
-
-    # timed region: events only around the dominant kernel's launches
-    L.profile(True)
-    # every 7th launch (coprime with the 8 updates of a vector step, so the samples rotate through the update
-    # positions) keeps the event cost off the clock
-    L.profile_filter(dominant, stride=7)
-    s0 = L.stats()
-    ctl.barrier()
-    L.sync()
-    t0 = time.perf_counter()
-    L.run(args.steps)
-    L.sync()
-    ctl.barrier()
-    dt = time.perf_counter() - t0
-    dt = ctl.max(dt)
-    s1 = L.stats()
-    us, work, launches = L.profile_get(dominant)
-    L.profile(False)
-
-    env_steps = N * args.steps * ctl.world
-    updates = s1["update_count"] - s0["update_count"]      # global updates (all-reduced: same on every rank)
+    head = Run(args, ctl, args.precision, args.steps, args.warmup, flags)
+    other = "bf16" if args.precision == "fp32" else "fp32"
+    beside = Run(args, ctl, other, args.beside_steps, 1, flags) if args.beside_steps > 0 else None
+    # the measured window is the steady-state loop: greedy acting and episode ends inside it
+    assert "act_forward" in head.comps, "acting forward missing from the measured loop"
+    assert head.episodes_total > 0, "no episode ended"
     if ctl.rank != 0:
         return
-    avg_us = us / max(launches, 1)
-    achieved = work / us / 1e6 if us > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(dominant)
+    N, B = args.envs, args.batch
+    label = config_label(N, args.replay, flags, ctl.world)
+    comps = {k: {kk: round(vv, 3) for kk, vv in v.items() if kk != "work"}
+             for k, v in sorted(head.comps.items(), key=lambda kv: -kv[1]["total_us_per_step"])}
     line = {
         "metric": METRIC,
-        "value": round(env_steps / dt, 1),
+        "value": round(head.value(), 1),
         "unit": "env-steps/s",
         "n_gpus": ctl.world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "ms_per_step": round(head.dt / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
-        "data": "synthetic: frames rendered by the batched Breakout env kernel from live play; "
-                "random-init (GlorotUniform) Nature-DQN",
-        "config": {"workload": f"{'C5' if flags else 'C2'}: {N} Breakout envs per GPU, replay {args.replay} in HBM, Nature-DQN "
-                               f"(3 conv + 2 dense), B={B}, update every {ua} env-steps (replay ratio "
-                               f"{args.replay_ratio} samples/env-step), epsilon-greedy acting"
-                               + (" + double-DQN" if args.double_dqn else "") + (" + prioritized replay" if args.per else ""),
-                   "envs_per_gpu": N, "batch": B, "replay_capacity": args.replay, "update_after_actions": ua,
-                   "parallelism": f"dp{ctl.world}" if ctl.world > 1 else "single", "env_dtype": "fp32",
-                   "qnet_dtype": "bf16 MFMA, fp32 accumulate + master weights"},
-        "grad_updates_per_sec": round(updates / dt, 2),
-        "samples_per_sec": round(updates * B * ctl.world / dt, 1),
-        "roofline": roofline(dominant, work, launches, avg_us, achieved, traffic, traffic_src),
-        "components": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                       for k, v in sorted(comps.items(), key=lambda kv: -kv[1]["total_us_per_step"])},
-        "episodes": s1["episode_count"],
-        "last_loss": s1["last_loss"],
+        "dtype": args.precision,
+        "data": "synthetic: frames rendered by the batched Breakout env kernel from live play; random-init "
+                "(GlorotUniform) Nature-DQN; replay prefilled to capacity before timing",
+        "config": {"workload": f"{label}: {N} Breakout envs per GPU, replay {args.replay} per GPU in HBM (prefilled), "
+                               f"Nature-DQN (3 conv + 2 dense) in {args.precision}, B={B}, update every {head.ua} "
+                               f"env-steps per GPU (replay ratio {args.replay_ratio} samples/env-step), epsilon-greedy "
+                               f"acting" + (" + double-DQN" if args.double_dqn else "")
+                               + (" + prioritized replay" if args.per else ""),
+                   "envs_per_gpu": N, "batch": B, "replay_capacity": args.replay, "update_after_actions": head.ua,
+                   "parallelism": f"dp{ctl.world}" if ctl.world > 1 else "single", "rccl_world": ctl.world,
+                   "env_dtype": "fp32 physics, u8 frames",
+                   "qnet_dtype": "fp32 (exact-fp32 MFMA v_mfma_f32_16x16x4_f32)" if args.precision == "fp32"
+                   else "bf16 MFMA operands, fp32 accumulate + master weights"},
+        "grad_updates_per_sec": round(head.updates / head.dt, 2),
+        "samples_per_sec": round(head.updates * B * ctl.world / head.dt, 1),
+        "replay_ratio": args.replay_ratio,
+        "roofline": head.roofline(),
+        **head.report(),
+        "steady_state": {"prefill_vector_steps": head.prefill, "episodes_in_window": head.episodes,
+                         "episodes_total": head.episodes_total, "epsilon": round(head.epsilon, 4),
+                         "running_reward": head.running_reward, "last_loss": head.last_loss},
+        "components_event_timed": comps,
     }
+    if beside is not None:
+        line[f"{other}_beside"] = {
+            "value": round(beside.value(), 1), "unit": "env-steps/s", "steps": beside.steps,
+            "ms_per_step": round(beside.dt / beside.steps * 1e3, 3),
+            "grad_updates_per_sec": round(beside.updates / beside.dt, 2), "roofline": beside.roofline(),
+            "note": "bf16 MFMA operands: the labelled fast path, not the reference's arithmetic" if other == "bf16"
+            else "fp32: the reference's arithmetic"}
     if ctl.world == 1:
+        log(f"cpu baseline: {args.cpu_sample} env-steps")
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample)
     print(json.dumps(line), flush=True)
 

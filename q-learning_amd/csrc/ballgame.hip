@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs H) {
     } else {
       for (int k = 1; k < kA; ++k) mx = fmaxf(mx, q[k]);
     }
-    H.y_out[b] = H.dones[b] ? H.rewards[b] : H.rewards[b] + mx * H.gamma;
+    H.y_out[b] = H.dones[b] ? H.rewards[b] : __fadd_rn(H.rewards[b], __fmul_rn(mx, H.gamma));
   }
   if (MODE == 3) {
     const int act = H.actions[b];

@@ -1,6 +1,7 @@
 // libqlx common pieces: error reporting, version, device selection.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 
 #include <mutex>
@@ -22,6 +23,18 @@ void set_lds_limit(const void* kernel, size_t bytes) {
   std::lock_guard<std::mutex> lock(mu);
   if (!done.insert({dev, kernel, bytes}).second) return;
   QLX_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+// QLX_DEBUG_SYNC=1: wait for the stream after each instrumented launch and name the launch in the error (fault
+// localisation on the GPU box; off by default)
+void debug_sync(hipStream_t s, const char* what) {
+  static const bool on = [] {
+    const char* v = std::getenv("QLX_DEBUG_SYNC");
+    return v && v[0] == '1';
+  }();
+  if (!on) return;
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) throw Error{QLX_E_HIP, std::string("after ") + what + ": " + hipGetErrorString(e)};
 }
 
 int current_device_checked(int device) {

@@ -176,6 +176,19 @@ __global__ void k_gather(ReplayView r, const uint64_t* idx, uint32_t B, const ui
   done[b] = r.done[t];
 }
 
+// this rank's contribution to the global solved() test: running reward, has-history flag, episode count, and the
+// minimum episode reward of its FIFO (+inf when empty, so the min over ranks ignores it)
+__global__ void k_book_local(const Book* book, const float* hist, uint32_t hist_cap, float* gsum, float* gmin) {
+  if (threadIdx.x != 0) return;
+  const Book b = *book;
+  float mn = __builtin_huge_valf();
+  for (uint32_t i = 0; i < b.hist_len; ++i) mn = fminf(mn, hist[(b.hist_head + i) % hist_cap]);
+  gsum[0] = b.running_reward;
+  gsum[1] = b.hist_len > 0 ? 1.0f : 0.0f;
+  gsum[2] = (float)b.episode_count;
+  gmin[0] = mn;
+}
+
 __global__ void k_obs_table(const uint8_t* obs, uint32_t n, const uint8_t** table) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n * 4) table[i] = obs + (size_t)i * kFramePix;
@@ -223,6 +236,10 @@ struct qlx_learner {
   bool dp_overlap = true;              // QLX_DP_OVERLAP=0: one whole-gradient all-reduce after the backward
   hipEvent_t ev_dense = nullptr, ev_reduced = nullptr;
   int world = 1, rank = 0;
+  // global solved() over ranks: per vector step, {sum running_reward, sum has_history, sum episodes} and {min episode
+  // reward} all-reduced on the learner stream (d_gsum[3], d_gmin[1])
+  float* d_gsum = nullptr;
+  float* d_gmin = nullptr;
   qlx::Profiler prof;
   // statistics events (write_checkpoint + learning_update_log, self_driving_tf_q_learner.rs:204-212,226-230)
   uint64_t stats_events = 0;
@@ -247,6 +264,7 @@ static void learner_targets(qlx_learner* L, uint32_t U) {
     hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, s, rv, L->d_idx, n, L->d_tab_s, L->d_tab_sn, L->d_bact,
                        L->d_brew, L->d_bdone);
   }
+  debug_sync(s, "gather");
   const float* q_select = nullptr;
   if (L->ddqn) {   // double DQN: a* = argmax Q_online(s') from the online net as it stands before this step's updates
     qlx_model* on = L->online;
@@ -333,22 +351,35 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
     launch_select_actions(s, N, kActions, step_before, L->p.epsilon_pure_random_steps, L->d_eps, L->eps_len, L->p.epsilon_min,
                           L->p.learner_seed, (uint32_t)L->rank * N, (uint32_t)L->vec_steps, L->online->w.q, L->d_actions);
   }
+  debug_sync(s, "act + select");
   L->step_count += N;
   // ---- env step (physics + frame) and replay push
   {
     ProfScope ps(&L->prof, "env_step", s, 7190.0 * N);   // state r/w + new frame + action/reward/done
     env_launch_step(L->env, L->d_actions, L->d_rewards, L->d_dones);
   }
+  debug_sync(s, "env_step");
   {
     ProfScope ps(&L->prof, "replay_push", s, 2.0 * 7056.0 * N + 10.0 * N);   // frame read + write + metadata
     replay_launch_push(L->rb, L->env, s, L->d_actions, L->d_rewards, L->d_dones);
     if (L->per) per_launch_push(s, L->prio.leaves(), L->rb->cap, L->rb->total - N, N, L->prio.d_max);
   }
+  debug_sync(s, "replay_push");
   {
     ProfScope ps(&L->prof, "episode_reset", s);
     launch_episode_book(s, N, L->d_rewards, L->d_dones, L->env->d_ep_steps, L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
                         (uint32_t)L->p.episode_reward_history_buffer_len, L->d_book, L->d_reset);
     env_launch_reset(L->env, L->d_reset, 1);
+  }
+  debug_sync(s, "episode book + reset");
+  if (L->comm && L->world > 1) {   // global solved(): tiny all-reduce of the episode statistics, every vector step
+    hipLaunchKernelGGL(k_book_local, dim3(1), dim3(64), 0, s, L->d_book, L->d_hist, (uint32_t)L->p.episode_reward_history_buffer_len,
+                       L->d_gsum, L->d_gmin);
+    QLX_HIP(hipGetLastError());
+    ncclResult_t r = ncclAllReduce(L->d_gsum, L->d_gsum, 3, ncclFloat, ncclSum, L->comm, s);
+    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    r = ncclAllReduce(L->d_gmin, L->d_gmin, 1, ncclFloat, ncclMin, L->comm, s);
+    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   }
   // ---- training updates
   const uint64_t ua = L->p.update_after_actions;
@@ -368,6 +399,7 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
         replay_launch_sample(L->rb, s, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank, L->B, L->d_idx);
       }
     }
+    debug_sync(s, "sample");
     learner_targets(L, U);
     for (uint32_t u = 0; u < U; ++u) learner_update(L, u);
     if (L->per) {
@@ -521,7 +553,7 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
     qlx_model_destroy(L->target);
     void* ptrs[] = {L->d_actions, L->d_rewards, L->d_dones, L->d_reset, (void*)L->d_obs_table, L->d_eps, L->d_ep_reward,
                     L->d_hist, L->d_book, L->d_idx, (void*)L->d_tab_s, (void*)L->d_tab_sn, L->d_bact, L->d_brew,
-                    L->d_bdone, L->d_losses, L->d_targets};
+                    L->d_bdone, L->d_losses, L->d_targets, L->d_gsum, L->d_gmin};
     for (void* p : ptrs) (void)hipFree(p);
     L->prio.release();
     (void)hipStreamDestroy(L->stream);
@@ -628,6 +660,15 @@ int32_t qlx_learner_stats_get(qlx_learner* L, qlx_learner_stats* out) {
     float mn = hist.empty() ? 0.0f : hist[0];
     for (float v : hist) mn = std::min(mn, v);
     out->solved = (!hist.empty() && b.running_reward >= goal && mn >= goal * L->p.lowest_episode_reward_goal_threshold_pct) ? 1 : 0;
+    if (L->comm && L->world > 1) {
+      // data parallel: solved over all ranks' episodes (as of the last vector step) = mean of the ranks' running rewards
+      // >= goal and the smallest episode reward of any rank's history >= goal * pct, every rank with a history
+      float gs[3], gm;
+      QLX_HIP(hipMemcpy(gs, L->d_gsum, sizeof(gs), hipMemcpyDeviceToHost));
+      QLX_HIP(hipMemcpy(&gm, L->d_gmin, sizeof(gm), hipMemcpyDeviceToHost));
+      out->solved = (gs[1] == (float)L->world && gs[0] / (float)L->world >= goal &&
+                     gm >= goal * L->p.lowest_episode_reward_goal_threshold_pct) ? 1 : 0;
+    }
     float loss = 0.0f;
     if (L->last_updates) QLX_HIP(hipMemcpy(&loss, L->d_losses + L->last_updates - 1, 4, hipMemcpyDeviceToHost));
     out->last_loss = loss;
@@ -739,7 +780,7 @@ static void learner_step_full(qlx_learner* L, bool train) {
   Book b;   // solved() after an episode ended in this step (:226-230)
   QLX_HIP(hipMemcpyAsync(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost, L->stream));
   QLX_HIP(hipStreamSynchronize(L->stream));
-  if (b.episode_count != L->seen_episodes) {
+  if (b.episode_count != L->seen_episodes || (L->comm && L->world > 1)) {
     L->seen_episodes = b.episode_count;
     qlx_learner_stats st{};
     const int32_t rc = qlx_learner_stats_get(L, &st);
@@ -782,6 +823,27 @@ int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const
     for (hipEvent_t* e : {&L->ev_dense, &L->ev_reduced}) QLX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     L->world = world;
     L->rank = rank;
+    QLX_HIP(hipMalloc(&L->d_gsum, 3 * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_gmin, sizeof(float)));
+    // rank 0's online weights, Adam slots and step count on every rank (one broadcast of the initial
+    // weights), and the target net = the online net as in SelfDrivingQLearner::new (self_driving_tf_q_learner.rs:94-116)
+    qlx_model* on = L->online;
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    int64_t* d_iter = nullptr;
+    QLX_HIP(hipMalloc(&d_iter, sizeof(int64_t)));
+    QLX_HIP(hipMemcpy(d_iter, &on->iterations, sizeof(int64_t), hipMemcpyHostToDevice));
+    for (float* buf : {on->d_params, on->d_m, on->d_v}) {
+      const ncclResult_t rb = ncclBroadcast(buf, buf, (size_t)kNumParams, ncclFloat, 0, L->comm, L->stream);
+      QLX_CHECK(rb == ncclSuccess, QLX_E_COMM, std::string("ncclBroadcast: ") + ncclGetErrorString(rb));
+    }
+    const ncclResult_t ri = ncclBroadcast(d_iter, d_iter, 1, ncclInt64, 0, L->comm, L->stream);
+    QLX_CHECK(ri == ncclSuccess, QLX_E_COMM, std::string("ncclBroadcast: ") + ncclGetErrorString(ri));
+    QLX_HIP(hipMemcpyAsync(L->target->d_params, on->d_params, kNumParams * sizeof(float), hipMemcpyDeviceToDevice, L->stream));
+    model_pack(on);
+    model_pack(L->target);
+    QLX_HIP(hipStreamSynchronize(L->stream));
+    QLX_HIP(hipMemcpy(&on->iterations, d_iter, sizeof(int64_t), hipMemcpyDeviceToHost));
+    QLX_HIP(hipFree(d_iter));
   });
 }
 

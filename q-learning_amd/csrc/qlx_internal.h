@@ -150,5 +150,7 @@ constexpr uint64_t kH1 = 0x9E3779B97F4A7C15ull, kH2 = 0xC2B2AE3D27D4EB4Full, kH3
 int current_device_checked(int device);
 // hipFuncAttributeMaxDynamicSharedMemorySize for `kernel` on the current device, once per (device, kernel, size)
 void set_lds_limit(const void* kernel, size_t bytes);
+// QLX_DEBUG_SYNC=1: synchronise `s` and throw naming `what` if a launch before it failed (no-op otherwise)
+void debug_sync(hipStream_t s, const char* what);
 
 }  // namespace qlx

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_fc2(Fc2Args A) {
       mx = fmaxf(fmaxf(q0, q1), q2);
     }
     const float r = A.rewards[b];
-    A.y_out[b] = A.dones[b] ? r : r + mx * A.gamma;
+    A.y_out[b] = A.dones[b] ? r : __fadd_rn(r, __fmul_rn(mx, A.gamma));   // two roundings, as the reference (add_arrays after array_mul)
   }
 }
 

@@ -339,6 +339,7 @@ template <class P>
 static void launch(const P& p, hipStream_t s) {
   hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), s, p);
   QLX_HIP(hipGetLastError());
+  debug_sync(s, __PRETTY_FUNCTION__);
 }
 
 template <class P1, class P2, class S>
@@ -347,6 +348,7 @@ static void launch_pair(const P1& p1, const P2& p2, const S& side, hipStream_t s
   hipLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, p1, p2,
                      side);
   QLX_HIP(hipGetLastError());
+  debug_sync(s, __PRETTY_FUNCTION__);
 }
 
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
@@ -392,6 +394,7 @@ void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s) {
     default: hipLaunchKernelGGL(k_head32<3>, g, blk, 0, s, a); break;
   }
   QLX_HIP(hipGetLastError());
+  debug_sync(s, "k_head32");
 }
 
 void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
@@ -413,6 +416,7 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
     f32_head(3, a, B, s);
     hipLaunchKernelGGL(k_dz4_32, dim3((B * 128 + 255) / 256), dim3(256), 0, s, w.fa4, p + voff(8), actions, w.gs, B, w.fdz4);
     QLX_HIP(hipGetLastError());
+    debug_sync(s, "k_dz4_32");
   }
   {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its three leading blocks
     ProfScope ps(m->prof, "f32_fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
@@ -454,6 +458,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     const int total = R.count[0] + R.count[1] + R.count[2];
     hipLaunchKernelGGL(k_wreduce32, dim3((total + 255) / 256), dim3(256), 0, s, R);
     QLX_HIP(hipGetLastError());
+    debug_sync(s, "k_wreduce32");
   }
 }
 
@@ -479,6 +484,7 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
   seg_tables(A.seg_first, A.off);
   hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
   QLX_HIP(hipGetLastError());
+  debug_sync(s, "k_norm32");
 }
 
 void f32_adam(qlx_model* m, hipStream_t s, float scale) {
@@ -494,6 +500,7 @@ void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
   hipLaunchKernelGGL(k_adam32, dim3(2048), dim3(256), 0, s, a);
   QLX_HIP(hipGetLastError());
+  debug_sync(s, "k_adam32");
   m->iterations = t;
 }
 

@@ -222,7 +222,7 @@ struct NoSide {
 //   conv dgrad      k = (kh, kw, oc) over the valid taps                                   fc1 dgrad   k = n
 //   weight grads    r = (b, oh, ow) ascending inside a sample chunk; fc1 / fc2 over b ascending, no chunks
 
-// conv1 forward: frames (u8, s2d layout, table[b * 4 + slot]) -> a1 [B][20][20][32] = relu(z + b0).
+// conv1 forward: frames (u8, s2d layout, table[b * 4 + slot]; a null entry is the zero frame) -> a1 [B][20][20][32] = relu(z + b0).
 // Slab s = kh; k = c * 8 + kw.  A row (b, oh, ow): 4 pixels kw = 4h .. 4h+3 of slot c are one aligned u32.
 struct PConv1Fwd {
   static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
@@ -240,6 +240,7 @@ struct PConv1Fwd {
     const int b = row / 400, p = row - b * 400, oh = p / 20, ow = p - oh * 20;
     const int c = k >> 3, h = (k >> 2) & 1;
     const uint8_t* f = table[b * 4 + c];
+    if (!f) return zero4();   // a ring slot before the episode's first frames: the zero frame (replay_dev.h)
     return u8x4(*reinterpret_cast<const uint32_t*>(f + ((oh + (kh >> 2)) * kBlocks + ow + h) * 16 + (kh & 3) * 4));
   }
   __device__ f32x4 ldB(int, int kh, int col, int k) const {   // W0[kh][kw][c][oc], k = c * 8 + kw
@@ -492,6 +493,7 @@ struct PConv1Wgrad {
     const int kh = row >> 5, c = (row >> 3) & 3, h = (row >> 2) & 1;
     const int bl = r / P, p = r - bl * P, oh = p / 20, ow = p - oh * 20, b = z * SC + bl;
     const uint8_t* f = table[b * 4 + c];
+    if (!f) return zero4();
     return u8x4(*reinterpret_cast<const uint32_t*>(f + ((oh + (kh >> 2)) * kBlocks + ow + h) * 16 + (kh & 3) * 4));
   }
   __device__ f32x4 ldB(int z, int s, int col, int k) const {

@@ -1,0 +1,112 @@
+// Host-side address check of the fp32 GEMM policies (qnet32_kernels.h): every operand load and epilogue store a
+// launch of qnet32.hip would issue is replayed on the CPU against host buffers of exactly the device workspace
+// sizes, under AddressSanitizer.  Dev tool (no GPU needed):
+//   hipcc --offload-host-only -x hip -I q-learning_amd/csrc -I include -fsanitize=address -g -O1 \
+//         scripts/q32_host_check.hip -o /tmp/q32_host_check && /tmp/q32_host_check 32 128
+#include <hip/hip_runtime.h>
+#undef __device__
+#define __device__ __attribute__((host, device))
+#include "qnet32_kernels.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace qlx;
+using namespace qlx::q32;
+
+constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
+using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3>;
+using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
+using PConv1WgradT = PConv1Wgrad<kSC1>;
+
+static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
+
+static long checks = 0;
+
+template <class P>
+static void replay(const P& p, const char* name) {
+  using OA = Opnd<P::BM, P::A_KMAJ>;
+  using OB = Opnd<P::BN, P::B_KMAJ>;
+  constexpr int T = P::WM * P::WN * 64;
+  constexpr int TM = P::BM / (P::WM * 16), TN = P::BN / (P::WN * 16);
+  volatile float sink = 0.0f;
+  for (int lb = 0; lb < p.g.blocks(); ++lb) {
+    int tm, tn, z;
+    p.decode(lb, tm, tn, z);
+    const int row0 = tm * P::BM, col0 = tn * P::BN;
+    const int ns = p.nslabs(z);
+    for (int s = 0; s < ns; ++s) {
+      for (int idx = 0; idx < OA::F4; ++idx) {
+        int r, k;
+        OA::coord(idx, r, k);
+        const f32x4 v = p.ldA(z, s, row0 + r, k);
+        sink = sink + v[0];
+        ++checks;
+      }
+      for (int idx = 0; idx < OB::F4; ++idx) {
+        int r, k;
+        OB::coord(idx, r, k);
+        const f32x4 v = p.ldB(z, s, col0 + r, k);
+        sink = sink + v[0];
+        ++checks;
+      }
+    }
+    for (int wave = 0; wave < T / 64; ++wave) {
+      const int wm = wave % P::WM, wn = wave / P::WM;
+      for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j)
+          for (int lane = 0; lane < 64; ++lane)
+            p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), zero4());
+    }
+    if constexpr (P::BIAS) {
+      if (tm == 0)
+        for (int t = 0; t < P::BN; ++t) p.epi_bias(z, col0 + t, 0.0f);
+    }
+  }
+  printf("%-14s blocks %6d ok\n", name, p.g.blocks());
+}
+
+template <class T>
+static T* buf(size_t n) { return static_cast<T*>(std::calloc(n, sizeof(T))); }
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 32;       // training batch
+  const int n = argc > 2 ? atoi(argv[2]) : B;        // forward batch (target pass)
+  const int C = n;                                    // forward chunk = whole pass here
+  // params in Keras layouts, exact sizes
+  float* w0 = buf<float>(8 * 8 * 4 * 32); float* b0 = buf<float>(32);
+  float* w1 = buf<float>(4 * 4 * 32 * 64); float* b1 = buf<float>(64);
+  float* w2 = buf<float>(3 * 3 * 64 * 64); float* b2 = buf<float>(64);
+  float* w3 = buf<float>(3136 * 512); float* b3 = buf<float>(512);
+  // frames: every table entry its own 7,056-byte allocation
+  const int F = std::max(B, n);
+  std::vector<const uint8_t*> table(F * 4);
+  for (size_t i = 0; i < table.size(); ++i)   // every 5th entry null: a ring slot before an episode's first frame
+    table[i] = i % 5 == 3 ? nullptr : buf<uint8_t>(kFramePix);
+  const uint8_t* const* tab = table.data();
+  float* a1 = buf<float>((size_t)C * 12800); float* a2 = buf<float>((size_t)C * 5184); float* a3 = buf<float>((size_t)C * 3136);
+  float* a4 = buf<float>((size_t)n * 512);
+  // forward over n
+  replay(PConv1Fwd{grid(n * 400, PConv1Fwd::BM, 32, 32, 1), tab, w0, b0, a1, n * 400}, "conv1_fwd");
+  replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
+  replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
+  replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
+  // backward over B (activations of a B-sample forward)
+  float* dz1 = buf<float>((size_t)B * 12800); float* dz2 = buf<float>((size_t)B * 5184);
+  float* dz3 = buf<float>((size_t)B * 3136); float* dz4 = buf<float>((size_t)B * 512);
+  float* s1 = buf<float>((size_t)((B + kSC1 - 1) / kSC1) * 257 * 32);
+  float* s2 = buf<float>((size_t)((B + kSC2 - 1) / kSC2) * 513 * 64);
+  float* s3 = buf<float>((size_t)((B + kSC3 - 1) / kSC3) * 577 * 64);
+  float* gw3 = buf<float>(3136 * 512); float* gb3 = buf<float>(512);
+  replay(PFc1Wgrad{grid(3136, 64, 512, 64, 1), a3, dz4, gw3, gb3, B}, "fc1_wgrad");
+  replay(PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, w3, a3, dz3, B}, "fc1_dgrad");
+  const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
+  replay(PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad");
+  replay(PConv3Wgrad{grid(576, 64, 64, 64, z3), a2, dz3, s3, B}, "conv3_wgrad");
+  replay(PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad");
+  replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
+  replay(PConv1WgradT{grid(256, PConv1WgradT::BM, 32, 32, z1), tab, dz1, s1, B}, "conv1_wgrad");
+  printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
+  return 0;
+}

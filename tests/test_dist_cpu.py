@@ -87,3 +87,19 @@ def test_bench_control_single_process():
     c = bench.Control()
     assert c.world == 1 and c.max(3.5) == 3.5 and c.bcast_bytes(b"x") == b"x"
     c.barrier()
+
+
+@pytest.mark.timeout(300)
+def test_bench_spawns_ranks_and_runs_control_plane():
+    """`bench.py --gpus 2` without a torch.distributed.run environment starts two rank processes itself (before any GPU
+    call) and their gloo control plane agrees: world 2, max / sum over ranks, rank 0's unique id on both ranks."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--control-only"],
+                         capture_output=True, text=True, env=env, timeout=240, check=True)
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, out.stdout
+    r = json.loads(line[0])
+    assert r == {"world": 2, "max_rank": 1.0, "sum_ones": 2.0, "uid_ok": True}
