@@ -63,6 +63,8 @@ def default_params(**kw):
                       env_seed=0x51A5EED, learner_seed=1, init_seed=2, rank=0, flags=0, per_alpha=0.6,
                       per_beta=0.4, per_eps=1e-6, qnet_precision=0, stats_after_steps=25_000, checkpoint_file=b"")
     for k, v in kw.items():
+        if k == "checkpoint_file" and isinstance(v, str):
+            v = v.encode()
         setattr(p, k, v)
     return p
 

@@ -183,20 +183,25 @@ def test_f32_c1_reference_loop_golden():
 def test_stats_events_and_checkpoint(tmp_path):
     """stats_after_steps (self_driving_tf_q_learner.rs:204-212): the learner writes its checkpoint and the
     learning_update_log once per vector step that crosses a multiple - same event count as the oracle; the file
-    holds the online weights of that moment and the log text equals the oracle's formatting of the same state."""
+    holds the online weights of that moment and the log text is the learning_update_log of that moment."""
     qlx = _qlx()
     path = str(tmp_path / "ql.ckpt")
     gpu, ref = make(32, 32, stats_after_steps=100, checkpoint_file=path, max_steps_per_episode=60, update_after_actions=8)
+    seen = 0
     for v in range(20):
         gpu.vector_step()
         ref.vector_step()
-    assert gpu.stats_events() == ref.stats_events() >= 6
-    m2 = qlx.DeepQLearningModel(seed=99)
-    m2.read_checkpoint(path)
-    for var in range(10):
-        assert same(m2.get(var), gpu.model.get(var))
-    log = gpu.last_log()
-    assert log == gpu.learning_update_log() and "reward_distribution" in log
+        assert gpu.stats_events() == ref.stats_events(), v
+        if gpu.stats_events() > seen:
+            seen = gpu.stats_events()
+            log = gpu.last_log()
+            assert log == gpu.learning_update_log() and "reward_distribution" in log
+            m2 = qlx.DeepQLearningModel(seed=99)
+            m2.read_checkpoint(path)
+            for var in range(10):
+                assert same(m2.get(var), gpu.model.get(var))
+            m2.close()
+    assert seen >= 6
 
 
 def test_bf16_pure_random_phase_parity():
