@@ -759,14 +759,23 @@ static void learner_stats_event(qlx_learner* L) {
     const int32_t rc = qlx_model_write_checkpoint(L->online, path);
     QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
   }
-  size_t n = 0;
-  int32_t rc = qlx_learner_update_log(L, nullptr, 0, &n);
-  QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
-  std::string text(n + 1, '\0');
-  rc = qlx_learner_update_log(L, &text[0], text.size(), &n);
-  QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
-  text.resize(n);
-  L->last_log = text;
+  Book b;
+  QLX_HIP(hipStreamSynchronize(L->stream));
+  QLX_HIP(hipMemcpy(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost));
+  if (b.hist_len == 0) {
+    // the reference's log asserts a finished episode (replay_buffer.rs:105-118 avg/min_episode_reward) and would panic;
+    // the library logs the counters instead and keeps running
+    L->last_log = "episode: 0, steps: " + std::to_string(L->step_count) + " (no finished episode yet)";
+  } else {
+    size_t n = 0;
+    int32_t rc = qlx_learner_update_log(L, nullptr, 0, &n);
+    QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+    std::string text(n + 1, '\0');
+    rc = qlx_learner_update_log(L, &text[0], text.size(), &n);
+    QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
+    text.resize(n);
+    L->last_log = text;
+  }
   L->stats_events += 1;
   if (L->log_cb) L->log_cb(L->last_log.c_str(), L->log_user);
 }
