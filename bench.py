@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md: f32-input MFMA, bf16)
+MIN_PREFILL = 400                                # vector steps before timing (steady state, see Run)
 PEAK_HBM_GBS = 8000.0                            # HBM3E
 # per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
 FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
@@ -193,14 +194,16 @@ class Run:
                 uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
                 L.dist_init(ctl.world, ctl.rank, uid)
             # steady state: replay at capacity and past the pure-random phase, whatever --warmup is
-            prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
+            # (and at least MIN_PREFILL vector steps, so every env has finished episodes: the first ball loss comes
+            # ~160 env-steps after launch)
+            prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N), MIN_PREFILL)
             log(f"{precision}: prefill {prefill} vector steps")
             L.prefill(prefill)
             log(f"{precision}: warmup {max(warmup, 1)} vector steps")
             L.run(max(warmup, 1))
             L.sync()
             s = L.stats()
-            assert s["replay_len"] == args.replay, s
+            assert s["replay_len"] == args.replay and s["episode_count"] > 0, s
             assert s["step_count"] >= p.epsilon_pure_random_steps, s
             self.prefill = prefill
             log(f"{precision}: profile pass")
