@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md: f32-input MFMA, bf16)
-MIN_PREFILL = 400                                # vector steps before timing (steady state, see Run)
+STEADY_RUN, MAX_DESYNC = 24, 4000                # steady state before timing: see Run._desync
 PEAK_HBM_GBS = 8000.0                            # HBM3E
 # per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
 FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
@@ -56,7 +56,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10, help="timed vector steps")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed training vector steps after the replay prefill")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed training vector steps after the steady-state prefill")
     ap.add_argument("--envs", type=int, default=8192, help="envs per GPU (C3: 8192; C2: 1024; C4: 4096 x 8)")
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--replay-ratio", type=int, default=8, help="samples per env-step (reference: 32 per 4 steps)")
@@ -194,12 +194,13 @@ class Run:
                 uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
                 L.dist_init(ctl.world, ctl.rank, uid)
             # steady state: replay at capacity and past the pure-random phase, whatever --warmup is
-            # (and at least MIN_PREFILL vector steps, so every env has finished episodes: the first ball loss comes
-            # ~160 env-steps after launch)
-            prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N), MIN_PREFILL)
+            prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
             log(f"{precision}: prefill {prefill} vector steps")
             L.prefill(prefill)
-            log(f"{precision}: warmup {max(warmup, 1)} vector steps")
+            # ... and episode ends spread over the steps: all envs launch together, so their first episodes end
+            # together (the first ball loss comes ~160 env-steps after launch); keep stepping (no updates) until
+            # episodes ended in each of the last STEADY_RUN vector steps, as they do in a long run
+            prefill += self._desync(L, p)
             L.run(max(warmup, 1))
             L.sync()
             s = L.stats()
@@ -213,6 +214,17 @@ class Run:
             log(f"{precision}: {self.value():.1f} env-steps/s")
         finally:
             L.close()
+
+    def _desync(self, L, p):
+        run, n, last = 0, 0, L.stats()["episode_count"]
+        while run < STEADY_RUN and n < MAX_DESYNC:
+            L.prefill(1)
+            n += 1
+            e = L.stats()["episode_count"]
+            run = run + 1 if e > last else 0
+            last = e
+        log(f"{self.precision}: {n} more vector steps until episodes end every step ({run} in a row)")
+        return n
 
     def _profile(self):
         """Event-timed per-scope device time over profile_steps vector steps (every launch bracketed by events, so
