@@ -89,8 +89,10 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
   float* Bs1 = Bs0 + OB::FLOATS;
-  f32x4 ra[NA], rb[NB];
-  auto load = [&](int s) {
+  // two register sets: slab s + 2 is in flight from global memory while slab s is multiplied from LDS and slab
+  // s + 1 waits in registers for its LDS buffer (two slabs of MFMA work cover a load's latency)
+  f32x4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
+  auto load = [&](int s, f32x4(&ra)[NA], f32x4(&rb)[NB]) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + i * T;
@@ -110,7 +112,9 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
       }
     }
   };
-  auto store = [&](float* as, float* bs) {
+  auto store = [&](int s, const f32x4(&ra)[NA], const f32x4(&rb)[NB]) {
+    float* as = (s & 1) ? As1 : As0;
+    float* bs = (s & 1) ? Bs1 : Bs0;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + i * T;
@@ -137,14 +141,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
   float bsum = 0.0f;
   const bool do_bias = P::BIAS && tm == 0 && tid < P::BN;
-  if (ns > 0) {
-    load(0);
-    store(As0, Bs0);
-  }
-  lds_barrier();
-  for (int s = 0; s < ns; ++s) {
-    const bool next = s + 1 < ns;
-    if (next) load(s + 1);
+  auto compute = [&](int s) {
     const float* a = (s & 1) ? As1 : As0;
     const float* b = (s & 1) ? Bs1 : Bs0;
     if (P::BIAS && do_bias)
@@ -162,8 +159,23 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (next) store((s & 1) ? As0 : As1, (s & 1) ? Bs0 : Bs1);
+  };
+  // iteration s: x holds slab s + 1, y is free
+  auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
+    if (s + 2 < ns) load(s + 2, ya, yb);
+    compute(s);
+    if (s + 1 < ns) store(s + 1, xa, xb);
     lds_barrier();
+  };
+  if (ns > 0) {
+    load(0, ra1, rb1);
+    store(0, ra1, rb1);
+  }
+  if (ns > 1) load(1, ra0, rb0);
+  lds_barrier();
+  for (int s = 0; s < ns; s += 2) {
+    iter(s, ra0, rb0, ra1, rb1);
+    if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -198,17 +210,19 @@ __global__ __launch_bounds__(256) void k_gemm32(const P p) {
   gemm_body(p, xcd_logical(blockIdx.x, gridDim.x), lds);
 }
 
-// two independent GEMMs in one grid (logical blocks [0, G1) run P1), plus `side` leading blocks running S
+// two independent GEMMs in one grid (hardware blocks [S::BLOCKS, S::BLOCKS + G1) run P1), plus `side` leading blocks
+// running S
 template <class P1, class P2, class S>
 __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, const S side) {
   extern __shared__ float lds[];
   const int b = blockIdx.x;
   if (b < S::BLOCKS) { side.run(b, lds); return; }
-  const int G = gridDim.x - S::BLOCKS;
-  const int lb = xcd_logical(b - S::BLOCKS, G);
+  // the problems take consecutive hardware blocks (so both spread over all eight XCDs, P1 - the longer weight-gradient
+  // tiles - dispatched first); inside each problem the XCD-grouped tile order
+  const int G = gridDim.x - S::BLOCKS, h = b - S::BLOCKS;
   const int g1 = p1.g.blocks();
-  if (lb < g1) gemm_body(p1, lb, lds);
-  else gemm_body(p2, lb - g1, lds);
+  if (h < g1) gemm_body(p1, xcd_logical(h, g1), lds);
+  else gemm_body(p2, xcd_logical(h - g1, G - g1), lds);
 }
 
 struct NoSide {
