@@ -187,6 +187,159 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   }
 }
 
+// Persistent form of gemm_body: the block runs the output tiles ids[0 .. nt) (logical tile numbers of P, a list the
+// host scheduler built) as ONE pipeline - the loads of the next tile's first slabs are in flight while the current
+// tile finishes and stores its epilogue, so no tile pays a cold start.  Per output the arithmetic is gemm_body's
+// (same fmaf chain in the same order): results are bit-identical.
+template <class P>
+__device__ __forceinline__ void gemm_persistent(const P& p, const int* ids, int nt, float* lds) {
+  using OA = Opnd<P::BM, P::A_KMAJ>;
+  using OB = Opnd<P::BN, P::B_KMAJ>;
+  constexpr int T = P::WM * P::WN * 64;
+  constexpr int TM = P::BM / (P::WM * 16), TN = P::BN / (P::WN * 16);
+  static_assert(TM * P::WM * 16 == P::BM && TN * P::WN * 16 == P::BN, "tile shape");
+  constexpr int NA = (OA::F4 + T - 1) / T, NB = (OB::F4 + T - 1) / T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % P::WM, wn = wave / P::WM;
+  float* As0 = lds;
+  float* As1 = lds + OA::FLOATS;
+  float* Bs0 = lds + 2 * OA::FLOATS;
+  float* Bs1 = Bs0 + OB::FLOATS;
+  struct Pos {
+    int j, s, ns, tm, row0, col0, z;
+  };
+  auto tile = [&](int j) {
+    Pos q{j, 0, 0, 0, 0, 0, 0};
+    if (j < nt) {
+      int tm, tn, z;
+      p.decode(ids[j], tm, tn, z);
+      q.ns = p.nslabs(z);
+      q.tm = tm;
+      q.row0 = tm * P::BM;
+      q.col0 = tn * P::BN;
+      q.z = z;
+    }
+    return q;
+  };
+  auto next = [&](const Pos& q) {
+    if (q.j >= nt) return q;
+    if (q.s + 1 < q.ns) {
+      Pos r = q;
+      r.s += 1;
+      return r;
+    }
+    return tile(q.j + 1);
+  };
+  f32x4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
+  auto load = [&](const Pos& q, f32x4(&ra)[NA], f32x4(&rb)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T;
+      if (OA::F4 % T == 0 || idx < OA::F4) {
+        int r, k;
+        OA::coord(idx, r, k);
+        ra[i] = p.ldA(q.z, q.s, q.row0 + r, k);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + i * T;
+      if (OB::F4 % T == 0 || idx < OB::F4) {
+        int r, k;
+        OB::coord(idx, r, k);
+        rb[i] = p.ldB(q.z, q.s, q.col0 + r, k);
+      }
+    }
+  };
+  auto store = [&](int buf, const f32x4(&ra)[NA], const f32x4(&rb)[NB]) {
+    float* as = buf ? As1 : As0;
+    float* bs = buf ? Bs1 : Bs0;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T;
+      if (OA::F4 % T == 0 || idx < OA::F4) {
+        int r, k;
+        OA::coord(idx, r, k);
+        OA::put(as, r, k, ra[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + i * T;
+      if (OB::F4 % T == 0 || idx < OB::F4) {
+        int r, k;
+        OB::coord(idx, r, k);
+        OB::put(bs, r, k, rb[i]);
+      }
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  float bsum = 0.0f;
+  auto compute = [&](int buf, const Pos& q) {
+    const float* a = buf ? As1 : As0;
+    const float* b = buf ? Bs1 : Bs0;
+    if (P::BIAS && q.tm == 0 && tid < P::BN)
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) bsum = bsum + OB::at(b, tid, k);
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](const Pos& q) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        p.epi(q.z, q.row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, q.col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
+        acc[i][j] = zero4();
+      }
+    if constexpr (P::BIAS) {
+      if (q.tm == 0 && tid < P::BN) p.epi_bias(q.z, q.col0 + tid, bsum);
+    }
+    bsum = 0.0f;
+  };
+  Pos pc = tile(0);
+  if (pc.j >= nt) return;
+  Pos p1 = next(pc), p2 = next(p1);
+  load(pc, ra1, rb1);
+  store(0, ra1, rb1);
+  if (p1.j < nt) load(p1, ra0, rb0);
+  lds_barrier();
+  int t = 0;
+  // x holds p1's slab, y is free; loads of p2 fly while pc is multiplied and p1 waits for its LDS buffer
+  auto step = [&](f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
+    if (p2.j < nt) load(p2, ya, yb);
+    compute(t & 1, pc);
+    if (pc.s + 1 == pc.ns) epilogue(pc);
+    if (p1.j < nt) store((t + 1) & 1, xa, xb);
+    lds_barrier();
+    pc = p1;
+    p1 = p2;
+    p2 = next(p2);
+    ++t;
+  };
+  for (;;) {
+    step(ra0, rb0, ra1, rb1);
+    if (pc.j >= nt) break;
+    step(ra1, rb1, ra0, rb0);
+    if (pc.j >= nt) break;
+  }
+}
+
 template <class P>
 constexpr size_t gemm_lds_bytes() {
   return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ>::FLOATS + Opnd<P::BN, P::B_KMAJ>::FLOATS) * sizeof(float);
@@ -195,7 +348,7 @@ constexpr size_t gemm_lds_bytes() {
 // grid layout shared by the policies: tile index fastest (col tile, then row tile), then z
 struct Grid {
   int tiles_m, tiles_n, nz;
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const {
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const {
     tn = lb % tiles_n;
     const int q = lb / tiles_n;
     tm = q % tiles_m;
@@ -225,6 +378,27 @@ __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, c
   else gemm_body(p2, xcd_logical(h - g1, G - g1), lds);
 }
 
+// persistent launches: block b runs the tile list ids[start[b] .. start[b + 1]) (host-built, see qnet32.hip Sched)
+template <class P>
+__global__ __launch_bounds__(256) void k_gemm32p(const P p, const int* start, const int* ids) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  gemm_persistent(p, ids + start[b], start[b + 1] - start[b], lds);
+}
+
+// two problems: blocks [S::BLOCKS, S::BLOCKS + g1blocks) run lists of P1, the rest lists of P2 (one start/ids table
+// over all non-side blocks; tile ids are each problem's own)
+template <class P1, class P2, class S>
+__global__ __launch_bounds__(256) void k_gemm32p_pair(const P1 p1, const P2 p2, const S side, const int* start, const int* ids,
+                                                      int g1blocks) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  if (b < S::BLOCKS) { side.run(b, lds); return; }
+  const int h = b - S::BLOCKS;
+  if (h < g1blocks) gemm_persistent(p1, ids + start[h], start[h + 1] - start[h], lds);
+  else gemm_persistent(p2, ids + start[h], start[h + 1] - start[h], lds);
+}
+
 struct NoSide {
   static constexpr int BLOCKS = 0;
   __device__ void run(int, float*) const {}
@@ -247,8 +421,8 @@ struct PConv1Fwd {
   const float* b0;
   float* a1;
   int M;             // B * 400
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return 8; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return 8; }
   __device__ f32x4 ldA(int, int kh, int row, int k) const {
     if (row >= M) return zero4();
     const int b = row / 400, p = row - b * 400, oh = p / 20, ow = p - oh * 20;
@@ -279,8 +453,8 @@ struct PConvFwd {
   const float* bias;
   float* out;        // [M][OC]
   int M;             // B * OH * OW
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return KS * KS * C / BK; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return KS * KS * C / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     if (row >= M) return zero4();
     const int tap = (s * BK) / C, c0 = (s * BK) % C, kh = tap / KS, kw = tap % KS;
@@ -307,8 +481,8 @@ struct PFc1Fwd {
   const float* b3;
   float* a4;
   int M;
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return 3136 / BK; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return 3136 / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     return row < M ? ld4(a3 + (size_t)row * 3136 + s * BK + k) : zero4();
   }
@@ -330,8 +504,8 @@ struct PFc1Dgrad {
   const float* a3;
   float* dz3;
   int M;
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return 512 / BK; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return 512 / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     return row < M ? ld4(dz4 + (size_t)row * 512 + s * BK + k) : zero4();
   }
@@ -356,8 +530,8 @@ struct PFc1Wgrad {
   float* dw3;
   float* db3;
   int B;
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return (B + BK - 1) / BK; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return (B + BK - 1) / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     const int b = s * BK + k;
     return (b < B && row < 3136) ? ld4(a3 + (size_t)b * 3136 + row) : zero4();
@@ -384,8 +558,8 @@ struct PConv3Dgrad {
   const float* a2;
   float* dz2;
   int M;              // B * 81
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return 18; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return 18; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     if (row >= M) return zero4();
     const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3, oc0 = (s & 1) * 32;
@@ -419,8 +593,8 @@ struct PConv2Dgrad {
   const float* a1;
   float* dz1;         // [B][20][20][32]
   int M;              // B * 100
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int nslabs(int) const { return 8; }
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return 8; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
     if (row >= M) return zero4();
     const int t = s >> 1, th = t >> 1, tw = t & 1, oc0 = (s & 1) * 32;
@@ -458,12 +632,12 @@ struct PConvWgrad {
   const float* dz;   // [B][OH][OW][OC]
   float* slab;
   int B;
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int rows_in(int z) const {
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int rows_in(int z) const {
     const int b0 = z * SC, b1 = b0 + SC < B ? b0 + SC : B;
     return (b1 - b0) * P;
   }
-  __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
+  __host__ __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
     const int r = s * BK + k;
     if (r >= rows_in(z)) return zero4();
@@ -495,12 +669,12 @@ struct PConv1Wgrad {
   const float* dz1;   // [B][20][20][32]
   float* slab;
   int B;
-  __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __device__ int rows_in(int z) const {
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int rows_in(int z) const {
     const int b0 = z * SC, b1 = b0 + SC < B ? b0 + SC : B;
     return (b1 - b0) * P;
   }
-  __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
+  __host__ __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
     const int r = s * BK + k;
     if (r >= rows_in(z)) return zero4();

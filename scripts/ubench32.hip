@@ -1,0 +1,173 @@
+// fp32 GEMM-core micro-benchmark (development tool, not part of the product): times the qnet32 layer policies at the
+// learner's batch sizes and a generic GEMM policy at several tile shapes, each launch alone on one stream (HIP events,
+// median of repeats).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include -I q-learning_amd/csrc scripts/ubench32.hip \
+//         -o scripts/ubench32 && ./scripts/ubench32
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "qnet32_kernels.h"
+
+using namespace qlx;
+using namespace qlx::q32;
+
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e = (x);                                                                        \
+    if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); }   \
+  } while (0)
+
+// C [M][N] = A [M][K] B [K][N], both row-major
+template <int BM_, int BN_, int WM_, int WN_>
+struct PGen {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
+  Grid g;
+  const float* A;
+  const float* Bm;
+  float* C;
+  int M, N, K;
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return K / BK; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const { return row < M ? ld4(A + (size_t)row * K + s * BK + k) : zero4(); }
+  __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(Bm + (size_t)(s * BK + k) * N + col); }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) C[(size_t)(row + r) * N + col] = v[r];
+  }
+};
+
+static float* dbuf(size_t n, uint32_t seed) {
+  std::vector<float> h(n);
+  std::mt19937 g(seed);
+  std::uniform_real_distribution<float> u(-1.0f, 1.0f);
+  for (auto& x : h) x = u(g);
+  float* d = nullptr;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+template <class F>
+static double time_us(F f, int reps = 15) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  f();
+  CK(hipDeviceSynchronize());
+  std::vector<float> t;
+  for (int i = 0; i < reps; ++i) {
+    CK(hipEventRecord(a, 0));
+    f();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    t.push_back(ms * 1e3f);
+  }
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
+
+template <class P>
+static void run1(const char* name, const P& p, double flop) {
+  CK(hipFuncSetAttribute((const void*)k_gemm32<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<P>()));
+  const double us = time_us([&] { hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), 0, p); });
+  printf("%-34s blocks %6d lds %6zu  %9.2f us  %7.2f TF  %5.1f %%\n", name, p.g.blocks(), gemm_lds_bytes<P>(), us,
+         flop / us / 1e6, flop / us / 1e6 / 157.3 * 100);
+}
+
+template <class P1, class P2>
+static void run2(const char* name, const P1& p1, const P2& p2, double flop) {
+  const size_t lds = std::max(gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>());
+  const double us = time_us([&] {
+    hipLaunchKernelGGL((k_gemm32_pair<P1, P2, NoSide>), dim3(p1.g.blocks() + p2.g.blocks()), dim3(256), lds, 0, p1, p2, NoSide{});
+  });
+  printf("%-34s blocks %6d lds %6zu  %9.2f us  %7.2f TF  %5.1f %%\n", name, p1.g.blocks() + p2.g.blocks(), lds, us,
+         flop / us / 1e6, flop / us / 1e6 / 157.3 * 100);
+}
+
+template <int BM, int BN, int WM, int WN>
+static void gen(int M, int N, int K, const float* A, const float* B, float* C) {
+  PGen<BM, BN, WM, WN> p{grid(M, BM, N, BN, 1), A, B, C, M, N, K};
+  char name[96];
+  snprintf(name, sizeof name, "gen %dx%dx%d t%dx%d w%dx%d", M, N, K, BM, BN, WM, WN);
+  run1(name, p, 2.0 * M * N * K);
+}
+
+int main(int argc, char** argv) {
+  const int Bs[2] = {1024, 8192};
+  // layer buffers sized for the larger batch
+  const int Bmax = 8192;
+  float* w = dbuf(1685667, 1);
+  float* a1 = dbuf((size_t)Bmax * 12800, 2);
+  float* a2 = dbuf((size_t)Bmax * 5184, 3);
+  float* a3 = dbuf((size_t)Bmax * 3136, 4);
+  float* a4 = dbuf((size_t)Bmax * 512, 5);
+  float* dz1 = dbuf((size_t)Bmax * 12800, 6);
+  float* dz2 = dbuf((size_t)Bmax * 5184, 7);
+  float* dz3 = dbuf((size_t)Bmax * 3136, 8);
+  float* dz4 = dbuf((size_t)Bmax * 512, 9);
+  float* slab = dbuf((size_t)2048 * 577 * 64, 10);
+  float* gw = dbuf((size_t)3136 * 513, 11);
+  // frames: one 7056-byte frame per (sample, slot)
+  uint8_t* frames = nullptr;
+  CK(hipMalloc(&frames, (size_t)Bmax * 4 * 7056));
+  CK(hipMemset(frames, 7, (size_t)Bmax * 4 * 7056));
+  std::vector<const uint8_t*> ht(Bmax * 4);
+  for (int i = 0; i < Bmax * 4; ++i) ht[i] = frames + (size_t)i * 7056;
+  const uint8_t** table = nullptr;
+  CK(hipMalloc(&table, ht.size() * sizeof(void*)));
+  CK(hipMemcpy(table, ht.data(), ht.size() * sizeof(void*), hipMemcpyHostToDevice));
+  const float* W0 = w;
+  const float* W1 = w + 8192 + 32;
+  const float* W2 = W1 + 32768 + 64;
+  const float* W3 = W2 + 36864 + 64;
+  for (int B : Bs) {
+    printf("--- B = %d\n", B);
+    run1("conv1_fwd", PConv1Fwd{grid(B * 400, PConv1Fwd::BM, 32, 32, 1), table, W0, W0 + 8192, a1, B * 400}, 2.0 * B * 400 * 32 * 256);
+    run1("conv2_fwd", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>{grid(B * 81, 64, 64, 64, 1), a1, W1, W1, a2, B * 81},
+         2.0 * B * 81 * 64 * 512);
+    run1("conv3_fwd", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>{grid(B * 49, 64, 64, 64, 1), a2, W2, W2, a3, B * 49},
+         2.0 * B * 49 * 64 * 576);
+    run1("fc1_fwd", PFc1Fwd{grid(B, PFc1Fwd::BM, 512, 64, 1), a3, W3, W3, a4, B}, 2.0 * B * 3136 * 512);
+    if (B > 1024) continue;
+    run1("fc1_wgrad", PFc1Wgrad{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B}, 2.0 * B * 3136 * 512);
+    run1("fc1_dgrad", PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, W3, a3, dz3, B}, 2.0 * B * 3136 * 512);
+    run2("fc1_bwd pair", PFc1Wgrad{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B}, PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, W3, a3, dz3, B},
+         4.0 * B * 3136 * 512);
+    run1("conv3_dgrad", PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, 2.0 * B * 49 * 64 * 576);
+    run1("conv3_wgrad", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, B / 16), a2, dz3, slab, B},
+         2.0 * B * 49 * 64 * 576);
+    run1("conv2_dgrad", PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, W1, a1, dz1, B * 100}, 2.0 * B * 81 * 64 * 512);
+    run1("conv2_wgrad", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, B / 16), a1, dz2, slab, B},
+         2.0 * B * 81 * 64 * 512);
+    run1("conv1_wgrad", PConv1Wgrad<4>{grid(256, 128, 32, 32, B / 4), table, dz1, slab, B}, 2.0 * B * 400 * 256 * 32);
+  }
+  printf("--- generic GEMM (A row-major, B row-major)\n");
+  {
+    const int M = 8192, N = 4096, K = 4096;
+    float* A = dbuf((size_t)65536 * 4 * 256, 20);
+    float* B = dbuf((size_t)K * N, 21);
+    float* C = dbuf((size_t)M * N, 22);
+    gen<64, 64, 2, 2>(M, N, K, A, B, C);
+    gen<128, 64, 2, 2>(M, N, K, A, B, C);
+    gen<128, 128, 2, 2>(M, N, K, A, B, C);
+    gen<64, 128, 2, 2>(M, N, K, A, B, C);
+    gen<128, 32, 4, 1>(M, N, K, A, B, C);
+    gen<32, 64, 2, 2>(M, N, K, A, B, C);
+    gen<64, 64, 2, 2>(65536, 64, 512, A, B, C);
+    gen<128, 64, 2, 2>(65536, 64, 512, A, B, C);
+    gen<64, 32, 4, 1>(65536 * 4, 32, 256, A, B, C);
+    gen<128, 32, 4, 1>(65536 * 4, 32, 256, A, B, C);
+  }
+  return 0;
+}
