@@ -75,7 +75,6 @@ struct qlx_model {
   int fc1bwd_map_B = -1, fc1bwd_grid = 0, fc1bwd_cap = 0;
   void* ws = nullptr;
   int ws_batch = 0;
-  void* f32_sched = nullptr;   // fp32 path: cached persistent tile lists per launch shape (qnet32.hip F32Sched)
   int last_batch = 0;
   qlx::ModelWs w;
   qlx::Profiler* prof = nullptr;   // set by the learner while profiling
@@ -136,7 +135,6 @@ void model_adam(qlx_model* m, hipStream_t s, float scale);
 
 // fp32 path (qnet32.hip), dispatched to by the model_* functions when m->f32
 void f32_workspace(qlx_model* m, int B);
-void f32_release(qlx_model* m);   // frees the fp32 path's cached launch tables
 void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
 void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s);   // mode 3 = training head
 void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,

@@ -338,192 +338,18 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   w.fgrad_batch = B;
 }
 
-// ---- persistent tile scheduling ----------------------------------------------------------------------------------
-// A launch runs as many blocks as fit on the chip at once (occupancy x CUs, at most one per tile); each block gets a
-// list of tiles and runs them as one pipeline (gemm_persistent).  Lists (built once per launch shape and cached in the
-// model): tiles are split into 8 contiguous logical ranges of about equal slab count, range x going to the blocks that
-// run on XCD x (hardware block b runs on XCD b % 8, so neighbouring tiles share an L2), and inside a range
-// longest-first onto the least loaded block.  Off by default (measured slower than hardware block dispatch on the
-// learner's shapes: 92.7K vs 102.8K env-steps/s at C3); QLX_F32_PERSISTENT=1 selects it.
-struct SchedEntry {
-  int* d = nullptr;   // start[G + 1] then ids[T]
-  int grid = 0, g1 = 0;
-};
-struct F32Sched {
-  std::map<std::tuple<const void*, int, int, int, int>, SchedEntry> m;
-  std::map<const void*, int> occ;
-};
-
-void f32_release(qlx_model* m) {
-  auto* S = static_cast<F32Sched*>(m->f32_sched);
-  if (!S) return;
-  for (auto& kv : S->m) (void)hipFree(kv.second.d);
-  delete S;
-  m->f32_sched = nullptr;
-}
-
-static bool persistent_on() {
-  static const bool on = [] {
-    const char* v = std::getenv("QLX_F32_PERSISTENT");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
-static int blocks_per_cu(F32Sched* S, const void* kern, size_t lds) {
-  auto it = S->occ.find(kern);
-  if (it != S->occ.end()) return it->second;
-  int nb = 0;
-  QLX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds));
-  nb = std::max(1, nb);
-  S->occ[kern] = nb;
-  return nb;
-}
-
-static int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    QLX_HIP(hipGetDevice(&dev));
-    QLX_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return n;
-}
-
 template <class P>
-static std::vector<int> tile_costs(const P& p) {
-  std::vector<int> c(p.g.blocks());
-  for (int lb = 0; lb < (int)c.size(); ++lb) {
-    int tm, tn, z;
-    p.decode(lb, tm, tn, z);
-    c[lb] = std::max(1, p.nslabs(z));
-  }
-  return c;
-}
-
-// lists of G blocks whose hardware ids start at b0; appends start offsets (relative to ids.size() at entry) and ids
-static void build_lists(const std::vector<int>& cost, int G, int b0, std::vector<int>& start, std::vector<int>& ids) {
-  const int T = (int)cost.size();
-  std::vector<std::vector<int>> lists(G);
-  std::vector<int> blocks_of[8];
-  for (int i = 0; i < G; ++i) blocks_of[(b0 + i) % 8].push_back(i);
-  int64_t total = 0;
-  for (int c : cost) total += c;
-  int t = 0;
-  int64_t done = 0;
-  int seen_blocks = 0;
-  for (int x = 0; x < 8; ++x) {
-    if (blocks_of[x].empty()) continue;
-    seen_blocks += (int)blocks_of[x].size();
-    const int64_t goal = total * seen_blocks / G;   // cumulative cost share up to and including XCD x
-    std::vector<int> range;
-    while (t < T && (done < goal || seen_blocks == G)) {
-      range.push_back(t);
-      done += cost[t];
-      ++t;
-    }
-    std::stable_sort(range.begin(), range.end(), [&](int a, int b) { return cost[a] > cost[b]; });
-    std::vector<int64_t> load(blocks_of[x].size(), 0);
-    for (int id : range) {
-      size_t best = 0;
-      for (size_t k = 1; k < load.size(); ++k)
-        if (load[k] < load[best]) best = k;
-      load[best] += cost[id];
-      lists[blocks_of[x][best]].push_back(id);
-    }
-  }
-  const int base = (int)ids.size();
-  for (int i = 0; i < G; ++i) {
-    std::sort(lists[i].begin(), lists[i].end());
-    start.push_back(base + (int)(ids.size() - base));
-    ids.insert(ids.end(), lists[i].begin(), lists[i].end());
-  }
-}
-
-static SchedEntry& upload(F32Sched* S, const std::tuple<const void*, int, int, int, int>& key, std::vector<int>& start,
-                          const std::vector<int>& ids, int grid, int g1, hipStream_t s) {
-  SchedEntry e;
-  e.grid = grid;
-  e.g1 = g1;
-  start.push_back((int)ids.size());
-  // ids are addressed relative to the ids array: shift the offsets past start[]
-  std::vector<int> buf(start.size() + ids.size());
-  for (size_t i = 0; i < start.size(); ++i) buf[i] = start[i];
-  std::copy(ids.begin(), ids.end(), buf.begin() + start.size());
-  QLX_HIP(hipMalloc(&e.d, buf.size() * sizeof(int)));
-  QLX_HIP(hipMemcpyAsync(e.d, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, s));
-  QLX_HIP(hipStreamSynchronize(s));
-  return S->m[key] = e;
-}
-
-static F32Sched* sched_of(qlx_model* m) {
-  if (!m->f32_sched) m->f32_sched = new F32Sched;
-  return static_cast<F32Sched*>(m->f32_sched);
-}
-
-template <class P>
-static void launch(qlx_model* m, const P& p, int extra, hipStream_t s) {
-  const size_t lds = gemm_lds_bytes<P>();
-  if (!persistent_on()) {
-    hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), lds, s, p);
-    QLX_HIP(hipGetLastError());
-    debug_sync(s, __PRETTY_FUNCTION__);
-    return;
-  }
-  F32Sched* S = sched_of(m);
-  const void* kern = (const void*)k_gemm32p<P>;
-  const auto key = std::make_tuple(kern, p.g.tiles_m, p.g.tiles_n, p.g.nz, extra);
-  auto it = S->m.find(key);
-  SchedEntry* e;
-  if (it != S->m.end()) {
-    e = &it->second;
-  } else {
-    const std::vector<int> cost = tile_costs(p);
-    const int G = std::min<int>((int)cost.size(), blocks_per_cu(S, kern, lds) * num_cus());
-    std::vector<int> start, ids;
-    build_lists(cost, G, 0, start, ids);
-    e = &upload(S, key, start, ids, G, G, s);
-  }
-  const int G = e->grid;
-  hipLaunchKernelGGL(k_gemm32p<P>, dim3(G), dim3(256), lds, s, p, (const int*)e->d, (const int*)e->d + G + 1);
+static void launch(qlx_model*, const P& p, int, hipStream_t s) {
+  hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), s, p);
   QLX_HIP(hipGetLastError());
   debug_sync(s, __PRETTY_FUNCTION__);
 }
 
 template <class P1, class P2, class S>
-static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side, int extra, hipStream_t s) {
+static void launch_pair(qlx_model*, const P1& p1, const P2& p2, const S& side, int, hipStream_t s) {
   const size_t lds = std::max(gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>());
-  if (!persistent_on()) {
-    hipLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, p1, p2,
-                       side);
-    QLX_HIP(hipGetLastError());
-    debug_sync(s, __PRETTY_FUNCTION__);
-    return;
-  }
-  F32Sched* Sc = sched_of(m);
-  const void* kern = (const void*)k_gemm32p_pair<P1, P2, S>;
-  const auto key = std::make_tuple(kern, p2.g.tiles_m, p2.g.tiles_n, p2.g.nz, extra);
-  auto it = Sc->m.find(key);
-  SchedEntry* e;
-  if (it != Sc->m.end()) {
-    e = &it->second;
-  } else {
-    const std::vector<int> c1 = tile_costs(p1), c2 = tile_costs(p2);
-    int64_t w1 = 0, w2 = 0;
-    for (int c : c1) w1 += c;
-    for (int c : c2) w2 += c;
-    const int slots = std::max(2, blocks_per_cu(Sc, kern, lds) * num_cus() - S::BLOCKS);
-    int G1 = (int)std::llround((double)slots * (double)w1 / (double)(w1 + w2));
-    G1 = std::max(1, std::min<int>({G1, (int)c1.size(), slots - 1}));
-    const int G2 = std::max(1, std::min<int>(slots - G1, (int)c2.size()));
-    std::vector<int> start, ids;
-    build_lists(c1, G1, S::BLOCKS, start, ids);
-    build_lists(c2, G2, S::BLOCKS + G1, start, ids);
-    e = &upload(Sc, key, start, ids, G1 + G2, G1, s);
-  }
-  const int G = e->grid;
-  hipLaunchKernelGGL((k_gemm32p_pair<P1, P2, S>), dim3(S::BLOCKS + G), dim3(256), lds, s, p1, p2, side, (const int*)e->d,
-                     (const int*)e->d + G + 1, e->g1);
+  hipLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, p1, p2,
+                     side);
   QLX_HIP(hipGetLastError());
   debug_sync(s, __PRETTY_FUNCTION__);
 }

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "qlx_internal.h"
 
@@ -66,6 +67,20 @@ __device__ __forceinline__ int xcd_logical(int b, int G) {
   return x * q + (x < r ? x : r) + i;
 }
 
+// Optional per-tile A-operand context: a policy with a member type ACtx provides
+//   ACtx a_ctx(int z, int row0, int tid) const                       once per tile, per thread (e.g. the frame pointers of its rows)
+//   f32x4 ldA_c(const ACtx&, int i, int z, int s, int row, int k) const    instead of ldA (i = the thread's load index)
+// so loop-invariant pointer loads (frame tables) leave the slab loop: one memory latency per slab, not two.
+template <class P, class = void>
+struct HasACtx : std::false_type {};
+template <class P>
+struct HasACtx<P, std::void_t<typename P::ACtx>> : std::true_type {};
+struct NoCtx {};
+template <class P, bool = HasACtx<P>::value>
+struct ACtxOf { using type = NoCtx; };
+template <class P>
+struct ACtxOf<P, true> { using type = typename P::ACtx; };
+
 // One output tile of a policy P (see the policies below for the members it provides):
 //   acc[row][col] = sum over the slabs s = 0 .. nslabs(z) - 1 and k = 0 .. 31 of A(z, s, row, k) * B(z, s, col, k),
 // one fmaf chain per output in (s, k) order; then P::epi stores it.  With P::BIAS the tiles of row-tile 0 also
@@ -85,6 +100,8 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   p.decode(lb, tm, tn, z);
   const int row0 = tm * P::BM, col0 = tn * P::BN;
   const int ns = p.nslabs(z);
+  typename ACtxOf<P>::type actx{};
+  if constexpr (HasACtx<P>::value) actx = p.a_ctx(z, row0, tid);
   float* As0 = lds;
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
@@ -99,7 +116,8 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
       if (OA::F4 % T == 0 || idx < OA::F4) {
         int r, k;
         OA::coord(idx, r, k);
-        ra[i] = p.ldA(z, s, row0 + r, k);
+        if constexpr (HasACtx<P>::value) ra[i] = p.ldA_c(actx, i, z, s, row0 + r, k);
+        else ra[i] = p.ldA(z, s, row0 + r, k);
       }
     }
 #pragma unroll
@@ -187,159 +205,6 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   }
 }
 
-// Persistent form of gemm_body: the block runs the output tiles ids[0 .. nt) (logical tile numbers of P, a list the
-// host scheduler built) as ONE pipeline - the loads of the next tile's first slabs are in flight while the current
-// tile finishes and stores its epilogue, so no tile pays a cold start.  Per output the arithmetic is gemm_body's
-// (same fmaf chain in the same order): results are bit-identical.
-template <class P>
-__device__ __forceinline__ void gemm_persistent(const P& p, const int* ids, int nt, float* lds) {
-  using OA = Opnd<P::BM, P::A_KMAJ>;
-  using OB = Opnd<P::BN, P::B_KMAJ>;
-  constexpr int T = P::WM * P::WN * 64;
-  constexpr int TM = P::BM / (P::WM * 16), TN = P::BN / (P::WN * 16);
-  static_assert(TM * P::WM * 16 == P::BM && TN * P::WN * 16 == P::BN, "tile shape");
-  constexpr int NA = (OA::F4 + T - 1) / T, NB = (OB::F4 + T - 1) / T;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave % P::WM, wn = wave / P::WM;
-  float* As0 = lds;
-  float* As1 = lds + OA::FLOATS;
-  float* Bs0 = lds + 2 * OA::FLOATS;
-  float* Bs1 = Bs0 + OB::FLOATS;
-  struct Pos {
-    int j, s, ns, tm, row0, col0, z;
-  };
-  auto tile = [&](int j) {
-    Pos q{j, 0, 0, 0, 0, 0, 0};
-    if (j < nt) {
-      int tm, tn, z;
-      p.decode(ids[j], tm, tn, z);
-      q.ns = p.nslabs(z);
-      q.tm = tm;
-      q.row0 = tm * P::BM;
-      q.col0 = tn * P::BN;
-      q.z = z;
-    }
-    return q;
-  };
-  auto next = [&](const Pos& q) {
-    if (q.j >= nt) return q;
-    if (q.s + 1 < q.ns) {
-      Pos r = q;
-      r.s += 1;
-      return r;
-    }
-    return tile(q.j + 1);
-  };
-  f32x4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
-  auto load = [&](const Pos& q, f32x4(&ra)[NA], f32x4(&rb)[NB]) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * T;
-      if (OA::F4 % T == 0 || idx < OA::F4) {
-        int r, k;
-        OA::coord(idx, r, k);
-        ra[i] = p.ldA(q.z, q.s, q.row0 + r, k);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + i * T;
-      if (OB::F4 % T == 0 || idx < OB::F4) {
-        int r, k;
-        OB::coord(idx, r, k);
-        rb[i] = p.ldB(q.z, q.s, q.col0 + r, k);
-      }
-    }
-  };
-  auto store = [&](int buf, const f32x4(&ra)[NA], const f32x4(&rb)[NB]) {
-    float* as = buf ? As1 : As0;
-    float* bs = buf ? Bs1 : Bs0;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * T;
-      if (OA::F4 % T == 0 || idx < OA::F4) {
-        int r, k;
-        OA::coord(idx, r, k);
-        OA::put(as, r, k, ra[i]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + i * T;
-      if (OB::F4 % T == 0 || idx < OB::F4) {
-        int r, k;
-        OB::coord(idx, r, k);
-        OB::put(bs, r, k, rb[i]);
-      }
-    }
-  };
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
-  float bsum = 0.0f;
-  auto compute = [&](int buf, const Pos& q) {
-    const float* a = buf ? As1 : As0;
-    const float* b = buf ? Bs1 : Bs0;
-    if (P::BIAS && q.tm == 0 && tid < P::BN)
-#pragma unroll 8
-      for (int k = 0; k < BK; ++k) bsum = bsum + OB::at(b, tid, k);
-#pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
-      float af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * 16, kk, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * 16, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-  };
-  auto epilogue = [&](const Pos& q) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        p.epi(q.z, q.row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, q.col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
-        acc[i][j] = zero4();
-      }
-    if constexpr (P::BIAS) {
-      if (q.tm == 0 && tid < P::BN) p.epi_bias(q.z, q.col0 + tid, bsum);
-    }
-    bsum = 0.0f;
-  };
-  Pos pc = tile(0);
-  if (pc.j >= nt) return;
-  Pos p1 = next(pc), p2 = next(p1);
-  load(pc, ra1, rb1);
-  store(0, ra1, rb1);
-  if (p1.j < nt) load(p1, ra0, rb0);
-  lds_barrier();
-  int t = 0;
-  // x holds p1's slab, y is free; loads of p2 fly while pc is multiplied and p1 waits for its LDS buffer
-  auto step = [&](f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
-    if (p2.j < nt) load(p2, ya, yb);
-    compute(t & 1, pc);
-    if (pc.s + 1 == pc.ns) epilogue(pc);
-    if (p1.j < nt) store((t + 1) & 1, xa, xb);
-    lds_barrier();
-    pc = p1;
-    p1 = p2;
-    p2 = next(p2);
-    ++t;
-  };
-  for (;;) {
-    step(ra0, rb0, ra1, rb1);
-    if (pc.j >= nt) break;
-    step(ra1, rb1, ra0, rb0);
-    if (pc.j >= nt) break;
-  }
-}
-
 template <class P>
 constexpr size_t gemm_lds_bytes() {
   return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ>::FLOATS + Opnd<P::BN, P::B_KMAJ>::FLOATS) * sizeof(float);
@@ -378,27 +243,6 @@ __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, c
   else gemm_body(p2, xcd_logical(h - g1, G - g1), lds);
 }
 
-// persistent launches: block b runs the tile list ids[start[b] .. start[b + 1]) (host-built, see qnet32.hip Sched)
-template <class P>
-__global__ __launch_bounds__(256) void k_gemm32p(const P p, const int* start, const int* ids) {
-  extern __shared__ float lds[];
-  const int b = blockIdx.x;
-  gemm_persistent(p, ids + start[b], start[b + 1] - start[b], lds);
-}
-
-// two problems: blocks [S::BLOCKS, S::BLOCKS + g1blocks) run lists of P1, the rest lists of P2 (one start/ids table
-// over all non-side blocks; tile ids are each problem's own)
-template <class P1, class P2, class S>
-__global__ __launch_bounds__(256) void k_gemm32p_pair(const P1 p1, const P2 p2, const S side, const int* start, const int* ids,
-                                                      int g1blocks) {
-  extern __shared__ float lds[];
-  const int b = blockIdx.x;
-  if (b < S::BLOCKS) { side.run(b, lds); return; }
-  const int h = b - S::BLOCKS;
-  if (h < g1blocks) gemm_persistent(p1, ids + start[h], start[h + 1] - start[h], lds);
-  else gemm_persistent(p2, ids + start[h], start[h + 1] - start[h], lds);
-}
-
 struct NoSide {
   static constexpr int BLOCKS = 0;
   __device__ void run(int, float*) const {}
@@ -423,13 +267,30 @@ struct PConv1Fwd {
   int M;             // B * 400
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 8; }
-  __device__ f32x4 ldA(int, int kh, int row, int k) const {
-    if (row >= M) return zero4();
-    const int b = row / 400, p = row - b * 400, oh = p / 20, ow = p - oh * 20;
-    const int c = k >> 3, h = (k >> 2) & 1;
-    const uint8_t* f = table[b * 4 + c];
-    if (!f) return zero4();   // a ring slot before the episode's first frames: the zero frame (replay_dev.h)
-    return u8x4(*reinterpret_cast<const uint32_t*>(f + ((oh + (kh >> 2)) * kBlocks + ow + h) * 16 + (kh & 3) * 4));
+  // the thread's 4 A rows (r = tid / 8 + 32 i) and channel group (c, h) = k = (tid & 7) * 4 are fixed for the tile:
+  // their 4-pixel words sit at base + kh-dependent offset, base resolved once per tile
+  struct ACtx {
+    const uint8_t* f[4];
+  };
+  __device__ ACtx a_ctx(int, int row0, int tid) const {
+    ACtx c;
+    const int k = (tid & 7) * 4, ch = k >> 3, h = (k >> 2) & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + (tid >> 3) + 32 * i;
+      c.f[i] = nullptr;
+      if (row < M) {
+        const int b = row / 400, p = row - b * 400, oh = p / 20, ow = p - oh * 20;
+        const uint8_t* f = table[b * 4 + ch];
+        if (f) c.f[i] = f + (oh * kBlocks + ow + h) * 16;
+      }
+    }
+    return c;
+  }
+  __device__ f32x4 ldA_c(const ACtx& c, int i, int, int kh, int, int) const {
+    const uint8_t* f = c.f[i];
+    if (!f) return zero4();   // past M, or a ring slot before the episode's first frames: the zero frame
+    return u8x4(*reinterpret_cast<const uint32_t*>(f + (kh >> 2) * kBlocks * 16 + (kh & 3) * 4));
   }
   __device__ f32x4 ldB(int, int kh, int col, int k) const {   // W0[kh][kw][c][oc], k = c * 8 + kw
     const int c = k >> 3, kw = k & 7;
@@ -675,6 +536,33 @@ struct PConv1Wgrad {
     return (b1 - b0) * P;
   }
   __host__ __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
+  // the thread's A row m = (kh, c, kw group) is fixed for the tile (KMAJ coord: row = (tid % 32) * 4): the chunk's
+  // SC frame pointers of its channel c, offset to its (kh, h), resolved once per tile
+  struct ACtx {
+    const uint8_t* f[SC];
+  };
+  __device__ ACtx a_ctx(int z, int row0, int tid) const {
+    ACtx c;
+    const int row = row0 + (tid % 32) * 4;
+    const int kh = row >> 5, ch = (row >> 3) & 3, h = (row >> 2) & 1;
+#pragma unroll
+    for (int bl = 0; bl < SC; ++bl) {
+      const int b = z * SC + bl;
+      const uint8_t* f = b < B ? table[b * 4 + ch] : nullptr;
+      c.f[bl] = f ? f + ((kh >> 2) * kBlocks + h) * 16 + (kh & 3) * 4 : nullptr;
+    }
+    return c;
+  }
+  __device__ f32x4 ldA_c(const ACtx& c, int, int z, int s, int, int k) const {
+    const int r = s * BK + k;
+    if (r >= rows_in(z)) return zero4();
+    const int bl = r / P, p = r - bl * P, oh = p / 20, ow = p - oh * 20;
+    const uint8_t* f = c.f[0];
+#pragma unroll
+    for (int j = 1; j < SC; ++j) f = bl == j ? c.f[j] : f;
+    if (!f) return zero4();
+    return u8x4(*reinterpret_cast<const uint32_t*>(f + (oh * kBlocks + ow) * 16));
+  }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
     const int r = s * BK + k;
     if (r >= rows_in(z)) return zero4();

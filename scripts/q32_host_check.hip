@@ -40,7 +40,9 @@ static void replay(const P& p, const char* name) {
       for (int idx = 0; idx < OA::F4; ++idx) {
         int r, k;
         OA::coord(idx, r, k);
-        const f32x4 v = p.ldA(z, s, row0 + r, k);
+        f32x4 v;
+        if constexpr (HasACtx<P>::value) v = p.ldA_c(p.a_ctx(z, row0, idx % T), idx / T, z, s, row0 + r, k);
+        else v = p.ldA(z, s, row0 + r, k);
         sink = sink + v[0];
         ++checks;
       }
