@@ -6,8 +6,7 @@
 // order is internal to its CPU kernels and pinned by no reference test: the order is therefore part of
 // this build's definition of the arithmetic, stated here once and followed by the GPU kernels
 // (q-learning_amd/csrc/qnet32_kernels.h).  tests/test_oracle_qnet.py pins this restatement against float64 torch.
-//   conv1 forward   z = sum over (kh, c, kw) of x[4oh+kh][4ow+kw][c] W0[kh][kw][c][oc]
-//   conv2 / conv3   z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
+//   conv1 .. conv3  z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
 //   dense           z = sum over k ascending (Flatten order h, w, c)
 //   every sum: acc = 0; acc = fmaf(x, w, acc) in that order; then + bias, ReLU (v > 0 ? v : 0)
 //   Huber head      e = q_a - y, h = w (|e| <= 1 ? (0.5 e) e : |e| - 0.5), g = (w clip(e, -1, 1)) / B,
@@ -45,8 +44,8 @@ static void conv1_fwd(const uint8_t* x, int B, const float* W, const float* bias
         float acc[32];
         for (int oc = 0; oc < 32; ++oc) acc[oc] = 0.0f;
         for (int kh = 0; kh < 8; ++kh)
-          for (int c = 0; c < 4; ++c)
-            for (int kw = 0; kw < 8; ++kw) {
+          for (int kw = 0; kw < 8; ++kw)
+            for (int c = 0; c < 4; ++c) {
               const float v = (float)x[(((size_t)b * 84 + oh * 4 + kh) * 84 + ow * 4 + kw) * 4 + c];
               if (v == 0.0f) continue;   // fmaf(0, w, acc) == acc (acc is never -0)
               const float* wr = W + ((kh * 8 + kw) * 4 + c) * 32;
@@ -264,8 +263,6 @@ float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* acti
   conv_dgrad(kC3, dz3.data(), B, q.w[4].data(), a.a2.data(), dz2.data());
   conv_wgrad(kC2, a.a1.data(), nullptr, dz2.data(), B, kSC2, g.g[2].data(), g.g[3].data());
   conv_dgrad(kC2, dz2.data(), B, q.w[2].data(), a.a1.data(), dz1.data());
-  // conv1's wgrad chain runs over (b, oh, ow) with its rows in the order (kh, c, kw) on the GPU; per output element
-  // the chain order is the same (b, oh, ow) whatever the row order, so the HWIO restatement gives the same bits
   const Cfg c1 = {84, 84, 4, 8, 4, 20, 20, 32};
   conv_wgrad(c1, nullptr, x8, dz1.data(), B, kSC1, g.g[0].data(), g.g[1].data());
   return loss;

@@ -148,8 +148,8 @@ struct SideFc2 {
 };
 
 // Conv weight gradients: dW = sum over sample chunks z in order of the chunk partials (t = 0; t = t + P_z), written into
-// the flat gradient.  Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32] with its rows (kh, c, kw)
-// mapped to HWIO (kh, kw, c).  The last row of each is the bias.
+// the flat gradient.  Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order.  The last
+// row of each is the bias.
 struct WRed {
   const float* slab[3];
   int nz[3];
@@ -179,12 +179,7 @@ __global__ __launch_bounds__(256) void k_wreduce32(WRed R) {
   const int oc = R.oc[L], m = e / oc, n = e - m * oc;
   const int M = R.count[L] / oc - 1;
   if (m == M) { R.gb[L][n] = t; return; }
-  int row = m;
-  if (L == 2) {   // conv1: (kh, c, kw) -> (kh, kw, c)
-    const int kh = m >> 5, c = (m >> 3) & 3, kw = m & 7;
-    row = (kh * 8 + kw) * 4 + c;
-  }
-  R.gw[L][(size_t)row * oc + n] = t;
+  R.gw[L][(size_t)m * oc + n] = t;
 }
 
 // clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg;
@@ -276,7 +271,6 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
 using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3>;
 using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
-using PConv1WgradT = PConv1Wgrad<kSC1>;
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
 
@@ -354,6 +348,16 @@ static void launch_pair(qlx_model*, const P1& p1, const P2& p2, const S& side, i
   debug_sync(s, __PRETTY_FUNCTION__);
 }
 
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    QLX_HIP(hipGetDevice(&dev));
+    QLX_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return n;
+}
+
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
 // forward over B samples in chunks of the workspace's forward chunk: a1..a3 hold the last chunk (the whole batch when
@@ -367,8 +371,11 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     const int n = std::min(w.fchunk, B - c0);
     {
       ProfScope ps(m->prof, "f32_conv1_fwd", s, 2.0 * n * 400 * 32 * 256);
-      PConv1Fwd P{grid(n * 400, PConv1Fwd::BM, 32, 32, 1), table + (size_t)c0 * 4, p + voff(0), p + voff(1), w.fa1, n * 400};
-      launch(m, P, n, s);
+      set_lds_limit((const void*)k_conv1_fwd32, 2 * kC1Frames);
+      hipLaunchKernelGGL(k_conv1_fwd32, dim3(std::min(n, 2 * num_cus())), dim3(256), 2 * kC1Frames, s, table + (size_t)c0 * 4, n,
+                         p + voff(0), p + voff(1), w.fa1);
+      QLX_HIP(hipGetLastError());
+      debug_sync(s, "k_conv1_fwd32");
     }
     {
       ProfScope ps(m->prof, "f32_conv2_fwd", s, 2.0 * n * 81 * 64 * 512);
@@ -449,8 +456,11 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   }
   {
     ProfScope ps(m->prof, "f32_conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
-    PConv1WgradT P{grid(256, PConv1WgradT::BM, 32, 32, z1), table, w.fdz1, w.fslab1, B};
-    launch(m, P, B, s);
+    constexpr size_t lds = kC1Frames + 400 * 16 * 4;
+    set_lds_limit((const void*)k_conv1_wgrad32, lds);
+    hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(256), lds, s, table, w.fdz1, B, z1, w.fslab1);
+    QLX_HIP(hipGetLastError());
+    debug_sync(s, "k_conv1_wgrad32");
   }
   {
     ProfScope ps(m->prof, "f32_wgrad_reduce", s);

@@ -250,58 +250,9 @@ struct NoSide {
 
 // ---------------------------------------------------------------------------------------------------------------
 // Layer policies.  Chain orders (oracle/qnet32_ref.cpp):
-//   conv1 forward   k = (kh, c, kw)            conv2 / conv3 forward  k = (kh, kw, c)      fc1 forward k = h, w, c
+//   conv forward    k = (kh, kw, c)  (conv1: k_conv1_fwd32 below)                          fc1 forward k = h, w, c
 //   conv dgrad      k = (kh, kw, oc) over the valid taps                                   fc1 dgrad   k = n
 //   weight grads    r = (b, oh, ow) ascending inside a sample chunk; fc1 / fc2 over b ascending, no chunks
-
-// conv1 forward: frames (u8, s2d layout, table[b * 4 + slot]; a null entry is the zero frame) -> a1 [B][20][20][32] = relu(z + b0).
-// Slab s = kh; k = c * 8 + kw.  A row (b, oh, ow): 4 pixels kw = 4h .. 4h+3 of slot c are one aligned u32.
-struct PConv1Fwd {
-  static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
-  static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
-  Grid g;
-  const uint8_t* const* table;
-  const float* w0;   // [8][8][4][32] HWIO
-  const float* b0;
-  float* a1;
-  int M;             // B * 400
-  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __host__ __device__ int nslabs(int) const { return 8; }
-  // the thread's 4 A rows (r = tid / 8 + 32 i) and channel group (c, h) = k = (tid & 7) * 4 are fixed for the tile:
-  // their 4-pixel words sit at base + kh-dependent offset, base resolved once per tile
-  struct ACtx {
-    const uint8_t* f[4];
-  };
-  __device__ ACtx a_ctx(int, int row0, int tid) const {
-    ACtx c;
-    const int k = (tid & 7) * 4, ch = k >> 3, h = (k >> 2) & 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = row0 + (tid >> 3) + 32 * i;
-      c.f[i] = nullptr;
-      if (row < M) {
-        const int b = row / 400, p = row - b * 400, oh = p / 20, ow = p - oh * 20;
-        const uint8_t* f = table[b * 4 + ch];
-        if (f) c.f[i] = f + (oh * kBlocks + ow + h) * 16;
-      }
-    }
-    return c;
-  }
-  __device__ f32x4 ldA_c(const ACtx& c, int i, int, int kh, int, int) const {
-    const uint8_t* f = c.f[i];
-    if (!f) return zero4();   // past M, or a ring slot before the episode's first frames: the zero frame
-    return u8x4(*reinterpret_cast<const uint32_t*>(f + (kh >> 2) * kBlocks * 16 + (kh & 3) * 4));
-  }
-  __device__ f32x4 ldB(int, int kh, int col, int k) const {   // W0[kh][kw][c][oc], k = c * 8 + kw
-    const int c = k >> 3, kw = k & 7;
-    return ld4(w0 + ((kh * 8 + kw) * 4 + c) * 32 + col);
-  }
-  __device__ void epi(int, int row, int col, f32x4 v) const {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < M) a1[(size_t)(row + r) * 32 + col] = relu(v[r] + b0[col]);
-  }
-};
 
 // conv2 / conv3 forward on fp32 NHWC input: out = relu(conv + bias); slab s: tap = 32 s / C, c0 = 32 s % C
 template <int H, int W, int C, int KS, int S, int OH, int OW, int OC>
@@ -518,71 +469,176 @@ struct PConvWgrad {
   __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * OC + col] = v; }
 };
 
-// conv1 weight gradient over sample chunk z: rows m = (kh, c, kw) (the forward's k order), cols oc, r = (b, oh, ow);
-// A (frames) is 4 consecutive kw per aligned u32.  The slab reduction maps m back to HWIO.
-template <int SC>
-struct PConv1Wgrad {
-  static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
-  static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
-  static constexpr int MROWS = 256, P = 400, CHUNK = SC;
-  Grid g;
-  const uint8_t* const* table;
-  const float* dz1;   // [B][20][20][32]
-  float* slab;
-  int B;
-  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
-  __host__ __device__ int rows_in(int z) const {
-    const int b0 = z * SC, b1 = b0 + SC < B ? b0 + SC : B;
-    return (b1 - b0) * P;
-  }
-  __host__ __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
-  // the thread's A row m = (kh, c, kw group) is fixed for the tile (KMAJ coord: row = (tid % 32) * 4): the chunk's
-  // SC frame pointers of its channel c, offset to its (kh, h), resolved once per tile
-  struct ACtx {
-    const uint8_t* f[SC];
-  };
-  __device__ ACtx a_ctx(int z, int row0, int tid) const {
-    ACtx c;
-    const int row = row0 + (tid % 32) * 4;
-    const int kh = row >> 5, ch = (row >> 3) & 3, h = (row >> 2) & 1;
+#ifndef QLX_Q32_POLICIES_ONLY   // (scripts/q32_host_check.hip replays the policies on the host without the kernels)
+// conv1 (8x8 stride 4, 4 -> 32 channels) from the u8 frames, one sample at a time per block with the sample's four
+// frames (28,224 B, s2d layout) staged in LDS while the next sample's frames are in flight in registers.
+
+constexpr int kC1Frames = 4 * kFramePix;   // 28,224 B of one sample's frames
+constexpr int kC1Chunks = kC1Frames / 16;  // 1,764 uint4
+
+// next sample's frames into registers (null table entry = the zero frame)
+__device__ __forceinline__ void c1_prefetch(const uint8_t* const* table, int b, uint4 (&pf)[7]) {
 #pragma unroll
-    for (int bl = 0; bl < SC; ++bl) {
-      const int b = z * SC + bl;
-      const uint8_t* f = b < B ? table[b * 4 + ch] : nullptr;
-      c.f[bl] = f ? f + ((kh >> 2) * kBlocks + h) * 16 + (kh & 3) * 4 : nullptr;
+  for (int j = 0; j < 7; ++j) {
+    const int q = threadIdx.x + 256 * j;
+    pf[j] = uint4{0, 0, 0, 0};
+    if (q < kC1Chunks) {
+      const int slot = q / 441, pos = q - slot * 441;
+      const uint8_t* f = table[b * 4 + slot];
+      if (f) pf[j] = *reinterpret_cast<const uint4*>(f + pos * 16);
     }
-    return c;
   }
-  __device__ f32x4 ldA_c(const ACtx& c, int, int z, int s, int, int k) const {
-    const int r = s * BK + k;
-    if (r >= rows_in(z)) return zero4();
-    const int bl = r / P, p = r - bl * P, oh = p / 20, ow = p - oh * 20;
-    const uint8_t* f = c.f[0];
+}
+__device__ __forceinline__ void c1_stage(uint8_t* dst, const uint4 (&pf)[7]) {
 #pragma unroll
-    for (int j = 1; j < SC; ++j) f = bl == j ? c.f[j] : f;
-    if (!f) return zero4();
-    return u8x4(*reinterpret_cast<const uint32_t*>(f + (oh * kBlocks + ow) * 16));
+  for (int j = 0; j < 7; ++j) {
+    const int q = threadIdx.x + 256 * j;
+    if (q < kC1Chunks) *reinterpret_cast<uint4*>(dst + q * 16) = pf[j];
   }
-  __device__ f32x4 ldA(int z, int s, int row, int k) const {
-    const int r = s * BK + k;
-    if (r >= rows_in(z)) return zero4();
-    const int kh = row >> 5, c = (row >> 3) & 3, h = (row >> 2) & 1;
-    const int bl = r / P, p = r - bl * P, oh = p / 20, ow = p - oh * 20, b = z * SC + bl;
-    const uint8_t* f = table[b * 4 + c];
-    if (!f) return zero4();
-    return u8x4(*reinterpret_cast<const uint32_t*>(f + ((oh + (kh >> 2)) * kBlocks + ow + h) * 16 + (kh & 3) * 4));
-  }
-  __device__ f32x4 ldB(int z, int s, int col, int k) const {
-    const int r = s * BK + k;
-    if (r >= rows_in(z)) return zero4();
-    return ld4(dz1 + ((size_t)z * SC * P + r) * 32 + col);
-  }
-  __device__ void epi(int z, int row, int col, f32x4 v) const {
+}
+__device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >> (8 * i)) & 0xFFu); }
+
+// forward: a1[b][r][oc] = relu(chain over k = (kh, kw, c) of x * W0[kh][kw][c][oc] + b0[oc]), r = (oh, ow).
+// Wave w owns output channels (w & 1) * 16 .. + 15 and the 16-row tiles rt = (w >> 1) + 2 j (13 / 12 of the 25); one
+// v_mfma_f32_16x16x4_f32 per (tile, kh, kw) with c on the lane groups, W0 fragments resident in VGPRs.
+__global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0, const float* b0,
+                                                        float* a1) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t c1lds[];   // [2][4][7056]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = wave & 1, rp = wave >> 1;
+  const int col = ct * 16 + (lane & 15), g = lane >> 4;
+  float wf[64];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) slab[((size_t)z * (MROWS + 1) + row + r) * 32 + col] = v[r];
+  for (int kk = 0; kk < 64; ++kk) wf[kk] = w0[(kk * 4 + g) * 32 + col];
+  const float bias = b0[col];
+  int ob[13];
+#pragma unroll
+  for (int j = 0; j < 13; ++j) {
+    const int r = (rp + 2 * j) * 16 + (lane & 15);
+    const int oh = r / 20, ow = r - oh * 20;
+    ob[j] = g * kFramePix + (oh * kBlocks + ow) * 16;   // lane group g reads ring slot g
   }
-  __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * 32 + col] = v; }
-};
+  const int nt = rp == 0 ? 13 : 12;
+  int b = blockIdx.x;
+  if (b >= B) return;
+  uint4 pf[7];
+  c1_prefetch(table, b, pf);
+  c1_stage(c1lds, pf);
+  __syncthreads();
+  for (int it = 0; b < B; b += gridDim.x, ++it) {
+    const uint8_t* fr = c1lds + (it & 1) * kC1Frames;
+    const int nb = b + gridDim.x;
+    if (nb < B) c1_prefetch(table, nb, pf);
+    f32x4 acc[13];
+#pragma unroll
+    for (int j = 0; j < 13; ++j) acc[j] = zero4();
+#pragma unroll
+    for (int kq = 0; kq < 16; ++kq) {   // (kh, kw half): 4 pixels of one s2d block per lane and tile
+      const int kh = kq >> 1, hw = kq & 1;
+      const int off = (kh >> 2) * kBlocks * 16 + (kh & 3) * 4 + hw * 16;
+      uint32_t d[13];
+#pragma unroll
+      for (int j = 0; j < 13; ++j)
+        if (j < nt) d[j] = *reinterpret_cast<const uint32_t*>(fr + ob[j] + off);
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw)
+#pragma unroll
+        for (int j = 0; j < 13; ++j)
+          if (j < nt) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[j], kw), wf[kq * 4 + kw], acc[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 13; ++j)
+      if (j < nt) {
+        const int r0 = (rp + 2 * j) * 16 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[j][i] + bias);
+      }
+    if (nb < B) c1_stage(c1lds + ((it + 1) & 1) * kC1Frames, pf);
+    __syncthreads();
+  }
+}
+
+// weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
+// x[r][m] dz1[r][oc], m = (kh, kw, c) HWIO, and slab[z][256][oc] = the same chain of dz1 (bias).  Block (z, hh) covers
+// output channels hh * 16 .. + 15; wave w the 16-row tiles 4 w .. 4 w + 3.  Per sample the frames and dz1's channel
+// half sit in LDS (53,824 B) while the next sample's are in flight in registers.
+constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
+__global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
+                                                          float* slab) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t c1lds[];   // frames [4][7056], then dz [400][16] f32
+  float* dzs = reinterpret_cast<float*>(c1lds + kC1Frames);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.x % nz, hh = blockIdx.x / nz;
+  const int g = lane >> 4;
+  const int b0 = z * QLX_F32_WGRAD_CHUNK_CONV1;
+  const int nb = min(QLX_F32_WGRAD_CHUNK_CONV1, B - b0);
+  // this lane's A row m per tile: byte offset of (kh, kw, c) inside the staged frames, relative to pixel (4 oh, 4 ow)
+  int mo[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int m = (wave * 4 + t) * 16 + (lane & 15);
+    const int kh = m >> 5, kw = (m >> 2) & 7, c = m & 3;
+    mo[t] = c * kFramePix + ((kh >> 2) * kBlocks + (kw >> 2)) * 16 + (kh & 3) * 4 + (kw & 3);
+  }
+  uint4 pf[14];
+  auto prefetch = [&](int b) {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      const int q = tid + 256 * j;
+      pf[j] = uint4{0, 0, 0, 0};
+      if (q < kC1Chunks) {
+        const int slot = q / 441, pos = q - slot * 441;
+        const uint8_t* f = table[b * 4 + slot];
+        if (f) pf[j] = *reinterpret_cast<const uint4*>(f + pos * 16);
+      } else if (q < kC1Chunks + kC1DzChunks) {
+        const int e = q - kC1Chunks, r = e >> 2, part = e & 3;
+        pf[j] = *reinterpret_cast<const uint4*>(dz1 + ((size_t)b * 400 + r) * 32 + hh * 16 + part * 4);
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      const int q = tid + 256 * j;
+      if (q < kC1Chunks + kC1DzChunks) *reinterpret_cast<uint4*>(c1lds + q * 16) = pf[j];
+    }
+  };
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = zero4();
+  float bsum = 0.0f;
+  prefetch(b0);
+  for (int bl = 0; bl < nb; ++bl) {
+    __syncthreads();   // the previous sample's LDS reads are done
+    stage();
+    __syncthreads();
+    if (bl + 1 < nb) prefetch(b0 + bl + 1);
+    for (int rs = 0; rs < 100; ++rs) {
+      const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
+      const float bv = dzs[r * 16 + (lane & 15)];
+      const int px = (oh * kBlocks + ow) * 16;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)c1lds[mo[t] + px], bv, acc[t], 0, 0, 0);
+      if (wave == 0) {   // bias chain in r order: lane groups hold r = 4 rs + 0 .. 3
+        const float v1 = __shfl(bv, lane + 16), v2 = __shfl(bv, lane + 32), v3 = __shfl(bv, lane + 48);
+        bsum = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(bsum, bv), v1), v2), v3);
+      }
+    }
+  }
+  float* out = slab + (size_t)z * 257 * 32;
+  const int oc = hh * 16 + (lane & 15);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int m0 = (wave * 4 + t) * 16 + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(size_t)(m0 + i) * 32 + oc] = acc[t][i];
+  }
+  if (wave == 0 && g == 0) out[256 * 32 + oc] = bsum;
+}
+
+#endif  // QLX_Q32_POLICIES_ONLY
 
 }  // namespace q32
 }  // namespace qlx

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #undef __device__
 #define __device__ __attribute__((host, device))
+#define QLX_Q32_POLICIES_ONLY
 #include "qnet32_kernels.h"
 
 #include <cstdio>
@@ -18,7 +19,6 @@ using namespace qlx::q32;
 constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
 using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3>;
 using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
-using PConv1WgradT = PConv1Wgrad<kSC1>;
 
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
@@ -90,7 +90,6 @@ int main(int argc, char** argv) {
   float* a1 = buf<float>((size_t)C * 12800); float* a2 = buf<float>((size_t)C * 5184); float* a3 = buf<float>((size_t)C * 3136);
   float* a4 = buf<float>((size_t)n * 512);
   // forward over n
-  replay(PConv1Fwd{grid(n * 400, PConv1Fwd::BM, 32, 32, 1), tab, w0, b0, a1, n * 400}, "conv1_fwd");
   replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
   replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
   replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
@@ -108,7 +107,6 @@ int main(int argc, char** argv) {
   replay(PConv3Wgrad{grid(576, 64, 64, 64, z3), a2, dz3, s3, B}, "conv3_wgrad");
   replay(PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
-  replay(PConv1WgradT{grid(256, PConv1WgradT::BM, 32, 32, z1), tab, dz1, s1, B}, "conv1_wgrad");
   printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
   return 0;
 }

@@ -133,7 +133,14 @@ int main(int argc, char** argv) {
   const float* W3 = W2 + 36864 + 64;
   for (int B : Bs) {
     printf("--- B = %d\n", B);
-    run1("conv1_fwd", PConv1Fwd{grid(B * 400, PConv1Fwd::BM, 32, 32, 1), table, W0, W0 + 8192, a1, B * 400}, 2.0 * B * 400 * 32 * 256);
+    {
+      const int G = std::min(B, 512);
+      CK(hipFuncSetAttribute((const void*)k_conv1_fwd32, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kC1Frames));
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32, dim3(G), dim3(256), 2 * kC1Frames, 0, table, B, W0, W0 + 8192, a1); });
+      const double f = 2.0 * B * 400 * 32 * 256;
+      printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_fwd (k_conv1_fwd32)", G, 2 * kC1Frames, us, f / us / 1e6,
+             f / us / 1e6 / 157.3 * 100);
+    }
     run1("conv2_fwd", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>{grid(B * 81, 64, 64, 64, 1), a1, W1, W1, a2, B * 81},
          2.0 * B * 81 * 64 * 512);
     run1("conv3_fwd", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>{grid(B * 49, 64, 64, 64, 1), a2, W2, W2, a3, B * 49},
@@ -150,7 +157,14 @@ int main(int argc, char** argv) {
     run1("conv2_dgrad", PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, W1, a1, dz1, B * 100}, 2.0 * B * 81 * 64 * 512);
     run1("conv2_wgrad", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, B / 16), a1, dz2, slab, B},
          2.0 * B * 81 * 64 * 512);
-    run1("conv1_wgrad", PConv1Wgrad<4>{grid(256, 128, 32, 32, B / 4), table, dz1, slab, B}, 2.0 * B * 400 * 256 * 32);
+    {
+      const int nz = B / 4, lds = kC1Frames + 400 * 16 * 4;
+      CK(hipFuncSetAttribute((const void*)k_conv1_wgrad32, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(256), lds, 0, table, dz1, B, nz, slab); });
+      const double f = 2.0 * B * 400 * 256 * 32;
+      printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_wgrad (k_conv1_wgrad32)", 2 * nz, lds, us,
+             f / us / 1e6, f / us / 1e6 / 157.3 * 100);
+    }
   }
   printf("--- generic GEMM (A row-major, B row-major)\n");
   {
