@@ -105,9 +105,12 @@ __global__ __launch_bounds__(256) void k_dz4_32(const float* a4, const float* w4
 }
 
 // dW4[k][n] = fmaf chain over b of a4[b][k] dq[b][n]; db4[n] = sum over b of dq[b][n]; loss = (sum over b of h_b) / B.
-// Leading blocks of the fc1 backward launch (independent of its GEMM tiles).
+// Leading blocks of the fc1 backward launch (independent of its GEMM tiles): one wave per 16-row tile of the GEMM
+// [a4^T ; 1] [dq | h] with v_mfma_f32_16x16x4_f32 (b on the lane groups, so each output is the b-ordered chain; the
+// all-ones row 512 gives db4 and the loss sum, fmaf(1, v, s) = s + v).  Operands for 8 MFMAs are loaded one batch
+// ahead of the batch being multiplied.
 struct SideFc2 {
-  static constexpr int BLOCKS = 3;
+  static constexpr int BLOCKS = 9;   // 33 row tiles (512 rows of a4^T + the ones row), 4 waves per block
   const float* a4;
   const uint8_t* act;
   const float* gs;
@@ -117,32 +120,44 @@ struct SideFc2 {
   float* db4;
   float* loss;
   __device__ void run(int blk, float*) const {
-    const int t = threadIdx.x;
-    if (blk < 2) {
-      const int k = blk * 256 + t;
-      float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-#pragma unroll 8
-      for (int b = 0; b < B; ++b) {
-        const float x = a4[(size_t)b * 512 + k];
-        const int a = act[b];
-        const float g = gs[b];
-        s0 = fmaf(x, a == 0 ? g : 0.0f, s0);
-        s1 = fmaf(x, a == 1 ? g : 0.0f, s1);
-        s2 = fmaf(x, a == 2 ? g : 0.0f, s2);
+    const int lane = threadIdx.x & 63;
+    const int t = blk * 4 + (int)(threadIdx.x >> 6);
+    if (t >= 33) return;
+    const int g = lane >> 4, n = lane & 15, m = t * 16 + n;
+    auto ld = [&](int s0, float (&av)[8], float (&bv)[8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int b = 4 * (s0 + j) + g;
+        av[j] = 0.0f;
+        bv[j] = 0.0f;
+        if (b < B) {
+          av[j] = t < 32 ? a4[(size_t)b * 512 + m] : (n == 0 ? 1.0f : 0.0f);
+          bv[j] = n < 3 ? (act[b] == n ? gs[b] : 0.0f) : (n == 3 ? hs[b] : 0.0f);
+        }
       }
-      dw4[k * 3 + 0] = s0;
-      dw4[k * 3 + 1] = s1;
-      dw4[k * 3 + 2] = s2;
-    } else if (t < 3) {
-      float s = 0.0f;
-#pragma unroll 8
-      for (int b = 0; b < B; ++b) s = __fadd_rn(s, act[b] == t ? gs[b] : 0.0f);
-      db4[t] = s;
-    } else if (t == 3) {
-      float s = 0.0f;
-#pragma unroll 8
-      for (int b = 0; b < B; ++b) s = __fadd_rn(s, hs[b]);
-      *loss = s / (float)B;
+    };
+    f32x4 acc = zero4();
+    auto mm = [&](const float (&av)[8], const float (&bv)[8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+    };
+    const int S = (B + 3) / 4;   // MFMA steps; zero operands past B leave the chains unchanged
+    float a0[8], b0[8], a1[8], b1[8];
+    ld(0, a0, b0);
+    for (int s0 = 0; s0 < S; s0 += 16) {
+      if (s0 + 8 < S) ld(s0 + 8, a1, b1);
+      mm(a0, b0);
+      if (s0 + 8 >= S) break;
+      if (s0 + 16 < S) ld(s0 + 16, a0, b0);
+      mm(a1, b1);
+    }
+    if (t < 32) {
+      if (n < 3)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dw4[(t * 16 + 4 * g + i) * 3 + n] = acc[i];
+    } else if (g == 0) {
+      if (n < 3) db4[n] = acc[0];
+      else if (n == 3) *loss = acc[0] / (float)B;
     }
   }
 };

@@ -615,6 +615,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* 
     stage();
     __syncthreads();
     if (bl + 1 < nb) prefetch(b0 + bl + 1);
+#pragma unroll 4
     for (int rs = 0; rs < 100; ++rs) {
       const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
       const float bv = dzs[r * 16 + (lane & 15)];
