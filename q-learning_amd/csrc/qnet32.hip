@@ -104,64 +104,6 @@ __global__ __launch_bounds__(256) void k_dz4_32(const float* a4, const float* w4
   *reinterpret_cast<f32x4*>(dz4 + (size_t)i * 4) = d;
 }
 
-// dW4[k][n] = fmaf chain over b of a4[b][k] dq[b][n]; db4[n] = sum over b of dq[b][n]; loss = (sum over b of h_b) / B.
-// Leading blocks of the fc1 backward launch (independent of its GEMM tiles): one wave per 16-row tile of the GEMM
-// [a4^T ; 1] [dq | h] with v_mfma_f32_16x16x4_f32 (b on the lane groups, so each output is the b-ordered chain; the
-// all-ones row 512 gives db4 and the loss sum, fmaf(1, v, s) = s + v).  Operands for 8 MFMAs are loaded one batch
-// ahead of the batch being multiplied.
-struct SideFc2 {
-  static constexpr int BLOCKS = 9;   // 33 row tiles (512 rows of a4^T + the ones row), 4 waves per block
-  const float* a4;
-  const uint8_t* act;
-  const float* gs;
-  const float* hs;
-  int B;
-  float* dw4;
-  float* db4;
-  float* loss;
-  __device__ void run(int blk, float*) const {
-    const int lane = threadIdx.x & 63;
-    const int t = blk * 4 + (int)(threadIdx.x >> 6);
-    if (t >= 33) return;
-    const int g = lane >> 4, n = lane & 15, m = t * 16 + n;
-    auto ld = [&](int s0, float (&av)[8], float (&bv)[8]) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int b = 4 * (s0 + j) + g;
-        av[j] = 0.0f;
-        bv[j] = 0.0f;
-        if (b < B) {
-          av[j] = t < 32 ? a4[(size_t)b * 512 + m] : (n == 0 ? 1.0f : 0.0f);
-          bv[j] = n < 3 ? (act[b] == n ? gs[b] : 0.0f) : (n == 3 ? hs[b] : 0.0f);
-        }
-      }
-    };
-    f32x4 acc = zero4();
-    auto mm = [&](const float (&av)[8], const float (&bv)[8]) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
-    };
-    const int S = (B + 3) / 4;   // MFMA steps; zero operands past B leave the chains unchanged
-    float a0[8], b0[8], a1[8], b1[8];
-    ld(0, a0, b0);
-    for (int s0 = 0; s0 < S; s0 += 16) {
-      if (s0 + 8 < S) ld(s0 + 8, a1, b1);
-      mm(a0, b0);
-      if (s0 + 8 >= S) break;
-      if (s0 + 16 < S) ld(s0 + 16, a0, b0);
-      mm(a1, b1);
-    }
-    if (t < 32) {
-      if (n < 3)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dw4[(t * 16 + 4 * g + i) * 3 + n] = acc[i];
-    } else if (g == 0) {
-      if (n < 3) db4[n] = acc[0];
-      else if (n == 3) *loss = acc[0] / (float)B;
-    }
-  }
-};
-
 // Conv weight gradients: dW = sum over sample chunks z in order of the chunk partials (t = 0; t = t + P_z), written into
 // the flat gradient.  Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order.  The last
 // row of each is the bias.
@@ -356,7 +298,7 @@ static void launch(qlx_model*, const P& p, int, hipStream_t s) {
 
 template <class P1, class P2, class S>
 static void launch_pair(qlx_model*, const P1& p1, const P2& p2, const S& side, int, hipStream_t s) {
-  const size_t lds = std::max(gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>());
+  const size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS});
   hipLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, p1, p2,
                      side);
   QLX_HIP(hipGetLastError());
@@ -392,20 +334,24 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       QLX_HIP(hipGetLastError());
       debug_sync(s, "k_conv1_fwd32");
     }
+    // tiles by batch: at chunk-size batches 64 x 64 tiles run best (~65 % of the fp32 peak), at training-size batches
+    // the narrower tiles that put more blocks on the chip (scripts/ubench32.hip sweep)
+    const bool big = n > 2048;
     {
       ProfScope ps(m->prof, "f32_conv2_fwd", s, 2.0 * n * 81 * 64 * 512);
-      PConv2Fwd P{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81};
-      launch(m, P, n, s);
+      if (big) launch(m, PConv2Fwd{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, n, s);
+      else launch(m, PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, n, s);
     }
     {
       ProfScope ps(m->prof, "f32_conv3_fwd", s, 2.0 * n * 49 * 64 * 576);
-      PConv3Fwd P{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49};
-      launch(m, P, n, s);
+      if (big) launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, n, s);
+      else launch(m, PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, n, s);
     }
     {
       ProfScope ps(m->prof, "f32_fc1_fwd", s, 2.0 * n * 3136 * 512);
-      PFc1Fwd P{grid(n, PFc1Fwd::BM, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n};
-      launch(m, P, n, s);
+      float* a4 = w.fa4 + (size_t)c0 * 512;
+      if (big) launch(m, PFc1Fwd{grid(n, 32, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), a4, n}, n, s);
+      else launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), a4, n}, n, s);
     }
   }
 }
@@ -445,8 +391,8 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
   }
   {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its three leading blocks
     ProfScope ps(m->prof, "f32_fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
-    PFc1Wgrad Pw{grid(3136, 64, 512, 64, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
-    PFc1Dgrad Pd{grid(B, 64, 3136, 64, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
+    PFc1WgradS Pw{grid(3136, 64, 512, 32, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
+    PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
     SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
     launch_pair(m, Pw, Pd, S, B, s);
   }
@@ -459,13 +405,13 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   {  // conv3: dz2 tiles + weight-gradient chunk tiles
     ProfScope ps(m->prof, "f32_conv3_bwd", s, 2.0 * 2.0 * B * 49 * 64 * 576);
-    PConv3Dgrad Pd{grid(B * 81, 64, 64, 64, 1), w.fdz3, p + voff(4), w.fa2, w.fdz2, B * 81};
+    PConv3DgradS Pd{grid(B * 81, 32, 64, 64, 1), w.fdz3, p + voff(4), w.fa2, w.fdz2, B * 81};
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
     launch_pair(m, Pw, Pd, NoSide{}, B, s);
   }
   {  // conv2: dz1 tiles (4 parity classes) + weight-gradient chunk tiles
     ProfScope ps(m->prof, "f32_conv2_bwd", s, 2.0 * B * 81 * 64 * 512 + 2.0 * B * 400 * 32 * 256);
-    PConv2Dgrad Pd{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), w.fdz2, p + voff(2), w.fa1, w.fdz1, B * 100};
+    PConv2DgradS Pd{grid(B * 100, 64, 32, 32, 4), w.fdz2, p + voff(2), w.fa1, w.fdz1, B * 100};
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
     launch_pair(m, Pw, Pd, NoSide{}, B, s);
   }

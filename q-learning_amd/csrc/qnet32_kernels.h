@@ -245,6 +245,7 @@ __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, c
 
 struct NoSide {
   static constexpr int BLOCKS = 0;
+  static constexpr size_t LDS = 0;
   __device__ void run(int, float*) const {}
 };
 
@@ -255,9 +256,9 @@ struct NoSide {
 //   weight grads    r = (b, oh, ow) ascending inside a sample chunk; fc1 / fc2 over b ascending, no chunks
 
 // conv2 / conv3 forward on fp32 NHWC input: out = relu(conv + bias); slab s: tap = 32 s / C, c0 = 32 s % C
-template <int H, int W, int C, int KS, int S, int OH, int OW, int OC>
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
 struct PConvFwd {
-  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* in;
@@ -282,10 +283,14 @@ struct PConvFwd {
 };
 using PConv2Fwd = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>;
 using PConv3Fwd = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>;
+// training-batch (B <= 2048) tile shapes: more, narrower blocks (scripts/ubench32.hip sweep at B = 1024)
+using PConv2FwdS = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>;
+using PConv3FwdS = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
 
 // fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3)
-struct PFc1Fwd {
-  static constexpr int BM = 32, BN = 64, WM = 2, WN = 2;
+template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PFc1FwdT {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* a3;
@@ -305,10 +310,13 @@ struct PFc1Fwd {
       if (row + r < M) a4[(size_t)(row + r) * 512 + col] = relu(v[r] + b3[col]);
   }
 };
+using PFc1Fwd = PFc1FwdT<>;
+using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
-struct PFc1Dgrad {
-  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PFc1DgradT {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
   Grid g;
   const float* dz4;
@@ -331,10 +339,13 @@ struct PFc1Dgrad {
       }
   }
 };
+using PFc1Dgrad = PFc1DgradT<>;
+using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
 
 // fc1 weight gradient: dW3 [3136][512] = a3^T dz4 over b ascending; db3 = column sums of dz4 (row-tile 0 blocks)
-struct PFc1Wgrad {
-  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PFc1WgradT {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
   Grid g;
   const float* a3;
@@ -359,10 +370,13 @@ struct PFc1Wgrad {
   }
   __device__ void epi_bias(int, int col, float v) const { db3[col] = v; }
 };
+using PFc1Wgrad = PFc1WgradT<>;
+using PFc1WgradS = PFc1WgradT<64, 32, 2, 2>;
 
 // conv3 backward-data: dz2 [B][9][9][64] = convT(dz3, W2) * (a2 > 0); rows (b, ih, iw), k = (kh, kw, oc)
-struct PConv3Dgrad {
-  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PConv3DgradT {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
   Grid g;
   const float* dz3;   // [B][7][7][64]
@@ -392,12 +406,15 @@ struct PConv3Dgrad {
       }
   }
 };
+using PConv3Dgrad = PConv3DgradT<>;
+using PConv3DgradS = PConv3DgradT<32, 64, 2, 2>;
 
 // conv2 backward-data by output parity class z = (py, px): rows (b, i, j) with ih = 2 i + py, iw = 2 j + px
 // (10 x 10 per class); taps t = (th, tw): kh = py + 2 th, kw = px + 2 tw, source dz2[b][i - th][j - tw];
 // k = (t, oc): the valid taps of the lexicographic (kh, kw, oc) order
-struct PConv2Dgrad {
-  static constexpr int BM = 128, BN = 32, WM = 4, WN = 1;
+template <int BM_ = 128, int BN_ = 32, int WM_ = 4, int WN_ = 1>
+struct PConv2DgradT {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
   Grid g;
   const float* dz2;   // [B][9][9][64]
@@ -431,12 +448,14 @@ struct PConv2Dgrad {
       }
   }
 };
+using PConv2Dgrad = PConv2DgradT<>;
+using PConv2DgradS = PConv2DgradT<64, 32, 4, 1>;
 
 // conv2 / conv3 weight gradient over sample chunk z (samples [z SC, min(B, (z + 1) SC))): rows m = (kh, kw, c),
 // cols oc, r = (b, oh, ow) ascending; partial slab[z][M + 1][OC] (row M = bias partial)
-template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC>
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
 struct PConvWgrad {
-  static constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
   static constexpr int MROWS = KS * KS * C, P = OH * OW, CHUNK = SC;
   Grid g;
@@ -467,6 +486,75 @@ struct PConvWgrad {
     for (int r = 0; r < 4; ++r) slab[((size_t)z * (MROWS + 1) + row + r) * OC + col] = v[r];
   }
   __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * OC + col] = v; }
+};
+
+// dW4[k][n] = fmaf chain over b of a4[b][k] dq[b][n]; db4[n] = sum over b of dq[b][n]; loss = (sum over b of h_b) / B.
+// Leading blocks of the fc1 backward launch (independent of its GEMM tiles), block t = one 16-row tile of the GEMM
+// [a4^T ; 1] [dq | h] on v_mfma_f32_16x16x4_f32 (b on the lane groups, so each output is the b-ordered chain; the
+// all-ones row 512 gives db4 and the loss sum, fmaf(1, v, s) = s + v).  Per 512 samples the block's four waves load
+// the tile's a4 columns and [dq | h] into LDS with every load in flight at once (40 KB, the GEMM tiles' own LDS size),
+// then wave 0 runs the chain from LDS: two memory latencies per launch instead of one per few MFMAs.
+struct SideFc2 {
+  static constexpr int BLOCKS = 33;   // 512 rows of a4^T + the ones row
+  static constexpr int HB = 512;      // samples per LDS pass
+  static constexpr size_t LDS = (size_t)HB * 20 * sizeof(float);
+  const float* a4;
+  const uint8_t* act;
+  const float* gs;
+  const float* hs;
+  int B;
+  float* dw4;
+  float* db4;
+  float* loss;
+  __device__ void run(int t, float* lds) const {
+    float* as = lds;              // [HB][16] a4 columns t*16 .. +15
+    float* ds = lds + HB * 16;    // [HB][4]  dq0, dq1, dq2, h
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, n = lane & 15;
+    f32x4 acc = zero4();
+    for (int b0 = 0; b0 < B; b0 += HB) {
+      __syncthreads();   // the previous pass's LDS reads are done
+      if (t < 32) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // 2,048 float4: row bl = q / 4, quarter q % 4
+          const int q = tid + 256 * j, bl = q >> 2, b = b0 + bl;
+          f32x4 v = zero4();
+          if (b < B) v = ld4(a4 + (size_t)b * 512 + t * 16 + (q & 3) * 4);
+          *reinterpret_cast<f32x4*>(as + q * 4) = v;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int bl = tid + 256 * j, b = b0 + bl;
+        f32x4 v = zero4();
+        if (b < B) {
+          const int a = act[b];
+          const float gv = gs[b];
+          v = f32x4{a == 0 ? gv : 0.0f, a == 1 ? gv : 0.0f, a == 2 ? gv : 0.0f, hs[b]};
+        }
+        *reinterpret_cast<f32x4*>(ds + bl * 4) = v;
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const int S = (min(HB, B - b0) + 3) / 4;   // zero rows past B leave the chains unchanged
+#pragma unroll 8
+        for (int s = 0; s < S; ++s) {
+          const int bl = 4 * s + g;
+          const float av = t < 32 ? as[bl * 16 + n] : (n == 0 ? 1.0f : 0.0f);
+          const float bv = n < 4 ? ds[bl * 4 + n] : 0.0f;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        }
+      }
+    }
+    if (tid >= 64) return;
+    if (t < 32) {
+      if (n < 3)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dw4[(t * 16 + 4 * g + i) * 3 + n] = acc[i];
+    } else if (g == 0) {
+      if (n < 3) db4[n] = acc[0];
+      else if (n == 3) *loss = acc[0] / (float)B;
+    }
+  }
 };
 
 #ifndef QLX_Q32_POLICIES_ONLY   // (scripts/q32_host_check.hip replays the policies on the host without the kernels)

@@ -93,6 +93,9 @@ int main(int argc, char** argv) {
   replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
   replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
   replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
+  replay(PConv2FwdS{grid(n * 81, 64, 64, 32, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd S");
+  replay(PConv3FwdS{grid(n * 49, 64, 64, 32, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd S");
+  replay(PFc1FwdS{grid(n, 32, 512, 32, 1), a3, w3, b3, a4, n}, "fc1_fwd S");
   // backward over B (activations of a B-sample forward)
   float* dz1 = buf<float>((size_t)B * 12800); float* dz2 = buf<float>((size_t)B * 5184);
   float* dz3 = buf<float>((size_t)B * 3136); float* dz4 = buf<float>((size_t)B * 512);
@@ -102,10 +105,14 @@ int main(int argc, char** argv) {
   float* gw3 = buf<float>(3136 * 512); float* gb3 = buf<float>(512);
   replay(PFc1Wgrad{grid(3136, 64, 512, 64, 1), a3, dz4, gw3, gb3, B}, "fc1_wgrad");
   replay(PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, w3, a3, dz3, B}, "fc1_dgrad");
+  replay(PFc1WgradS{grid(3136, 64, 512, 32, 1), a3, dz4, gw3, gb3, B}, "fc1_wgrad S");
+  replay(PFc1DgradS{grid(B, 32, 3136, 64, 1), dz4, w3, a3, dz3, B}, "fc1_dgrad S");
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   replay(PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad");
+  replay(PConv3DgradS{grid(B * 81, 32, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad S");
   replay(PConv3Wgrad{grid(576, 64, 64, 64, z3), a2, dz3, s3, B}, "conv3_wgrad");
   replay(PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad");
+  replay(PConv2DgradS{grid(B * 100, 64, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad S");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
   printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
   return 0;

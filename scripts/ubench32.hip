@@ -151,6 +151,26 @@ int main(int argc, char** argv) {
     run1("fc1_dgrad", PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, W3, a3, dz3, B}, 2.0 * B * 3136 * 512);
     run2("fc1_bwd pair", PFc1Wgrad{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B}, PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, W3, a3, dz3, B},
          4.0 * B * 3136 * 512);
+    {
+      uint8_t* act = nullptr;
+      CK(hipMalloc(&act, B));
+      CK(hipMemset(act, 1, B));
+      PFc1WgradS Pw{grid(3136, 64, 512, 32, 1), a3, dz4, gw, gw, B};
+      PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B};
+      SideFc2 S{a4, act, dz4, dz4 + 1024, B, gw, gw + 2000, gw + 3000};
+      const size_t lds = std::max({gemm_lds_bytes<PFc1WgradS>(), gemm_lds_bytes<PFc1DgradS>(), SideFc2::LDS});
+      double us = time_us([&] {
+        hipLaunchKernelGGL((k_gemm32_pair<PFc1WgradS, PFc1DgradS, SideFc2>), dim3(SideFc2::BLOCKS + Pw.g.blocks() + Pd.g.blocks()),
+                           dim3(256), lds, 0, Pw, Pd, S);
+      });
+      printf("%-34s %9.2f us\n", "fc1_bwd pair + SideFc2", us);
+      PFc1WgradS Pw0{Grid{0, 1, 1}, a3, dz4, gw, gw, B};
+      PFc1DgradS Pd0{Grid{0, 1, 1}, dz4, W3, a3, dz3, B};
+      us = time_us([&] {
+        hipLaunchKernelGGL((k_gemm32_pair<PFc1WgradS, PFc1DgradS, SideFc2>), dim3(SideFc2::BLOCKS), dim3(256), lds, 0, Pw0, Pd0, S);
+      });
+      printf("%-34s %9.2f us\n", "SideFc2 alone", us);
+    }
     run1("conv3_dgrad", PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, 2.0 * B * 49 * 64 * 576);
     run1("conv3_wgrad", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, B / 16), a2, dz3, slab, B},
          2.0 * B * 49 * 64 * 576);
@@ -166,6 +186,41 @@ int main(int argc, char** argv) {
              f / us / 1e6, f / us / 1e6 / 157.3 * 100);
     }
   }
+  printf("--- tile variants, B = 1024\n");
+  {
+    const int B = 1024;
+#define V(NAME, P, ...) run1(NAME " " #P, P{__VA_ARGS__}, flop)
+    double flop = 2.0 * B * 3136 * 512;
+    run1("fc1_fwd t32x32 w2x2", PFc1FwdT<32, 32, 2, 2>{grid(B, 32, 512, 32, 1), a3, W3, W3, a4, B}, flop);
+    run1("fc1_fwd t64x32 w2x2", PFc1FwdT<64, 32, 2, 2>{grid(B, 64, 512, 32, 1), a3, W3, W3, a4, B}, flop);
+    run1("fc1_fwd t64x64 w2x2", PFc1FwdT<64, 64, 2, 2>{grid(B, 64, 512, 64, 1), a3, W3, W3, a4, B}, flop);
+    run1("fc1_fwd t32x128 w2x2", PFc1FwdT<32, 128, 2, 2>{grid(B, 32, 512, 128, 1), a3, W3, W3, a4, B}, flop);
+    run1("fc1_dgrad t64x32 w2x2", PFc1DgradT<64, 32, 2, 2>{grid(B, 64, 3136, 32, 1), dz4, W3, a3, dz3, B}, flop);
+    run1("fc1_dgrad t32x64 w2x2", PFc1DgradT<32, 64, 2, 2>{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B}, flop);
+    run1("fc1_dgrad t128x64 w2x2", PFc1DgradT<128, 64, 2, 2>{grid(B, 128, 3136, 64, 1), dz4, W3, a3, dz3, B}, flop);
+    run1("fc1_wgrad t64x32 w2x2", PFc1WgradT<64, 32, 2, 2>{grid(3136, 64, 512, 32, 1), a3, dz4, gw, gw, B}, flop);
+    run1("fc1_wgrad t128x64 w2x2", PFc1WgradT<128, 64, 2, 2>{grid(3136, 128, 512, 64, 1), a3, dz4, gw, gw, B}, flop);
+    run1("fc1_wgrad t64x128 w2x2", PFc1WgradT<64, 128, 2, 2>{grid(3136, 64, 512, 128, 1), a3, dz4, gw, gw, B}, flop);
+    flop = 2.0 * B * 81 * 64 * 512;
+    run1("conv2_fwd t64x32 w2x2", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>{grid(B * 81, 64, 64, 32, 1), a1, W1, W1, a2, B * 81}, flop);
+    run1("conv2_fwd t32x64 w2x2", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 32, 64, 2, 2>{grid(B * 81, 32, 64, 64, 1), a1, W1, W1, a2, B * 81}, flop);
+    run1("conv2_fwd t128x64 w2x2", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 128, 64, 2, 2>{grid(B * 81, 128, 64, 64, 1), a1, W1, W1, a2, B * 81}, flop);
+    run1("conv2_fwd t128x64 w4x1", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 128, 64, 4, 1>{grid(B * 81, 128, 64, 64, 1), a1, W1, W1, a2, B * 81}, flop);
+    run1("conv2_dgrad t64x32 w2x2", PConv2DgradT<64, 32, 2, 2>{grid(B * 100, 64, 32, 32, 4), dz2, W1, a1, dz1, B * 100}, flop);
+    run1("conv2_dgrad t64x32 w4x1", PConv2DgradT<64, 32, 4, 1>{grid(B * 100, 64, 32, 32, 4), dz2, W1, a1, dz1, B * 100}, flop);
+    run1("conv2_dgrad t32x32 w2x2", PConv2DgradT<32, 32, 2, 2>{grid(B * 100, 32, 32, 32, 4), dz2, W1, a1, dz1, B * 100}, flop);
+    run1("conv2_wgrad t64x32 w2x2", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 32, 2, 2>{grid(512, 64, 64, 32, B / 16), a1, dz2, slab, B}, flop);
+    run1("conv2_wgrad t128x64 w2x2", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16, 128, 64, 2, 2>{grid(512, 128, 64, 64, B / 16), a1, dz2, slab, B}, flop);
+    flop = 2.0 * B * 49 * 64 * 576;
+    run1("conv3_fwd t64x32 w2x2", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>{grid(B * 49, 64, 64, 32, 1), a2, W2, W2, a3, B * 49}, flop);
+    run1("conv3_fwd t32x64 w2x2", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 32, 64, 2, 2>{grid(B * 49, 32, 64, 64, 1), a2, W2, W2, a3, B * 49}, flop);
+    run1("conv3_fwd t128x64 w2x2", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 128, 64, 2, 2>{grid(B * 49, 128, 64, 64, 1), a2, W2, W2, a3, B * 49}, flop);
+    run1("conv3_dgrad t64x32 w2x2", PConv3DgradT<64, 32, 2, 2>{grid(B * 81, 64, 64, 32, 1), dz3, W2, a2, dz2, B * 81}, flop);
+    run1("conv3_dgrad t32x64 w2x2", PConv3DgradT<32, 64, 2, 2>{grid(B * 81, 32, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
+    run1("conv3_dgrad t128x64 w2x2", PConv3DgradT<128, 64, 2, 2>{grid(B * 81, 128, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
+    run1("conv3_wgrad t64x32 w2x2", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 32, 2, 2>{grid(576, 64, 64, 32, B / 16), a2, dz3, slab, B}, flop);
+#undef V
+  }
   printf("--- generic GEMM (A row-major, B row-major)\n");
   {
     const int M = 8192, N = 4096, K = 4096;
@@ -173,11 +228,6 @@ int main(int argc, char** argv) {
     float* B = dbuf((size_t)K * N, 21);
     float* C = dbuf((size_t)M * N, 22);
     gen<64, 64, 2, 2>(M, N, K, A, B, C);
-    gen<128, 64, 2, 2>(M, N, K, A, B, C);
-    gen<128, 128, 2, 2>(M, N, K, A, B, C);
-    gen<64, 128, 2, 2>(M, N, K, A, B, C);
-    gen<128, 32, 4, 1>(M, N, K, A, B, C);
-    gen<32, 64, 2, 2>(M, N, K, A, B, C);
     gen<64, 64, 2, 2>(65536, 64, 512, A, B, C);
     gen<128, 64, 2, 2>(65536, 64, 512, A, B, C);
     gen<64, 32, 4, 1>(65536 * 4, 32, 256, A, B, C);
