@@ -42,14 +42,15 @@ TRANSITION_BYTES = 56_454          # logical (a, s, s', r, done) of one sampled 
 ADAM_BYTES = 53_941_344            # clip_by_norm + Adam per update: g read twice, w / m / v read and written
 # profiler scopes of each precision: the GEMM-shaped kernels (FLOP work) and their per-layer grouping
 GEMM_SCOPES = {
-    "fp32": ("f32_conv1_fwd", "f32_conv2_fwd", "f32_conv3_fwd", "f32_fc1_fwd", "f32_fc1_bwd", "f32_conv3_bwd",
-             "f32_conv2_bwd", "f32_conv1_wgrad"),
+    "fp32": ("f32_conv1_fwd", "f32_conv2_fwd", "f32_conv3_fwd", "f32_fc1_fwd", "f32_conv1_fwd_big", "f32_conv2_fwd_big",
+             "f32_conv3_fwd_big", "f32_fc1_fwd_big", "f32_fc1_bwd", "f32_conv3_bwd", "f32_conv2_bwd", "f32_conv1_wgrad"),
     "bf16": ("trunk_fwd", "trunk_fwd_nostore", "trunk_bwd_data", "fc1_fwd", "fc1_bwd", "conv23_wgrad", "conv1_wgrad"),
 }
 ADAM_SCOPES = {"fp32": ("f32_norms", "f32_adam"), "bf16": ("sumsq", "adam")}
 # the kernels that deliver sampled transitions into the net: index draw, gather, and the conv1 frame fetch of the
-# online and target passes (fp32: conv1 is its own launch)
-SAMPLE_SCOPES = {"fp32": ("sample", "gather", "f32_conv1_fwd"), "bf16": ("sample", "gather")}
+# online pass (s) and of the batched target pass (s'; conv1_fwd_big, which also runs the one acting chunk: its share is
+# taken by sample count)
+SAMPLE_SCOPES = {"fp32": ("sample", "gather", "f32_conv1_fwd", "f32_conv1_fwd_big"), "bf16": ("sample", "gather")}
 
 
 def parse():
@@ -291,7 +292,9 @@ class Run:
                 layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
         upd = self.updates / max(self.steps, 1) / max(self.ctl.world, 1)   # updates per vector step on one GPU
         B = self.args.batch
-        t_samp = sum(c[k]["total_us_per_step"] for k in SAMPLE_SCOPES[self.precision] if k in c)
+        t_samp = sum(c[k]["total_us_per_step"] for k in SAMPLE_SCOPES[self.precision][:3] if k in c)
+        if "f32_conv1_fwd_big" in c:   # the target chunks' share (U*B of the U*B + n_envs samples per vector step)
+            t_samp += c["f32_conv1_fwd_big"]["total_us_per_step"] * upd * B / (upd * B + self.args.envs)
         samp_gbs = rate(upd * B * TRANSITION_BYTES, t_samp, 1e3)
         t_adam = sum(c[k]["total_us_per_step"] for k in ADAM_SCOPES[self.precision] if k in c)
         adam_gbs = rate(upd * ADAM_BYTES, t_adam, 1e3)

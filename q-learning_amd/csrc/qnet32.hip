@@ -5,6 +5,7 @@
 // batch_predict_max_future_reward), :63-82 (train_model; intended q_a = Q(s)[a] of
 // create_ql_model_ballgame_3x3x4_5_512.py:71-78), legacy Keras Adam(lr 2.5e-4, clipnorm 1.0) = tf.clip_by_norm per
 // variable + ResourceApplyAdam, Huber(delta = 1) mean over the batch.  Orders of every reduction: DESIGN.md §6.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -289,20 +290,26 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   w.fgrad_batch = B;
 }
 
+// Every fp32 launch is timed (when the learner profiles) by start / stop events bound to its own dispatch
+// (hipExtLaunchKernelGGL), so a scope's average is the kernel's duration as a kernel trace reports it.
 template <class P>
-static void launch(qlx_model*, const P& p, int, hipStream_t s) {
-  hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), s, p);
+static void launch(qlx_model* m, const P& p, const char* scope, double work, hipStream_t s) {
+  hipEvent_t ea = nullptr, eb = nullptr;
+  if (m->prof) m->prof->ext(scope, work, &ea, &eb);
+  hipExtLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), s, ea, eb, 0u, p);
   QLX_HIP(hipGetLastError());
-  debug_sync(s, __PRETTY_FUNCTION__);
+  debug_sync(s, scope);
 }
 
 template <class P1, class P2, class S>
-static void launch_pair(qlx_model*, const P1& p1, const P2& p2, const S& side, int, hipStream_t s) {
+static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side, const char* scope, double work, hipStream_t s) {
   const size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS});
-  hipLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, p1, p2,
-                     side);
+  hipEvent_t ea = nullptr, eb = nullptr;
+  if (m->prof) m->prof->ext(scope, work, &ea, &eb);
+  hipExtLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, ea, eb, 0u,
+                        p1, p2, side);
   QLX_HIP(hipGetLastError());
-  debug_sync(s, __PRETTY_FUNCTION__);
+  debug_sync(s, scope);
 }
 
 static int num_cus() {
@@ -326,32 +333,35 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
   const float* p = m->d_params;
   for (int c0 = 0; c0 < B; c0 += w.fchunk) {
     const int n = std::min(w.fchunk, B - c0);
-    {
-      ProfScope ps(m->prof, "f32_conv1_fwd", s, 2.0 * n * 400 * 32 * 256);
-      set_lds_limit((const void*)k_conv1_fwd32, 2 * kC1Frames);
-      hipLaunchKernelGGL(k_conv1_fwd32, dim3(std::min(n, 2 * num_cus())), dim3(256), 2 * kC1Frames, s, table + (size_t)c0 * 4, n,
-                         p + voff(0), p + voff(1), w.fa1);
-      QLX_HIP(hipGetLastError());
-      debug_sync(s, "k_conv1_fwd32");
-    }
-    // tiles by batch: at chunk-size batches 64 x 64 tiles run best (~65 % of the fp32 peak), at training-size batches
-    // the narrower tiles that put more blocks on the chip (scripts/ubench32.hip sweep)
+    // tiles by batch: at chunk-size batches (target pass, acting) 64 x 64 tiles run best (~65 % of the fp32 peak), at
+    // training-size batches the narrower tiles that put more blocks on the chip (scripts/ubench32.hip sweep); the two
+    // shapes are separate kernels and separate profiler scopes (suffix _big)
     const bool big = n > 2048;
     {
-      ProfScope ps(m->prof, "f32_conv2_fwd", s, 2.0 * n * 81 * 64 * 512);
-      if (big) launch(m, PConv2Fwd{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, n, s);
-      else launch(m, PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, n, s);
+      const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
+      hipEvent_t ea = nullptr, eb = nullptr;
+      if (m->prof) m->prof->ext(sc, 2.0 * n * 400 * 32 * 256, &ea, &eb);
+      auto kern = big ? k_conv1_fwd32<1> : k_conv1_fwd32<0>;
+      set_lds_limit((const void*)kern, 2 * kC1Frames);
+      hipExtLaunchKernelGGL(kern, dim3(std::min(n, 2 * num_cus())), dim3(256), 2 * kC1Frames, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
+                            p + voff(0), p + voff(1), w.fa1);
+      QLX_HIP(hipGetLastError());
+      debug_sync(s, sc);
     }
-    {
-      ProfScope ps(m->prof, "f32_conv3_fwd", s, 2.0 * n * 49 * 64 * 576);
-      if (big) launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, n, s);
-      else launch(m, PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, n, s);
-    }
-    {
-      ProfScope ps(m->prof, "f32_fc1_fwd", s, 2.0 * n * 3136 * 512);
-      float* a4 = w.fa4 + (size_t)c0 * 512;
-      if (big) launch(m, PFc1Fwd{grid(n, 32, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), a4, n}, n, s);
-      else launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), a4, n}, n, s);
+    if (big) {
+      launch(m, PConv2Fwd{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, "f32_conv2_fwd_big",
+             2.0 * n * 81 * 64 * 512, s);
+      launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd_big",
+             2.0 * n * 49 * 64 * 576, s);
+      launch(m, PFc1Fwd{grid(n, 32, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
+             2.0 * n * 3136 * 512, s);
+    } else {
+      launch(m, PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, "f32_conv2_fwd",
+             2.0 * n * 81 * 64 * 512, s);
+      launch(m, PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd",
+             2.0 * n * 49 * 64 * 576, s);
+      launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
+             2.0 * n * 3136 * 512, s);
     }
   }
 }
@@ -389,12 +399,11 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_dz4_32");
   }
-  {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its three leading blocks
-    ProfScope ps(m->prof, "f32_fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
+  {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its leading blocks
     PFc1WgradS Pw{grid(3136, 64, 512, 32, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
     PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
     SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
-    launch_pair(m, Pw, Pd, S, B, s);
+    launch_pair(m, Pw, Pd, S, "f32_fc1_bwd", 2.0 * 2.0 * B * 512 * 3136, s);
   }
 }
 
@@ -403,23 +412,24 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   const float* p = m->d_params;
   float* G = m->d_grads;
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
+  // algorithmic FLOPs (backward-data + weight gradient of the layer; the padded taps the dgrad tiles multiply are
+  // not counted)
   {  // conv3: dz2 tiles + weight-gradient chunk tiles
-    ProfScope ps(m->prof, "f32_conv3_bwd", s, 2.0 * 2.0 * B * 49 * 64 * 576);
     PConv3DgradS Pd{grid(B * 81, 32, 64, 64, 1), w.fdz3, p + voff(4), w.fa2, w.fdz2, B * 81};
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-    launch_pair(m, Pw, Pd, NoSide{}, B, s);
+    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 tiles (4 parity classes) + weight-gradient chunk tiles
-    ProfScope ps(m->prof, "f32_conv2_bwd", s, 2.0 * B * 81 * 64 * 512 + 2.0 * B * 400 * 32 * 256);
     PConv2DgradS Pd{grid(B * 100, 64, 32, 32, 4), w.fdz2, p + voff(2), w.fa1, w.fdz1, B * 100};
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
-    launch_pair(m, Pw, Pd, NoSide{}, B, s);
+    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
-    ProfScope ps(m->prof, "f32_conv1_wgrad", s, 2.0 * B * 400 * 256 * 32);
     constexpr size_t lds = kC1Frames + 400 * 16 * 4;
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);
-    hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(256), lds, s, table, w.fdz1, B, z1, w.fslab1);
+    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(256), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv1_wgrad32");
   }

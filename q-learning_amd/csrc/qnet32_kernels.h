@@ -589,6 +589,9 @@ __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >>
 // forward: a1[b][r][oc] = relu(chain over k = (kh, kw, c) of x * W0[kh][kw][c][oc] + b0[oc]), r = (oh, ow).
 // Wave w owns output channels (w & 1) * 16 .. + 15 and the 16-row tiles rt = (w >> 1) + 2 j (13 / 12 of the 25); one
 // v_mfma_f32_16x16x4_f32 per (tile, kh, kw) with c on the lane groups, W0 fragments resident in VGPRs.
+// ROLE only names the instantiation (0: training batches, 1: chunk-size target / acting passes), so a kernel trace
+// tells the two launch shapes apart
+template <int ROLE>
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0, const float* b0,
                                                         float* a1) {
   extern __shared__ __attribute__((aligned(16))) uint8_t c1lds[];   // [2][4][7056]
