@@ -425,7 +425,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
-    constexpr size_t lds = kC1Frames + 400 * 16 * 4;
+    constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
     hipEvent_t ea = nullptr, eb = nullptr;
     if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);

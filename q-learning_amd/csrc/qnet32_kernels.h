@@ -559,10 +559,13 @@ struct SideFc2 {
 
 #ifndef QLX_Q32_POLICIES_ONLY   // (scripts/q32_host_check.hip replays the policies on the host without the kernels)
 // conv1 (8x8 stride 4, 4 -> 32 channels) from the u8 frames, one sample at a time per block with the sample's four
-// frames (28,224 B, s2d layout) staged in LDS while the next sample's frames are in flight in registers.
-
-constexpr int kC1Frames = 4 * kFramePix;   // 28,224 B of one sample's frames
-constexpr int kC1Chunks = kC1Frames / 16;  // 1,764 uint4
+// frames staged in LDS while the next sample's frames are in flight in registers.
+// LDS frame layout (rows): slot c, image row x, dword y / 4 holds pixels (x, y .. y + 3) at dword c * 1776 + x * 21 + y / 4.
+// Rows of 21 dwords make 16 consecutive output positions (oh, ow) hit 16 consecutive banks (84 = 20 mod 64 dwords per
+// oh step), and the slot stride 1,776 = 48 mod 64 puts the four slots (the MFMA lane groups) on disjoint bank ranges.
+constexpr int kC1SlotDw = 1776;                 // 84 rows x 21 dwords + 12 (bank skew)
+constexpr int kC1Frames = 4 * kC1SlotDw * 4;    // 28,416 B of one sample's frames in LDS
+constexpr int kC1Chunks = 4 * kFramePix / 16;   // 1,764 s2d uint4 chunks in HBM
 
 // next sample's frames into registers (null table entry = the zero frame)
 __device__ __forceinline__ void c1_prefetch(const uint8_t* const* table, int b, uint4 (&pf)[7]) {
@@ -577,11 +580,20 @@ __device__ __forceinline__ void c1_prefetch(const uint8_t* const* table, int b, 
     }
   }
 }
-__device__ __forceinline__ void c1_stage(uint8_t* dst, const uint4 (&pf)[7]) {
+// s2d chunk (slot, block row bx, block column by) = pixels x = 4 bx + xl, y = 4 by .. 4 by + 3 in component xl
+__device__ __forceinline__ void c1_put(uint32_t* dst, int q, const uint4& v) {
+  const int slot = q / 441, pos = q - slot * 441, bx = pos / 21, by = pos - bx * 21;
+  uint32_t* d = dst + slot * kC1SlotDw + 4 * bx * 21 + by;
+  d[0] = v.x;
+  d[21] = v.y;
+  d[42] = v.z;
+  d[63] = v.w;
+}
+__device__ __forceinline__ void c1_stage(uint32_t* dst, const uint4 (&pf)[7]) {
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     const int q = threadIdx.x + 256 * j;
-    if (q < kC1Chunks) *reinterpret_cast<uint4*>(dst + q * 16) = pf[j];
+    if (q < kC1Chunks) c1_put(dst, q, pf[j]);
   }
 }
 __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >> (8 * i)) & 0xFFu); }
@@ -594,7 +606,7 @@ __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >>
 template <int ROLE>
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0, const float* b0,
                                                         float* a1) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t c1lds[];   // [2][4][7056]
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // [2][4 slots][1776 dwords]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ct = wave & 1, rp = wave >> 1;
@@ -603,35 +615,38 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 #pragma unroll
   for (int kk = 0; kk < 64; ++kk) wf[kk] = w0[(kk * 4 + g) * 32 + col];
   const float bias = b0[col];
-  int ob[13];
+  // dword offsets of the lane's 13 tile rows (lane group g reads ring slot g), two 16-bit offsets per register
+  uint32_t ob2[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) ob2[j] = 0;
 #pragma unroll
   for (int j = 0; j < 13; ++j) {
     const int r = (rp + 2 * j) * 16 + (lane & 15);
     const int oh = r / 20, ow = r - oh * 20;
-    ob[j] = g * kFramePix + (oh * kBlocks + ow) * 16;   // lane group g reads ring slot g
+    ob2[j >> 1] |= (uint32_t)(g * kC1SlotDw + 4 * oh * 21 + ow) << (16 * (j & 1));
   }
   const int nt = rp == 0 ? 13 : 12;
   int b = blockIdx.x;
   if (b >= B) return;
   uint4 pf[7];
   c1_prefetch(table, b, pf);
-  c1_stage(c1lds, pf);
+  c1_stage(c1w, pf);
   __syncthreads();
   for (int it = 0; b < B; b += gridDim.x, ++it) {
-    const uint8_t* fr = c1lds + (it & 1) * kC1Frames;
+    const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
     const int nb = b + gridDim.x;
     if (nb < B) c1_prefetch(table, nb, pf);
     f32x4 acc[13];
 #pragma unroll
     for (int j = 0; j < 13; ++j) acc[j] = zero4();
 #pragma unroll
-    for (int kq = 0; kq < 16; ++kq) {   // (kh, kw half): 4 pixels of one s2d block per lane and tile
+    for (int kq = 0; kq < 16; ++kq) {   // (kh, kw half): pixels (4 oh + kh, 4 ow + 4 hw .. + 3) per lane and tile
       const int kh = kq >> 1, hw = kq & 1;
-      const int off = (kh >> 2) * kBlocks * 16 + (kh & 3) * 4 + hw * 16;
+      const int off = kh * 21 + hw;
       uint32_t d[13];
 #pragma unroll
       for (int j = 0; j < 13; ++j)
-        if (j < nt) d[j] = *reinterpret_cast<const uint32_t*>(fr + ob[j] + off);
+        if (j < nt) d[j] = fr[((ob2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + off];
 #pragma unroll
       for (int kw = 0; kw < 4; ++kw)
 #pragma unroll
@@ -645,20 +660,21 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[j][i] + bias);
       }
-    if (nb < B) c1_stage(c1lds + ((it + 1) & 1) * kC1Frames, pf);
+    if (nb < B) c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);
     __syncthreads();
   }
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
 // x[r][m] dz1[r][oc], m = (kh, kw, c) HWIO, and slab[z][256][oc] = the same chain of dz1 (bias).  Block (z, hh) covers
-// output channels hh * 16 .. + 15; wave w the 16-row tiles 4 w .. 4 w + 3.  Per sample the frames and dz1's channel
-// half sit in LDS (53,824 B) while the next sample's are in flight in registers.
+// output channels hh * 16 .. + 15; wave w the 16-row tiles 4 w .. 4 w + 3.  Per sample the frames (row layout) and
+// dz1's channel half sit in LDS (54,016 B) while the next sample's are in flight in registers.
 constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
 __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
                                                           float* slab) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t c1lds[];   // frames [4][7056], then dz [400][16] f32
-  float* dzs = reinterpret_cast<float*>(c1lds + kC1Frames);
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1776] dwords, then dz [400][16] f32
+  const uint8_t* fb = reinterpret_cast<const uint8_t*>(c1w);
+  float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1SlotDw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int z = blockIdx.x % nz, hh = blockIdx.x / nz;
@@ -671,7 +687,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* 
   for (int t = 0; t < 4; ++t) {
     const int m = (wave * 4 + t) * 16 + (lane & 15);
     const int kh = m >> 5, kw = (m >> 2) & 7, c = m & 3;
-    mo[t] = c * kFramePix + ((kh >> 2) * kBlocks + (kw >> 2)) * 16 + (kh & 3) * 4 + (kw & 3);
+    mo[t] = c * kC1SlotDw * 4 + kh * 84 + kw;
   }
   uint4 pf[14];
   auto prefetch = [&](int b) {
@@ -693,7 +709,8 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* 
 #pragma unroll
     for (int j = 0; j < 14; ++j) {
       const int q = tid + 256 * j;
-      if (q < kC1Chunks + kC1DzChunks) *reinterpret_cast<uint4*>(c1lds + q * 16) = pf[j];
+      if (q < kC1Chunks) c1_put(c1w, q, pf[j]);
+      else if (q < kC1Chunks + kC1DzChunks) *reinterpret_cast<uint4*>(dzs + (q - kC1Chunks) * 4) = pf[j];
     }
   };
   f32x4 acc[4];
@@ -710,9 +727,9 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* 
     for (int rs = 0; rs < 100; ++rs) {
       const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
       const float bv = dzs[r * 16 + (lane & 15)];
-      const int px = (oh * kBlocks + ow) * 16;
+      const int px = oh * 336 + ow * 4;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)c1lds[mo[t] + px], bv, acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)fb[mo[t] + px], bv, acc[t], 0, 0, 0);
       if (wave == 0) {   // bias chain in r order: lane groups hold r = 4 rs + 0 .. 3
         const float v1 = __shfl(bv, lane + 16), v2 = __shfl(bv, lane + 32), v3 = __shfl(bv, lane + 48);
         bsum = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(bsum, bv), v1), v2), v3);
