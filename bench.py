@@ -109,6 +109,14 @@ class Control:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def min(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return float(t.item())
+
     def sum(self, x):
         if not self.dist:
             return x
@@ -165,6 +173,8 @@ def config_label(N, replay, flags, world):
         return "C5"
     if flags == 3 and world == 1 and N == 8192:
         return "C5 (one GPU's shard)"
+    if flags == 0 and world > 1 and N == 8192 and replay == 1_000_000:
+        return f"C3 per GPU x {world} (weak scaling)"
     return f"custom ({world} GPU)"
 
 
@@ -217,12 +227,15 @@ class Run:
             L.close()
 
     def _desync(self, L, p):
+        # the stop decision is global (min over ranks): every rank must run the same number of vector steps, since each
+        # one carries collectives (the episode-statistics all-reduce)
         run, n, last = 0, 0, L.stats()["episode_count"]
         while run < STEADY_RUN and n < MAX_DESYNC:
             L.prefill(1)
             n += 1
             e = L.stats()["episode_count"]
-            run = run + 1 if e > last else 0
+            ended = self.ctl.min(1.0 if e > last else 0.0)
+            run = run + 1 if ended > 0 else 0
             last = e
         log(f"{self.precision}: {n} more vector steps until episodes end every step ({run} in a row)")
         return n
@@ -333,8 +346,8 @@ def control_check(ctl):
     every rank.  Rank 0 prints one JSON line."""
     uid = ctl.bcast_bytes(bytes(range(128)) if ctl.rank == 0 else bytes(128))
     ctl.barrier()
-    out = {"world": ctl.world, "max_rank": ctl.max(float(ctl.rank)), "sum_ones": ctl.sum(1.0),
-           "uid_ok": ctl.sum(1.0 if uid == bytes(range(128)) else 0.0) == ctl.world}
+    out = {"world": ctl.world, "max_rank": ctl.max(float(ctl.rank)), "min_rank": ctl.min(float(ctl.rank)),
+           "sum_ones": ctl.sum(1.0), "uid_ok": ctl.sum(1.0 if uid == bytes(range(128)) else 0.0) == ctl.world}
     ctl.barrier()
     if ctl.rank == 0:
         print(json.dumps(out), flush=True)

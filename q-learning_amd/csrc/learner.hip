@@ -240,6 +240,12 @@ struct qlx_learner {
   // reward} all-reduced on the learner stream (d_gsum[3], d_gmin[1])
   float* d_gsum = nullptr;
   float* d_gmin = nullptr;
+  // QLX_TARGET_OVERLAP=1: the batched target pass after its first chunk runs on tgt_stream beside the update chain;
+  // update u waits for the event of its chunk (fp32, no double DQN)
+  bool tgt_overlap = false;
+  hipStream_t tgt_stream = nullptr;
+  hipEvent_t ev_gather = nullptr;
+  std::vector<hipEvent_t> ev_tgt;
   qlx::Profiler prof;
   // statistics events (write_checkpoint + learning_update_log, self_driving_tf_q_learner.rs:204-212,226-230)
   uint64_t stats_events = 0;
@@ -255,6 +261,25 @@ namespace qlx {
 // updates run (a target sync happens only between vector steps) and all U batches were sampled up front
 // from the same replay state, so y = r + gamma * max_a Q_target(s') (or r if done) for the U*B sampled
 // transitions is one batched forward - the same values as U separate passes.
+// updates per target chunk of the overlapped target pass (kF32FwdChunk samples at B = 1024)
+static uint32_t tgt_chunk_updates(const qlx_learner* L) { return std::max<uint32_t>(1, (uint32_t)kF32FwdChunk / L->B); }
+
+// y for the updates [u0, u0 + nu) from the target net on stream s (after the gather)
+static void learner_targets_range(qlx_learner* L, uint32_t u0, uint32_t nu, const float* q_select, hipStream_t s) {
+  const uint32_t n = nu * L->B;
+  const size_t o = (size_t)u0 * L->B;
+  qlx_model* tg = L->target;
+  model_workspace(tg, (int)n);
+  model_forward_trunk(tg, L->d_tab_sn + o * 4, (int)n, s, false);
+  Fc2Args ta = fc2_args(tg, (int)n);
+  ta.q_select = q_select ? q_select + o * kActions : nullptr;
+  ta.rewards = L->d_brew + o;
+  ta.dones = L->d_bdone + o;
+  ta.gamma = L->p.gamma;
+  ta.y_out = L->d_targets + o;
+  launch_fc2(2, ta, (int)n, s);
+}
+
 static void learner_targets(qlx_learner* L, uint32_t U) {
   hipStream_t s = L->stream;
   const uint32_t n = U * L->B;
@@ -273,16 +298,20 @@ static void learner_targets(qlx_learner* L, uint32_t U) {
     launch_fc2(0, oa, (int)n, s);
     q_select = on->w.q;
   }
-  qlx_model* tg = L->target;
-  model_workspace(tg, (int)n);
-  model_forward_trunk(tg, L->d_tab_sn, (int)n, s, false);
-  Fc2Args ta = fc2_args(tg, (int)n);
-  ta.q_select = q_select;
-  ta.rewards = L->d_brew;
-  ta.dones = L->d_bdone;
-  ta.gamma = L->p.gamma;
-  ta.y_out = L->d_targets;
-  launch_fc2(2, ta, (int)n, s);
+  if (!L->tgt_overlap) {
+    learner_targets_range(L, 0, U, q_select, s);
+    return;
+  }
+  // first chunk on the learner stream (update 0 needs it now), the rest beside the update chain
+  const uint32_t C = tgt_chunk_updates(L), c0 = std::min(C, U);
+  learner_targets_range(L, 0, c0, nullptr, s);
+  if (c0 == U) return;
+  QLX_HIP(hipEventRecord(L->ev_gather, s));
+  QLX_HIP(hipStreamWaitEvent(L->tgt_stream, L->ev_gather, 0));
+  for (uint32_t u0 = c0, c = 1; u0 < U; u0 += C, ++c) {
+    learner_targets_range(L, u0, std::min(C, U - u0), nullptr, L->tgt_stream);
+    QLX_HIP(hipEventRecord(L->ev_tgt[c], L->tgt_stream));
+  }
 }
 
 static void learner_update(qlx_learner* L, uint32_t u_local) {
@@ -401,7 +430,11 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
     }
     debug_sync(s, "sample");
     learner_targets(L, U);
-    for (uint32_t u = 0; u < U; ++u) learner_update(L, u);
+    const uint32_t C = tgt_chunk_updates(L);
+    for (uint32_t u = 0; u < U; ++u) {
+      if (L->tgt_overlap && u >= C && u % C == 0) QLX_HIP(hipStreamWaitEvent(s, L->ev_tgt[u / C], 0));
+      learner_update(L, u);
+    }
     if (L->per) {
       ProfScope ps(&L->prof, "priorities", s);
       per_launch_update(s, L->d_idx, L->prio.d_td, U * L->B, cap, start, L->p.per_alpha, L->p.per_eps, L->prio.d_owner,
@@ -528,6 +561,14 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
       if (L->ddqn) model_workspace(L->online, (int)(L->max_updates * B));   // + the online pass over s'
       if (L->per) L->prio.init(p->history_buffer_len, UB);
+      const char* tov = std::getenv("QLX_TARGET_OVERLAP");
+      L->tgt_overlap = tov && tov[0] == '1' && p->qnet_precision == QLX_PREC_F32 && !L->ddqn;
+      if (L->tgt_overlap) {
+        QLX_HIP(hipStreamCreateWithFlags(&L->tgt_stream, hipStreamNonBlocking));
+        QLX_HIP(hipEventCreateWithFlags(&L->ev_gather, hipEventDisableTiming));
+        L->ev_tgt.resize(L->max_updates / tgt_chunk_updates(L) + 2, nullptr);
+        for (auto& e : L->ev_tgt) QLX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
       QLX_HIP(hipStreamSynchronize(L->stream));
     } catch (...) {
       qlx_learner_destroy(L);
@@ -545,8 +586,14 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
     if (L->comm_stream) (void)hipStreamSynchronize(L->comm_stream);
     if (L->comm) (void)ncclCommDestroy(L->comm);
     if (L->comm_stream) (void)hipStreamDestroy(L->comm_stream);
-    for (hipEvent_t e : {L->ev_dense, L->ev_reduced})
+    for (hipEvent_t e : {L->ev_dense, L->ev_reduced, L->ev_gather})
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : L->ev_tgt)
+      if (e) (void)hipEventDestroy(e);
+    if (L->tgt_stream) {
+      (void)hipStreamSynchronize(L->tgt_stream);
+      (void)hipStreamDestroy(L->tgt_stream);
+    }
     qlx_env_destroy(L->env);
     qlx_replay_destroy(L->rb);
     qlx_model_destroy(L->online);
@@ -752,7 +799,7 @@ int32_t qlx_learner_update_log(qlx_learner* L, char* buf, size_t cap, size_t* le
 // stats_after_steps, and once more when an episode ended and solved() holds.  The log text goes to the callback (the
 // reference's log::info!) and stays readable through qlx_learner_last_log.  With stats_after_steps = 0 nothing runs.
 static void learner_stats_event(qlx_learner* L) {
-  if (L->p.checkpoint_file[0]) {
+  if (L->p.checkpoint_file[0] && L->rank == 0) {   // data parallel: the weights are identical, rank 0 writes the file
     char path[257];
     std::memcpy(path, L->p.checkpoint_file, 256);
     path[256] = 0;

@@ -102,4 +102,4 @@ def test_bench_spawns_ranks_and_runs_control_plane():
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(line) == 1, out.stdout
     r = json.loads(line[0])
-    assert r == {"world": 2, "max_rank": 1.0, "sum_ones": 2.0, "uid_ok": True}
+    assert r == {"world": 2, "max_rank": 1.0, "min_rank": 0.0, "sum_ones": 2.0, "uid_ok": True}
