@@ -12,9 +12,11 @@
 //   Huber head      e = q_a - y, h = w (|e| <= 1 ? (0.5 e) e : |e| - 0.5), g = (w clip(e, -1, 1)) / B,
 //                   loss = (sum over b ascending of h) / B
 //   dense-3 bwd     dz4[b][k] = a4 > 0 ? W4[k][a_b] g_b : 0; dW4[k][n] = chain over b of a4[b][k] dq[b][n]
-//   dense-512 bwd   dW3[k][n] = chain over b of a3[b][k] dz4[b][n]; db3 = sum over b; dz3 = a3 > 0 ? chain over n : 0
+//   dense-512 bwd   dW3[k][n] = chain over b of a3[b][k] dz4[b][n]; dz3 = a3 > 0 ? chain over n : 0
 //   conv dgrad      dz_in[b][ih][iw][c] = a_in > 0 ? chain over the valid taps (kh, kw, oc) lexicographic : 0
 //   conv wgrad      per sample chunk z of SC_l samples: P_z = chain over (b, oh, ow) ascending; dW = ((0 + P_0) + P_1) ..
+//                   bias: P_z = ((C0 + C1) + C2) + C3, Cq = chain over the chunk-local rows r = q mod 4 ascending
+//   dense-512 db3   ((C0 + C1) + C2) + C3, Cq = chain over b = q mod 4 ascending
 //   clip_by_norm    per variable: segments of 8192 elements; 256 lane chains fmaf(g, g, t) over i = lane mod 256;
 //                   4 x 64-lane xor butterflies (32 .. 1); ((w0 + w1) + w2) + w3; segments summed in order
 //   Adam            legacy ResourceApplyAdam with explicit roundings (qnet_ref.cpp)
@@ -117,17 +119,19 @@ void qnet32_forward(const QNet& q, const uint8_t* x8, int B, Acts& a) {
 static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const float* dz, int B, int SC, float* dW, float* db) {
   const int KK = c.K * c.K * c.C, nz = (B + SC - 1) / SC;
   std::vector<float> part((size_t)nz * (KK + 1) * c.OC, 0.0f);
+  std::vector<float> Pq((size_t)nz * 4 * c.OC, 0.0f);   // bias: chains C0..C3 per chunk
 #pragma omp parallel for schedule(dynamic)
   for (int z = 0; z < nz; ++z) {
     float* P = part.data() + (size_t)z * (KK + 1) * c.OC;
-    float* Pb = P + (size_t)KK * c.OC;
     for (int b = z * SC; b < std::min(B, (z + 1) * SC); ++b)
       for (int oh = 0; oh < c.OH; ++oh)
         for (int ow = 0; ow < c.OW; ++ow) {
           const float* d = dz + (((size_t)b * c.OH + oh) * c.OW + ow) * c.OC;
           bool any = false;
           for (int oc = 0; oc < c.OC; ++oc) {
-            Pb[oc] = Pb[oc] + d[oc];
+            // four interleaved chains over the chunk-local row index r mod 4 (combined below)
+            float* Cq = Pq.data() + ((size_t)z * 4 + ((b - z * SC) * c.OH * c.OW + oh * c.OW + ow) % 4) * c.OC;
+            Cq[oc] = Cq[oc] + d[oc];
             any |= d[oc] != 0.0f;
           }
           if (!any) continue;   // fmaf(x, 0, acc) == acc
@@ -148,6 +152,11 @@ static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const 
     for (int z = 0; z < nz; ++z) t = t + part[(size_t)z * (KK + 1) * c.OC + i];
     dW[i] = t;
   }
+  for (int z = 0; z < nz; ++z)   // bias partial of chunk z = ((C0 + C1) + C2) + C3
+    for (int oc = 0; oc < c.OC; ++oc) {
+      const float* C = Pq.data() + (size_t)z * 4 * c.OC;
+      part[((size_t)z * (KK + 1) + KK) * c.OC + oc] = ((C[oc] + C[c.OC + oc]) + C[2 * c.OC + oc]) + C[3 * c.OC + oc];
+    }
   for (int oc = 0; oc < c.OC; ++oc) {
     float t = 0.0f;
     for (int z = 0; z < nz; ++z) t = t + part[((size_t)z * (KK + 1) + KK) * c.OC + oc];
@@ -237,10 +246,10 @@ float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* acti
       for (int n = 0; n < 512; ++n) row[n] = fma32(v, d[n], row[n]);
     }
   }
-  for (int n = 0; n < 512; ++n) {
-    float s = 0.0f;
-    for (int b = 0; b < B; ++b) s = s + dz4[(size_t)b * 512 + n];
-    g.g[7][n] = s;
+  for (int n = 0; n < 512; ++n) {   // db3: four chains over b mod 4, ((C0 + C1) + C2) + C3
+    float C[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < B; ++b) C[b % 4] = C[b % 4] + dz4[(size_t)b * 512 + n];
+    g.g[7][n] = ((C[0] + C[1]) + C[2]) + C[3];
   }
   std::vector<float> W3T((size_t)512 * 3136);
   for (int k = 0; k < 3136; ++k)

@@ -160,20 +160,42 @@ void learner_book_stats(const Book& b, const float* ring, uint32_t ring_cap, flo
 }
 
 // ---- replay sample gather: frame pointer tables + metadata of one update ------------------------
+// (ycache != null: the Bellman target of each sampled slot is read from the per-slot memo instead, see ycache_fill)
 __global__ void k_gather(ReplayView r, const uint64_t* idx, uint32_t B, const uint8_t** tab_s, const uint8_t** tab_sn,
-                         uint8_t* act, float* rew, uint8_t* done) {
+                         uint8_t* act, float* rew, uint8_t* done, const float* ycache, float* y) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const uint64_t i = idx[b];
   const uint8_t* f[4];
   replay_frames(r, i, 0, f);
   for (int j = 0; j < 4; ++j) tab_s[b * 4 + j] = f[j];
-  replay_frames(r, i, 1, f);
-  for (int j = 0; j < 4; ++j) tab_sn[b * 4 + j] = f[j];
   const uint64_t t = (r.total - r.len + i) % r.cap;
   act[b] = r.action[t];
+  if (ycache) {
+    y[b] = ycache[t];
+    return;
+  }
+  replay_frames(r, i, 1, f);
+  for (int j = 0; j < 4; ++j) tab_sn[b * 4 + j] = f[j];
   rew[b] = r.reward[t];
   done[b] = r.done[t];
+}
+
+// s' frame pointers, reward and done of the logical replay indices [i0, i0 + n)
+__global__ void k_slot_tables(ReplayView r, uint64_t i0, uint32_t n, const uint8_t** tab_sn, float* rew, uint8_t* done) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const uint8_t* f[4];
+  replay_frames(r, i0 + b, 1, f);
+  for (int j = 0; j < 4; ++j) tab_sn[b * 4 + j] = f[j];
+  const uint64_t t = (r.total - r.len + i0 + b) % r.cap;
+  rew[b] = r.reward[t];
+  done[b] = r.done[t];
+}
+
+__global__ void k_slot_put(ReplayView r, uint64_t i0, uint32_t n, const float* y, float* ycache) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < n) ycache[(r.total - r.len + i0 + b) % r.cap] = y[b];
 }
 
 // this rank's contribution to the global solved() test: running reward, has-history flag, episode count, and the
@@ -246,6 +268,16 @@ struct qlx_learner {
   hipStream_t tgt_stream = nullptr;
   hipEvent_t ev_gather = nullptr;
   std::vector<hipEvent_t> ev_tgt;
+  // Bellman-target memo per replay slot (ycache_fill): on when the target net is frozen (target_sync_steps == 0,
+  // the reference) and y does not depend on the online net (no double DQN); QLX_TARGET_CACHE=0 turns it off
+  bool ycache = false;
+  float* d_ycache = nullptr;           // [capacity] y of the transition in each ring slot
+  const uint8_t** d_ytab = nullptr;    // [ychunk * 4]
+  float* d_yrew = nullptr;             // [ychunk]
+  uint8_t* d_ydone = nullptr;          // [ychunk]
+  float* d_ytmp = nullptr;             // [ychunk]
+  uint32_t ychunk = 0;
+  uint64_t ycache_version = 0;         // target->version the memo was computed with
   qlx::Profiler prof;
   // statistics events (write_checkpoint + learning_update_log, self_driving_tf_q_learner.rs:204-212,226-230)
   uint64_t stats_events = 0;
@@ -280,6 +312,34 @@ static void learner_targets_range(qlx_learner* L, uint32_t u0, uint32_t nu, cons
   launch_fc2(2, ta, (int)n, s);
 }
 
+// Target memo.  With the target net frozen, y = r + gamma * max_a Q_target(s') (or r if done) of a transition is a
+// fixed function of the transition, and every kernel of the forward computes each sample's chains independently
+// of the rest of its batch, so y can be computed once, when the transition enters the replay, and
+// read back at every sampling: bit-identical to the per-batch target pass, which at replay ratio 8 evaluates each
+// transition's s' eight times on average.  A write of the target weights from outside (model_pack: dist_init's
+// broadcast, the model API) invalidates the memo and the next push recomputes every live slot.
+static void ycache_fill(qlx_learner* L, uint64_t i0, uint64_t n) {
+  hipStream_t s = L->stream;
+  const ReplayView rv = replay_view(L->rb);
+  qlx_model* tg = L->target;
+  for (uint64_t c0 = 0; c0 < n; c0 += L->ychunk) {
+    const uint32_t m = (uint32_t)std::min<uint64_t>(L->ychunk, n - c0);
+    hipLaunchKernelGGL(k_slot_tables, dim3((m + 255) / 256), dim3(256), 0, s, rv, i0 + c0, m, L->d_ytab, L->d_yrew, L->d_ydone);
+    QLX_HIP(hipGetLastError());
+    model_forward_trunk(tg, L->d_ytab, (int)m, s, false);
+    Fc2Args ta = fc2_args(tg, (int)m);
+    ta.q_select = nullptr;
+    ta.rewards = L->d_yrew;
+    ta.dones = L->d_ydone;
+    ta.gamma = L->p.gamma;
+    ta.y_out = L->d_ytmp;
+    launch_fc2(2, ta, (int)m, s);
+    hipLaunchKernelGGL(k_slot_put, dim3((m + 255) / 256), dim3(256), 0, s, rv, i0 + c0, m, L->d_ytmp, L->d_ycache);
+    QLX_HIP(hipGetLastError());
+  }
+  debug_sync(s, "ycache_fill");
+}
+
 static void learner_targets(qlx_learner* L, uint32_t U) {
   hipStream_t s = L->stream;
   const uint32_t n = U * L->B;
@@ -287,9 +347,10 @@ static void learner_targets(qlx_learner* L, uint32_t U) {
   {
     ProfScope ps(&L->prof, "gather", s);
     hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, s, rv, L->d_idx, n, L->d_tab_s, L->d_tab_sn, L->d_bact,
-                       L->d_brew, L->d_bdone);
+                       L->d_brew, L->d_bdone, L->ycache ? L->d_ycache : nullptr, L->d_targets);
   }
   debug_sync(s, "gather");
+  if (L->ycache) return;
   const float* q_select = nullptr;
   if (L->ddqn) {   // double DQN: a* = argmax Q_online(s') from the online net as it stands before this step's updates
     qlx_model* on = L->online;
@@ -394,6 +455,16 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
     if (L->per) per_launch_push(s, L->prio.leaves(), L->rb->cap, L->rb->total - N, N, L->prio.d_max);
   }
   debug_sync(s, "replay_push");
+  if (L->ycache) {   // y of the N new transitions (all live slots after a write of the target weights)
+    ProfScope ps(&L->prof, "target_memo", s);
+    if (L->target->version != L->ycache_version) {
+      ycache_fill(L, 0, L->rb->len());
+      L->ycache_version = L->target->version;
+    } else {
+      const uint64_t len = L->rb->len(), fresh = std::min<uint64_t>(N, len);
+      ycache_fill(L, len - fresh, fresh);
+    }
+  }
   {
     ProfScope ps(&L->prof, "episode_reset", s);
     launch_episode_book(s, N, L->d_rewards, L->d_dones, L->env->d_ep_steps, L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
@@ -558,11 +629,24 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       hipLaunchKernelGGL(k_obs_table, dim3((N * 4 + 255) / 256), dim3(256), 0, L->stream, L->env->d_obs, N, L->d_obs_table);
       QLX_HIP(hipGetLastError());
       model_workspace(L->online, (int)std::max(N, B));
-      model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
+      const char* tc = std::getenv("QLX_TARGET_CACHE");
+      L->ycache = p->target_sync_steps == 0 && !L->ddqn && !(tc && tc[0] == '0');
+      if (L->ycache) {
+        L->ychunk = std::min<uint32_t>(N, (uint32_t)kF32FwdChunk);
+        QLX_HIP(hipMalloc(&L->d_ycache, p->history_buffer_len * sizeof(float)));
+        QLX_HIP(hipMalloc(&L->d_ytab, (size_t)L->ychunk * 4 * sizeof(void*)));
+        QLX_HIP(hipMalloc(&L->d_yrew, L->ychunk * sizeof(float)));
+        QLX_HIP(hipMalloc(&L->d_ydone, L->ychunk));
+        QLX_HIP(hipMalloc(&L->d_ytmp, L->ychunk * sizeof(float)));
+        L->ycache_version = L->target->version;
+        model_workspace(L->target, (int)L->ychunk);
+      } else {
+        model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
+      }
       if (L->ddqn) model_workspace(L->online, (int)(L->max_updates * B));   // + the online pass over s'
       if (L->per) L->prio.init(p->history_buffer_len, UB);
       const char* tov = std::getenv("QLX_TARGET_OVERLAP");
-      L->tgt_overlap = tov && tov[0] == '1' && p->qnet_precision == QLX_PREC_F32 && !L->ddqn;
+      L->tgt_overlap = tov && tov[0] == '1' && p->qnet_precision == QLX_PREC_F32 && !L->ddqn && !L->ycache;
       if (L->tgt_overlap) {
         QLX_HIP(hipStreamCreateWithFlags(&L->tgt_stream, hipStreamNonBlocking));
         QLX_HIP(hipEventCreateWithFlags(&L->ev_gather, hipEventDisableTiming));
@@ -600,7 +684,8 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
     qlx_model_destroy(L->target);
     void* ptrs[] = {L->d_actions, L->d_rewards, L->d_dones, L->d_reset, (void*)L->d_obs_table, L->d_eps, L->d_ep_reward,
                     L->d_hist, L->d_book, L->d_idx, (void*)L->d_tab_s, (void*)L->d_tab_sn, L->d_bact, L->d_brew,
-                    L->d_bdone, L->d_losses, L->d_targets, L->d_gsum, L->d_gmin};
+                    L->d_bdone, L->d_losses, L->d_targets, L->d_gsum, L->d_gmin, L->d_ycache, (void*)L->d_ytab,
+                    L->d_yrew, L->d_ydone, L->d_ytmp};
     for (void* p : ptrs) (void)hipFree(p);
     L->prio.release();
     (void)hipStreamDestroy(L->stream);

@@ -59,6 +59,7 @@ struct qlx_model {
   // bf16 MFMA operand copies ([n][k], k contiguous)
   __bf16 *wf0 = nullptr, *wf1 = nullptr, *wb1 = nullptr, *wf2 = nullptr, *wb2 = nullptr, *wb3 = nullptr;
   int64_t iterations = 0;
+  uint64_t version = 0;   // bumped by model_pack, i.e. on every write of the weights from outside the optimizer
   float lr = 0.00025f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, clipnorm = 1.0f;
   int n_ranges = 0;
   int64_t *d_rbeg = nullptr, *d_rend = nullptr;

@@ -513,6 +513,7 @@ static PackPtrs pack_ptrs(qlx_model* m) {
 }
 
 void model_pack(qlx_model* m) {
+  m->version += 1;
   if (m->f32) return;   // the fp32 path reads the master weights directly
   hipLaunchKernelGGL(k_pack_all, dim3(2048), dim3(256), 0, m->stream, m->d_params, (int64_t)kNumParams, pack_ptrs(m));
   QLX_HIP(hipGetLastError());

@@ -31,29 +31,35 @@ static int64_t voff(int v) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// dense 512 -> 3 head, one thread per sample: q[n] = (fmaf chain over k ascending of a4[k] W4[k][n]) + b4[n]
+// dense 512 -> 3 head: q[b][n] = (fmaf chain over k ascending of a4[b][k] W4[k][n]) + b4[n], as the MFMA product
+// W4^T a4^T (one wave per 16 samples: A = W4^T rows n < 3, B = a4 columns; each output is the k-ordered chain), the
+// three q of a sample in one lane.
 //   MODE 0: q;  1: q + argmax (predict_action);  2: Bellman target y = r + max_a q * gamma (or q at the online net's
 //   argmax, double DQN), y = r if done;  3: training head (Huber value h, dloss/dq_a g, |e|)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
-  __shared__ float w4s[512 * 3];
-  for (int i = threadIdx.x; i < 512 * 3; i += 256) w4s[i] = A.w4[i];
+  __shared__ float w4s[512 * 4];   // W4 [k][n], n padded to 4 (column 3 = 0)
+  for (int i = threadIdx.x; i < 512 * 4; i += 256) w4s[i] = (i & 3) < 3 ? A.w4[(i >> 2) * 3 + (i & 3)] : 0.0f;
   __syncthreads();
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= A.B) return;
-  const float* x = A.a4f + (size_t)b * 512;
-  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-#pragma unroll 4
-  for (int k = 0; k < 512; k += 4) {
-    const f32x4 v = ld4(x + k);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s0 = (blockIdx.x * 4 + wave) * 16;
+  if (s0 >= A.B) return;   // wave-uniform, no barrier follows
+  const int j = lane & 15, g = lane >> 4, n = lane & 15;
+  const int b = s0 + j;
+  const bool valid = b < A.B;
+  const float* x = A.a4f + (size_t)(valid ? b : s0) * 512 + g;   // B operand: a4[b][4 t + g]
+  f32x4 acc = zero4();
+  // the lane's 128 operands are all in flight at once (a wave's whole chain waits for one memory latency)
+  float xv[128];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s0 = fmaf(v[j], w4s[(k + j) * 3 + 0], s0);
-      s1 = fmaf(v[j], w4s[(k + j) * 3 + 1], s1);
-      s2 = fmaf(v[j], w4s[(k + j) * 3 + 2], s2);
-    }
+  for (int t = 0; t < 128; ++t) xv[t] = valid ? x[4 * t] : 0.0f;
+#pragma unroll
+  for (int t = 0; t < 128; ++t) {
+    const float wv = n < 3 ? w4s[(4 * t + g) * 4 + n] : 0.0f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, xv[t], acc, 0, 0, 0);
   }
-  const float q0 = __fadd_rn(s0, A.b4[0]), q1 = __fadd_rn(s1, A.b4[1]), q2 = __fadd_rn(s2, A.b4[2]);
+  if (g != 0 || !valid) return;   // lane (j, 0) holds rows n = 0 .. 3 of sample j
+  const float q0 = __fadd_rn(acc[0], A.b4[0]), q1 = __fadd_rn(acc[1], A.b4[1]), q2 = __fadd_rn(acc[2], A.b4[2]);
   if (A.q) { A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2; }
   if (MODE == 1) {   // tf.argmax: first maximal index
     int best = 0;
@@ -126,6 +132,13 @@ __global__ __launch_bounds__(256) void k_wreduce32(WRed R) {
   const int nz = R.nz[L];
   float t = 0.0f;
   int z = 0;
+  for (; z + 32 <= nz; z += 32) {   // 32 partial loads in flight, then the in-order sum
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = p[(size_t)(z + j) * stride];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) t = __fadd_rn(t, v[j]);
+  }
   for (; z + 8 <= nz; z += 8) {
     float v[8];
 #pragma unroll
@@ -160,8 +173,16 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   const int64_t b = (int64_t)j * kNormSeg, e = std::min<int64_t>(n, b + kNormSeg);
   const float* g = A.g + A.off[v];
   float t = 0.0f;
-  for (int64_t i = b + threadIdx.x; i < e; i += 256) {
-    const float x = __fmul_rn(g[i], A.scale);
+  float xs[kNormSeg / 256];   // the lane's 32 elements, all loads in flight before the chain
+#pragma unroll
+  for (int k = 0; k < kNormSeg / 256; ++k) {
+    const int64_t i = b + threadIdx.x + 256 * k;
+    xs[k] = i < e ? g[i] : 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < kNormSeg / 256; ++k) {
+    if (b + threadIdx.x + 256 * k >= e) break;
+    const float x = __fmul_rn(xs[k], A.scale);
     t = fmaf(x, x, t);
   }
   for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
@@ -209,15 +230,38 @@ __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
     }
   }
   __syncthreads();
-  const int64_t count = A.off[kNumVars];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
-    int var = 0;
-    while (i >= A.off[var + 1]) ++var;
-    const float denom = fmaxf(nrm[var], A.clipnorm);
-    float m = A.m[i], v = A.v[i];
-    A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
-    A.m[i] = m;
-    A.v[i] = v;
+  // four elements per thread and step (16-byte accesses; every variable but the last starts at a multiple of 4, so a
+  // group never straddles two variables; the last group is finished element by element)
+  const int64_t count = A.off[kNumVars], n4 = count / 4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = q * 4;
+    if (q < n4) {
+      int var = 0;
+      while (i0 >= A.off[var + 1]) ++var;
+      const float denom = fmaxf(nrm[var], A.clipnorm);
+      const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
+      f32x4 m = ld4(A.m + i0), v = ld4(A.v + i0), o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float mk = m[k], vk = v[k];
+        o[k] = adam32_elem(g[k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[k]);
+        m[k] = mk;
+        v[k] = vk;
+      }
+      *reinterpret_cast<f32x4*>(A.w + i0) = o;
+      *reinterpret_cast<f32x4*>(A.m + i0) = m;
+      *reinterpret_cast<f32x4*>(A.v + i0) = v;
+    } else {
+      for (int64_t i = i0; i < count; ++i) {
+        int var = 0;
+        while (i >= A.off[var + 1]) ++var;
+        const float denom = fmaxf(nrm[var], A.clipnorm);
+        float m = A.m[i], v = A.v[i];
+        A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
+        A.m[i] = m;
+        A.v[i] = v;
+      }
+    }
   }
 }
 
@@ -367,7 +411,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
 }
 
 void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s) {
-  const dim3 g((B + 255) / 256), blk(256);
+  const dim3 g((B + 63) / 64), blk(256);   // 16 samples per wave
   switch (mode) {
     case 0: hipLaunchKernelGGL(k_head32<0>, g, blk, 0, s, a); break;
     case 1: hipLaunchKernelGGL(k_head32<1>, g, blk, 0, s, a); break;
@@ -429,7 +473,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     hipEvent_t ea = nullptr, eb = nullptr;
     if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);
-    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(256), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1);
+    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv1_wgrad32");
   }

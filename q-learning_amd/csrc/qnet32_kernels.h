@@ -24,17 +24,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;   // reduction depth staged per LDS slab
 
-// Operand tile in LDS.  RMAJ: t[row][k] (pitch BK + 4: the 16 rows x 4 k of a fragment read hit 64 distinct
-// banks); KMAJ: t[k][row] (pitch = rows padded to 16 mod 64, same property).  Writes are 16-byte float4 along the
-// operand's contiguous source dimension.
-__host__ __device__ constexpr int kmaj_pitch(int rows) { return rows + (((16 - rows % 64) % 64) + 64) % 64; }
+// Operand tile in LDS for MFMA shape MF (16: v_mfma_f32_16x16x4_f32, 32: v_mfma_f32_32x32x2_f32).  RMAJ: t[row][k]
+// (pitch BK + 4); KMAJ: t[k][row] (pitch = rows padded to MF mod 64, so the MF rows x (64 / MF) k of a fragment read
+// hit distinct banks).  Writes are 16-byte float4 along the operand's contiguous source dimension.
+__host__ __device__ constexpr int kmaj_pitch(int rows, int mf) { return rows + (((mf - rows % 64) % 64) + 64) % 64; }
 
-template <int ROWS, bool KMAJ>
+template <int ROWS, bool KMAJ, int MF = 16>
 struct Opnd {
-  static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS) : BK + 4;
+  static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS, MF) : BK + 4;
   static constexpr int FLOATS = KMAJ ? BK * PITCH : ROWS * PITCH;
   static constexpr int F4 = ROWS * BK / 4;   // float4 per slab
-  __device__ static void coord(int idx, int& row, int& k) {
+  static constexpr int KG = 64 / MF;         // k per MFMA (lane groups)
+  __host__ __device__ static void coord(int idx, int& row, int& k) {
     if (KMAJ) { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
     else { row = idx >> 3; k = (idx & 7) * 4; }
   }
@@ -42,9 +43,21 @@ struct Opnd {
     *reinterpret_cast<f32x4*>(t + (KMAJ ? k * PITCH + row : row * PITCH + k)) = v;
   }
   __device__ static float at(const float* t, int row, int k) { return KMAJ ? t[k * PITCH + row] : t[row * PITCH + k]; }
-  // MFMA 16x16x4 operand of the 16 rows from r0, k step kk: lane l holds (r0 + (l & 15), 4 kk + (l >> 4))
-  __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & 15), 4 * kk + (lane >> 4)); }
+  // MFMA operand of the MF rows from r0, k step kk: lane l holds (r0 + l % MF, KG kk + l / MF)
+  __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & (MF - 1)), KG * kk + lane / MF); }
 };
+
+// MFMA shape of a policy: its member MF when it has one, else 16
+template <class P, class = void>
+struct MfOf : std::integral_constant<int, 16> {};
+template <class P>
+struct MfOf<P, std::void_t<decltype(P::MF)>> : std::integral_constant<int, P::MF> {};
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <int MF>
+struct MfAcc { typedef f32x4 type; };
+template <>
+struct MfAcc<32> { typedef f32x16 type; };
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -84,14 +97,16 @@ struct ACtxOf<P, true> { using type = typename P::ACtx; };
 // One output tile of a policy P (see the policies below for the members it provides):
 //   acc[row][col] = sum over the slabs s = 0 .. nslabs(z) - 1 and k = 0 .. 31 of A(z, s, row, k) * B(z, s, col, k),
 // one fmaf chain per output in (s, k) order; then P::epi stores it.  With P::BIAS the tiles of row-tile 0 also
-// sum B's column over the same order (bias gradient = the all-ones row of A).
+// sum B's columns (bias gradient): four chains over the reduction index mod 4, combined ((C0 + C1) + C2) + C3.
 template <class P>
 __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
-  using OA = Opnd<P::BM, P::A_KMAJ>;
-  using OB = Opnd<P::BN, P::B_KMAJ>;
+  constexpr int MF = MfOf<P>::value;
+  using OA = Opnd<P::BM, P::A_KMAJ, MF>;
+  using OB = Opnd<P::BN, P::B_KMAJ, MF>;
+  using Acc = typename MfAcc<MF>::type;
   constexpr int T = P::WM * P::WN * 64;
-  constexpr int TM = P::BM / (P::WM * 16), TN = P::BN / (P::WN * 16);
-  static_assert(TM * P::WM * 16 == P::BM && TN * P::WN * 16 == P::BN, "tile shape");
+  constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
+  static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
   constexpr int NA = (OA::F4 + T - 1) / T, NB = (OB::F4 + T - 1) / T;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -152,30 +167,39 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
       }
     }
   };
-  f32x4 acc[TM][TN];
+  Acc acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
-  float bsum = 0.0f;
-  const bool do_bias = P::BIAS && tm == 0 && tid < P::BN;
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < MF * MF / 64; ++e) acc[i][j][e] = 0.0f;
+  // bias (BIAS policies, row-tile 0): column sums of B as KG interleaved chains - lane group q of the wave's B fragments
+  // chains the k = q mod KG rows - combined in group order at the end
+  float bsum[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bsum[j] = 0.0f;
+  const bool do_bias = P::BIAS && tm == 0 && wm == 0;
   auto compute = [&](int s) {
     const float* a = (s & 1) ? As1 : As0;
     const float* b = (s & 1) ? Bs1 : Bs0;
-    if (P::BIAS && do_bias)
-#pragma unroll 8
-      for (int k = 0; k < BK; ++k) bsum = bsum + OB::at(b, tid, k);
 #pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
+    for (int kk = 0; kk < BK / OA::KG; ++kk) {
       float af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * 16, kk, lane);
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * 16, kk, lane);
+      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
+      if (P::BIAS && do_bias)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bsum[j] = __fadd_rn(bsum[j], bf[j]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (MF == 16) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
     }
   };
   // iteration s: x holds slab s + 1, y is free
@@ -195,19 +219,36 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     iter(s, ra0, rb0, ra1, rb1);
     if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
   }
+  // accumulator layout: MF 16: lane l holds rows 4 (l / 16) .. + 3 of column l % 16; MF 32: element 4 q + e is row
+  // 8 q + 4 (l / 32) + e of column l % 32
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (MF == 16) {
+        p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          p.epi(z, row0 + (wm * TM + i) * 32 + 8 * q + 4 * (lane >> 5), col0 + (wn * TN + j) * 32 + (lane & 31),
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]});
+      }
+    }
   if constexpr (P::BIAS) {
-    if (do_bias) p.epi_bias(z, col0 + tid, bsum);
+    if (do_bias) {
+      static_assert(MF == 16, "bias chains: 16x16x4 fragments");
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float c1 = __shfl(bsum[j], lane + 16), c2 = __shfl(bsum[j], lane + 32), c3 = __shfl(bsum[j], lane + 48);
+        if (lane < 16) p.epi_bias(z, col0 + (wn * TN + j) * 16 + lane, __fadd_rn(__fadd_rn(__fadd_rn(bsum[j], c1), c2), c3));
+      }
+    }
   }
 }
 
 template <class P>
 constexpr size_t gemm_lds_bytes() {
-  return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ>::FLOATS + Opnd<P::BN, P::B_KMAJ>::FLOATS) * sizeof(float);
+  return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ, MfOf<P>::value>::FLOATS + Opnd<P::BN, P::B_KMAJ, MfOf<P>::value>::FLOATS) * sizeof(float);
 }
 
 // grid layout shared by the policies: tile index fastest (col tile, then row tile), then z
@@ -256,9 +297,10 @@ struct NoSide {
 //   weight grads    r = (b, oh, ow) ascending inside a sample chunk; fc1 / fc2 over b ascending, no chunks
 
 // conv2 / conv3 forward on fp32 NHWC input: out = relu(conv + bias); slab s: tap = 32 s / C, c0 = 32 s % C
-template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
+          int MF_ = 16>
 struct PConvFwd {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* in;
@@ -288,9 +330,9 @@ using PConv2FwdS = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>;
 using PConv3FwdS = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
 
 // fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3)
-template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1FwdT {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* a3;
@@ -314,9 +356,9 @@ using PFc1Fwd = PFc1FwdT<>;
 using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
-template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1DgradT {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
   Grid g;
   const float* dz4;
@@ -343,9 +385,9 @@ using PFc1Dgrad = PFc1DgradT<>;
 using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
 
 // fc1 weight gradient: dW3 [3136][512] = a3^T dz4 over b ascending; db3 = column sums of dz4 (row-tile 0 blocks)
-template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1WgradT {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
   Grid g;
   const float* a3;
@@ -374,9 +416,9 @@ using PFc1Wgrad = PFc1WgradT<>;
 using PFc1WgradS = PFc1WgradT<64, 32, 2, 2>;
 
 // conv3 backward-data: dz2 [B][9][9][64] = convT(dz3, W2) * (a2 > 0); rows (b, ih, iw), k = (kh, kw, oc)
-template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PConv3DgradT {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
   Grid g;
   const float* dz3;   // [B][7][7][64]
@@ -412,9 +454,9 @@ using PConv3DgradS = PConv3DgradT<32, 64, 2, 2>;
 // conv2 backward-data by output parity class z = (py, px): rows (b, i, j) with ih = 2 i + py, iw = 2 j + px
 // (10 x 10 per class); taps t = (th, tw): kh = py + 2 th, kw = px + 2 tw, source dz2[b][i - th][j - tw];
 // k = (t, oc): the valid taps of the lexicographic (kh, kw, oc) order
-template <int BM_ = 128, int BN_ = 32, int WM_ = 4, int WN_ = 1>
+template <int BM_ = 128, int BN_ = 32, int WM_ = 4, int WN_ = 1, int MF_ = 16>
 struct PConv2DgradT {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
   Grid g;
   const float* dz2;   // [B][9][9][64]
@@ -453,9 +495,10 @@ using PConv2DgradS = PConv2DgradT<64, 32, 4, 1>;
 
 // conv2 / conv3 weight gradient over sample chunk z (samples [z SC, min(B, (z + 1) SC))): rows m = (kh, kw, c),
 // cols oc, r = (b, oh, ow) ascending; partial slab[z][M + 1][OC] (row M = bias partial)
-template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
+          int MF_ = 16>
 struct PConvWgrad {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
   static constexpr int MROWS = KS * KS * C, P = OH * OW, CHUNK = SC;
   Grid g;
@@ -666,29 +709,26 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
-// x[r][m] dz1[r][oc], m = (kh, kw, c) HWIO, and slab[z][256][oc] = the same chain of dz1 (bias).  Block (z, hh) covers
-// output channels hh * 16 .. + 15; wave w the 16-row tiles 4 w .. 4 w + 3.  Per sample the frames (row layout) and
-// dz1's channel half sit in LDS (54,016 B) while the next sample's are in flight in registers.
+// x[r][m] dz1[r][oc], m = (kh, kw, c) HWIO; bias slab[z][256][oc] = ((C0 + C1) + C2) + C3 with Cq the chain over (b, rs)
+// ascending of dz1[b][4 rs + q][oc] (the four lane groups' chains of the MFMA B operand).  Block (z, hh)
+// covers output channels hh * 16 .. + 15.  Wave w owns kh = 2 w, 2 w + 1: lane row rho = (kh low bit, h, c), tile
+// t = kw - 4 h, so one LDS dword (pixels 4 ow + 4 h .. + 3 of image row 4 oh + kh) feeds the lane's four MFMAs of a
+// step.  Per sample the frames (row layout) and dz1's channel half sit in LDS (54,016 B) while the next sample's are in
+// flight in registers.
 constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
-__global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
-                                                          float* slab) {
+constexpr int kC1WgradThreads = 256;
+__global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
+                                                                       float* slab) {
   extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1776] dwords, then dz [400][16] f32
-  const uint8_t* fb = reinterpret_cast<const uint8_t*>(c1w);
   float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1SlotDw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int z = blockIdx.x % nz, hh = blockIdx.x / nz;
-  const int g = lane >> 4;
+  const int g = lane >> 4, l15 = lane & 15;
   const int b0 = z * QLX_F32_WGRAD_CHUNK_CONV1;
   const int nb = min(QLX_F32_WGRAD_CHUNK_CONV1, B - b0);
-  // this lane's A row m per tile: byte offset of (kh, kw, c) inside the staged frames, relative to pixel (4 oh, 4 ow)
-  int mo[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int m = (wave * 4 + t) * 16 + (lane & 15);
-    const int kh = m >> 5, kw = (m >> 2) & 7, c = m & 3;
-    mo[t] = c * kC1SlotDw * 4 + kh * 84 + kw;
-  }
+  // this lane's A row rho = l15: kh = 2 w + rho / 8, h = (rho / 4) % 2, c = rho % 4; dword of (x = 4 oh + kh, y / 4 = ow + h)
+  const int ao = (l15 & 3) * kC1SlotDw + (2 * wave + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
   uint4 pf[14];
   auto prefetch = [&](int b) {
 #pragma unroll
@@ -716,7 +756,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* 
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = zero4();
-  float bsum = 0.0f;
+  float bsum = 0.0f;   // lane (oc, q): chain Cq of its B-operand values
   prefetch(b0);
   for (int bl = 0; bl < nb; ++bl) {
     __syncthreads();   // the previous sample's LDS reads are done
@@ -726,25 +766,26 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad32(const uint8_t* const* 
 #pragma unroll 4
     for (int rs = 0; rs < 100; ++rs) {
       const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
-      const float bv = dzs[r * 16 + (lane & 15)];
-      const int px = oh * 336 + ow * 4;
+      const float bv = dzs[r * 16 + l15];
+      const uint32_t px = c1w[ao + 84 * oh + ow];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)fb[mo[t] + px], bv, acc[t], 0, 0, 0);
-      if (wave == 0) {   // bias chain in r order: lane groups hold r = 4 rs + 0 .. 3
-        const float v1 = __shfl(bv, lane + 16), v2 = __shfl(bv, lane + 32), v3 = __shfl(bv, lane + 48);
-        bsum = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(bsum, bv), v1), v2), v3);
-      }
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px, t), bv, acc[t], 0, 0, 0);
+      if (wave == 0) bsum = __fadd_rn(bsum, bv);
     }
   }
   float* out = slab + (size_t)z * 257 * 32;
-  const int oc = hh * 16 + (lane & 15);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int m0 = (wave * 4 + t) * 16 + 4 * g;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[(size_t)(m0 + i) * 32 + oc] = acc[t][i];
+  const int oc = hh * 16 + l15;
+  if (wave == 0) {   // ((C0 + C1) + C2) + C3 in row 0
+    const float c1 = __shfl(bsum, lane + 16), c2 = __shfl(bsum, lane + 32), c3 = __shfl(bsum, lane + 48);
+    if (g == 0) out[256 * 32 + oc] = __fadd_rn(__fadd_rn(__fadd_rn(bsum, c1), c2), c3);
   }
-  if (wave == 0 && g == 0) out[256 * 32 + oc] = bsum;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // output row rho = 4 g + i of tile t -> HWIO (kh, kw = 4 h + t, c)
+      const int rho = 4 * g + i, kh = 2 * wave + (rho >> 3), kw = 4 * ((rho >> 2) & 1) + t, c = rho & 3;
+      out[(size_t)((kh * 8 + kw) * 4 + c) * 32 + oc] = acc[t][i];
+    }
 }
 
 #endif  // QLX_Q32_POLICIES_ONLY

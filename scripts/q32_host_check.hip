@@ -26,10 +26,11 @@ static long checks = 0;
 
 template <class P>
 static void replay(const P& p, const char* name) {
-  using OA = Opnd<P::BM, P::A_KMAJ>;
-  using OB = Opnd<P::BN, P::B_KMAJ>;
+  constexpr int MF = MfOf<P>::value;
+  using OA = Opnd<P::BM, P::A_KMAJ, MF>;
+  using OB = Opnd<P::BN, P::B_KMAJ, MF>;
   constexpr int T = P::WM * P::WN * 64;
-  constexpr int TM = P::BM / (P::WM * 16), TN = P::BN / (P::WN * 16);
+  constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
   volatile float sink = 0.0f;
   for (int lb = 0; lb < p.g.blocks(); ++lb) {
     int tm, tn, z;
@@ -58,8 +59,12 @@ static void replay(const P& p, const char* name) {
       const int wm = wave % P::WM, wn = wave / P::WM;
       for (int i = 0; i < TM; ++i)
         for (int j = 0; j < TN; ++j)
-          for (int lane = 0; lane < 64; ++lane)
-            p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), zero4());
+          for (int lane = 0; lane < 64; ++lane) {
+            if (MF == 16) p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), zero4());
+            else
+              for (int q = 0; q < 4; ++q)
+                p.epi(z, row0 + (wm * TM + i) * 32 + 8 * q + 4 * (lane >> 5), col0 + (wn * TN + j) * 32 + (lane & 31), zero4());
+          }
     }
     if constexpr (P::BIAS) {
       if (tm == 0)

@@ -22,6 +22,95 @@ using namespace qlx::q32;
     if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); }   \
   } while (0)
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// experimental core: v_mfma_f32_32x32x2_f32, wave tile TM x TN of 32 x 32 (A pitch PA, B k-major pitch rows + 32 mod 64)
+template <int BM, int BN, int WM, int WN, int PA>
+__global__ __launch_bounds__(256) void k_gen32x32(const float* A, const float* Bm, float* C, int M, int N, int K) {
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32), T = 256;
+  constexpr int PB = BN + (((32 - BN % 64) % 64) + 64) % 64;
+  constexpr int AF = BM * PA, BF = BK * PB;
+  constexpr int NA = BM * BK / 4 / T, NB = BN * BK / 4 / T;
+  extern __shared__ float lds[];
+  float* As[2] = {lds, lds + AF};
+  float* Bs[2] = {lds + 2 * AF, lds + 2 * AF + BF};
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave % WM, wn = wave / WM;
+  const int tiles_n = N / BN, lb = xcd_logical(blockIdx.x, gridDim.x), tm = lb / tiles_n, tn = lb % tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN, ns = K / BK;
+  f32x4 ra[2][NA], rb[2][NB];
+  auto load = [&](int s, f32x4(&a)[NA], f32x4(&b)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) { const int idx = tid + i * T, r = idx >> 3, k = (idx & 7) * 4; a[i] = ld4(A + (size_t)(row0 + r) * K + s * BK + k); }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) { const int idx = tid + i * T, k = idx / (BN / 4), c = (idx % (BN / 4)) * 4; b[i] = ld4(Bm + (size_t)(s * BK + k) * N + col0 + c); }
+  };
+  auto store = [&](int s, const f32x4(&a)[NA], const f32x4(&b)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) { const int idx = tid + i * T, r = idx >> 3, k = (idx & 7) * 4; *reinterpret_cast<f32x4*>(As[s & 1] + r * PA + k) = a[i]; }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) { const int idx = tid + i * T, k = idx / (BN / 4), c = (idx % (BN / 4)) * 4; *reinterpret_cast<f32x4*>(Bs[s & 1] + k * PB + c) = b[i]; }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  auto compute = [&](int s) {
+    const float* a = As[s & 1];
+    const float* b = Bs[s & 1];
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = a[((wm * TM + i) * 32 + (lane & 31)) * PA + 2 * kk + (lane >> 5)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = b[(2 * kk + (lane >> 5)) * PB + (wn * TN + j) * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  load(0, ra[1], rb[1]);
+  store(0, ra[1], rb[1]);
+  if (ns > 1) load(1, ra[0], rb[0]);
+  lds_barrier();
+  for (int s = 0; s < ns; s += 2) {
+    if (s + 2 < ns) load(s + 2, ra[1], rb[1]);
+    compute(s);
+    if (s + 1 < ns) store(s + 1, ra[0], rb[0]);
+    lds_barrier();
+    if (s + 1 >= ns) break;
+    if (s + 3 < ns) load(s + 3, ra[0], rb[0]);
+    compute(s + 1);
+    if (s + 2 < ns) store(s + 2, ra[1], rb[1]);
+    lds_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row0 + (wm * TM + i) * 32 + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3), col = col0 + (wn * TN + j) * 32 + (lane & 31);
+        C[(size_t)row * N + col] = acc[i][j][e];
+      }
+}
+
+template <int BM, int BN, int WM, int WN, int PA>
+static void gen32(int M, int N, int K, const float* A, const float* B, float* C) {
+  constexpr int PB = BN + (((32 - BN % 64) % 64) + 64) % 64;
+  const size_t lds = 2 * (size_t)(BM * PA + BK * PB) * 4;
+  auto kern = k_gen32x32<BM, BN, WM, WN, PA>;
+  CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int G = (M / BM) * (N / BN);
+  const double us = time_us([&] { hipLaunchKernelGGL(kern, dim3(G), dim3(256), lds, 0, A, B, C, M, N, K); });
+  const double f = 2.0 * M * N * K;
+  printf("gen32x32 %dx%dx%d t%dx%d w%dx%d pa%d     blocks %6d lds %6zu  %9.2f us  %7.2f TF  %5.1f %%\n", M, N, K, BM, BN, WM, WN, PA, G,
+         lds, us, f / us / 1e6, f / us / 1e6 / 157.3 * 100);
+}
+
 // C [M][N] = A [M][K] B [K][N], both row-major
 template <int BM_, int BN_, int WM_, int WN_>
 struct PGen {
@@ -180,7 +269,7 @@ int main(int argc, char** argv) {
     {
       const int nz = B / 4, lds = kC1Frames + 400 * 16 * 4;
       CK(hipFuncSetAttribute((const void*)k_conv1_wgrad32, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(256), lds, 0, table, dz1, B, nz, slab); });
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(kC1WgradThreads), lds, 0, table, dz1, B, nz, slab); });
       const double f = 2.0 * B * 400 * 256 * 32;
       printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_wgrad (k_conv1_wgrad32)", 2 * nz, lds, us,
              f / us / 1e6, f / us / 1e6 / 157.3 * 100);
@@ -219,6 +308,29 @@ int main(int argc, char** argv) {
     run1("conv3_dgrad t32x64 w2x2", PConv3DgradT<32, 64, 2, 2>{grid(B * 81, 32, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_dgrad t128x64 w2x2", PConv3DgradT<128, 64, 2, 2>{grid(B * 81, 128, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_wgrad t64x32 w2x2", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 32, 2, 2>{grid(576, 64, 64, 32, B / 16), a2, dz3, slab, B}, flop);
+    printf("--- MF 32 (v_mfma_f32_32x32x2_f32) variants\n");
+    for (int BB : {1024, 8192}) {
+      double f2 = 2.0 * BB * 81 * 64 * 512, f3 = 2.0 * BB * 49 * 64 * 576, f1 = 2.0 * BB * 3136 * 512;
+      printf("B = %d\n", BB);
+      run1("conv2_fwd t64x64 w2x2 mf32", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2, 32>{grid(BB * 81, 64, 64, 64, 1), a1, W1, W1, a2, BB * 81}, f2);
+      run1("conv2_fwd t128x32 w4x1 mf32", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 128, 32, 4, 1, 32>{grid(BB * 81, 128, 64, 32, 1), a1, W1, W1, a2, BB * 81}, f2);
+      run1("conv2_fwd t128x64 w4x1 mf32", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 128, 64, 4, 1, 32>{grid(BB * 81, 128, 64, 64, 1), a1, W1, W1, a2, BB * 81}, f2);
+      run1("conv3_fwd t64x64 w2x2 mf32", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2, 32>{grid(BB * 49, 64, 64, 64, 1), a2, W2, W2, a3, BB * 49}, f3);
+      run1("conv3_fwd t128x32 w4x1 mf32", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 128, 32, 4, 1, 32>{grid(BB * 49, 128, 64, 32, 1), a2, W2, W2, a3, BB * 49}, f3);
+      run1("fc1_fwd t64x64 w2x2 mf32", PFc1FwdT<64, 64, 2, 2, 32>{grid(BB, 64, 512, 64, 1), a3, W3, W3, a4, BB}, f1);
+      run1("fc1_fwd t32x128 w1x4 mf32", PFc1FwdT<32, 128, 1, 4, 32>{grid(BB, 32, 512, 128, 1), a3, W3, W3, a4, BB}, f1);
+      if (BB > 1024) continue;
+      run1("fc1_dgrad t64x64 w2x2 mf32", PFc1DgradT<64, 64, 2, 2, 32>{grid(BB, 64, 3136, 64, 1), dz4, W3, a3, dz3, BB}, f1);
+      run1("fc1_dgrad t128x32 w4x1 mf32", PFc1DgradT<128, 32, 4, 1, 32>{grid(BB, 128, 3136, 32, 1), dz4, W3, a3, dz3, BB}, f1);
+      run1("fc1_wgrad t64x64 w2x2 mf32", PFc1WgradT<64, 64, 2, 2, 32>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, BB}, f1);
+      run1("fc1_wgrad t32x128 w1x4 mf32", PFc1WgradT<32, 128, 1, 4, 32>{grid(3136, 32, 512, 128, 1), a3, dz4, gw, gw, BB}, f1);
+      run1("conv3_dgrad t64x64 w2x2 mf32", PConv3DgradT<64, 64, 2, 2, 32>{grid(BB * 81, 64, 64, 64, 1), dz3, W2, a2, dz2, BB * 81}, f3);
+      run1("conv3_dgrad t128x32 w4x1 mf32", PConv3DgradT<128, 32, 4, 1, 32>{grid(BB * 81, 128, 64, 32, 1), dz3, W2, a2, dz2, BB * 81}, f3);
+      run1("conv3_wgrad t64x64 w2x2 mf32", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 64, 2, 2, 32>{grid(576, 64, 64, 64, BB / 16), a2, dz3, slab, BB}, f3);
+      run1("conv2_dgrad t128x32 w4x1 mf32", PConv2DgradT<128, 32, 4, 1, 32>{grid(BB * 100, 128, 32, 32, 4), dz2, W1, a1, dz1, BB * 100}, f2);
+      run1("conv2_wgrad t64x64 w2x2 mf32", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 64, 2, 2, 32>{grid(512, 64, 64, 64, BB / 16), a1, dz2, slab, BB}, f2);
+      run1("conv2_wgrad t128x64 w2x2 mf32", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16, 128, 64, 2, 2, 32>{grid(512, 128, 64, 64, BB / 16), a1, dz2, slab, BB}, f2);
+    }
 #undef V
   }
   printf("--- generic GEMM (A row-major, B row-major)\n");
@@ -228,6 +340,12 @@ int main(int argc, char** argv) {
     float* B = dbuf((size_t)K * N, 21);
     float* C = dbuf((size_t)M * N, 22);
     gen<64, 64, 2, 2>(M, N, K, A, B, C);
+    gen32<64, 64, 2, 2, 36>(M, N, K, A, B, C);
+    gen32<128, 64, 2, 2, 36>(M, N, K, A, B, C);
+    gen32<128, 128, 2, 2, 36>(M, N, K, A, B, C);
+    gen32<64, 64, 2, 2, 40>(M, N, K, A, B, C);
+    gen32<64, 64, 2, 2, 36>(65536, 64, 512, A, B, C);
+    gen32<128, 64, 2, 2, 36>(65536, 64, 512, A, B, C);
     gen<64, 64, 2, 2>(65536, 64, 512, A, B, C);
     gen<128, 64, 2, 2>(65536, 64, 512, A, B, C);
     gen<64, 32, 4, 1>(65536 * 4, 32, 256, A, B, C);

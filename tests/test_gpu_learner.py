@@ -146,6 +146,38 @@ def test_f32_c3_config():
     assert same(np.float32(loss), g["losses"][0])
 
 
+@pytest.mark.parametrize("prec", [0, 1])
+def test_target_memo_matches_per_batch_target_pass(monkeypatch, prec):
+    """The per-slot Bellman-target memo (default while the target net is frozen, learner.hip ycache_fill) gives the
+    same targets, losses and weights as the per-batch target pass (QLX_TARGET_CACHE=0) - bit for bit, also across
+    the replay FIFO wrap and after the target weights are overwritten mid-run (the memo is rebuilt for every slot)."""
+    qlx = _qlx()
+
+    def run(cache):
+        monkeypatch.setenv("QLX_TARGET_CACHE", "1" if cache else "0")
+        p = qlx.Parameter(n_envs=64, batch_size=32, history_buffer_len=1000, update_after_actions=8,
+                          epsilon_pure_random_steps=400, epsilon_greedy_steps=2000.0, max_steps_per_episode=200,
+                          stats_after_steps=0, qnet_precision=prec)
+        L = qlx.SelfDrivingQLearner(p)
+        out = []
+        for v in range(30):
+            if v == 18:
+                w = L.stabilized_model.get(9)
+                L.stabilized_model.set(9, (w + np.float32(0.01)).astype(np.float32))
+            L.vector_step()
+            g = L.last()
+            out.append((g["targets"].copy(), g["losses"].copy()))
+        return out, [L.model.get(v) for v in range(10)]
+
+    memo, w_memo = run(True)
+    plain, w_plain = run(False)
+    for v, ((ym, lm), (yp, lp)) in enumerate(zip(memo, plain)):
+        assert same(ym, yp), f"targets differ @ vector step {v}"
+        assert same(lm, lp), f"losses differ @ vector step {v}"
+    for a, b in zip(w_memo, w_plain):
+        assert same(a, b)
+
+
 C1_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c1_learner_f32.npz")
 
 
