@@ -17,12 +17,14 @@
 //   conv wgrad      per sample chunk z of SC_l samples: P_z = chain over (b, oh, ow) ascending; dW = ((0 + P_0) + P_1) ..
 //                   bias: P_z = ((C0 + C1) + C2) + C3, Cq = chain over the chunk-local rows r = q mod 4 ascending
 //   dense-512 db3   ((C0 + C1) + C2) + C3, Cq = chain over b = q mod 4 ascending
-//   clip_by_norm    per variable: segments of 8192 elements; 256 lane chains fmaf(g, g, t) over i = lane mod 256;
-//                   4 x 64-lane xor butterflies (32 .. 1); ((w0 + w1) + w2) + w3; segments summed in order
+//   clip_by_norm    per variable: segments of 2048 elements; lane l < 256 chains fmaf(g, g, t) over the segment's
+//                   elements 4 l .. 4 l + 3, 1024 + 4 l .. + 3; 4 x 64-lane xor butterflies (32 .. 1); ((w0 + w1) + w2)
+//                   + w3 -> partial j; 64 lane chains over the partials j = lane mod 64 ascending, one xor butterfly
 //   Adam            legacy ResourceApplyAdam with explicit roundings (qnet_ref.cpp)
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include <omp.h>
 
@@ -32,7 +34,7 @@ namespace orc {
 
 // chunk sizes of the conv weight-gradient partials (include/qlx.h QLX_F32_WGRAD_CHUNK_CONV*; tests check equality)
 constexpr int kSC1 = 4, kSC2 = 16, kSC3 = 16;
-constexpr int kNormSeg = 8192;
+constexpr int kNormSeg = 2048;
 
 static inline float fma32(float a, float b, float c) { return std::fmaf(a, b, c); }
 static inline float relu(float v) { return v > 0.0f ? v : 0.0f; }
@@ -277,31 +279,43 @@ float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* acti
   return loss;
 }
 
+// 64-lane xor butterfly (32 .. 1) of v[0..63]: every lane ends with the same value
+static float butterfly64(const float* in) {
+  float v[64];
+  std::memcpy(v, in, sizeof(v));
+  for (int off = 32; off > 0; off >>= 1) {
+    float nv[64];
+    for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+    std::memcpy(v, nv, sizeof(v));
+  }
+  return v[0];
+}
+
 // per-variable sums of squares in the build's order (header)
 static float sumsq32(const float* g, int64_t n) {
-  float total = 0.0f;
+  std::vector<float> part;
   for (int64_t b = 0; b < n; b += kNormSeg) {
-    const int64_t e = std::min<int64_t>(n, b + kNormSeg);
     float t[256];
     for (int l = 0; l < 256; ++l) {
       float s = 0.0f;
-      for (int64_t i = b + l; i < e; i += 256) s = fma32(g[i], g[i], s);
+      for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < 4; ++k) {
+          const int64_t i = b + 1024 * h + 4 * l + k;
+          if (i < n) s = fma32(g[i], g[i], s);
+        }
       t[l] = s;
     }
     float w[4];
-    for (int wv = 0; wv < 4; ++wv) {
-      float v[64];
-      for (int l = 0; l < 64; ++l) v[l] = t[wv * 64 + l];
-      for (int off = 32; off > 0; off >>= 1) {
-        float nv[64];
-        for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
-        std::memcpy(v, nv, sizeof(v));
-      }
-      w[wv] = v[0];
-    }
-    total = total + (((w[0] + w[1]) + w[2]) + w[3]);
+    for (int wv = 0; wv < 4; ++wv) w[wv] = butterfly64(t + 64 * wv);
+    part.push_back(((w[0] + w[1]) + w[2]) + w[3]);
   }
-  return total;
+  float c[64];
+  for (int l = 0; l < 64; ++l) {
+    float s = 0.0f;
+    for (size_t j = l; j < part.size(); j += 64) s = s + part[j];
+    c[l] = s;
+  }
+  return butterfly64(c);
 }
 
 void qnet32_apply_adam(QNet& q, const Grads& g, float* norms_out) {

@@ -153,10 +153,11 @@ __global__ __launch_bounds__(256) void k_wreduce32(WRed R) {
   R.gw[L][(size_t)m * oc + n] = t;
 }
 
-// clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg;
-// lane chain t = fmaf(x, x, t) over i = tid, tid + 256, ...; wave xor butterfly (32, 16, .., 1); then
-// ((w0 + w1) + w2) + w3.  Norm_v = sum over its segments in order (k_adam32).
-constexpr int kNormSeg = 8192;
+// clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg = 2048;
+// thread t chains t = fmaf(x, x, t) over its elements j S + 4 t .. + 3, then j S + 1024 + 4 t .. + 3 (x = g * scale);
+// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  Norm_v from its partials in k_adam32.
+constexpr int kNormSeg = 2048;
+constexpr int kNormSegMax = 1024;   // partials per variable the Adam prologue reduces (16 per lane)
 struct NormArgs {
   const float* g;
   float scale;
@@ -170,21 +171,27 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   while (v < kNumVars - 1 && (int)blockIdx.x >= A.seg_first[v + 1]) ++v;
   const int j = blockIdx.x - A.seg_first[v];
   const int64_t n = A.off[v + 1] - A.off[v];
-  const int64_t b = (int64_t)j * kNormSeg, e = std::min<int64_t>(n, b + kNormSeg);
-  const float* g = A.g + A.off[v];
+  const int64_t b = (int64_t)j * kNormSeg;
+  const float* g = A.g + A.off[v];   // variable offsets are multiples of 4 floats (16-byte loads)
+  f32x4 x[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t i = b + 1024 * h + 4 * threadIdx.x;
+    if (i + 4 <= n) {
+      x[h] = ld4(g + i);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[h][k] = i + k < n ? g[i + k] : 0.0f;   // zeros leave the chain unchanged
+    }
+  }
   float t = 0.0f;
-  float xs[kNormSeg / 256];   // the lane's 32 elements, all loads in flight before the chain
 #pragma unroll
-  for (int k = 0; k < kNormSeg / 256; ++k) {
-    const int64_t i = b + threadIdx.x + 256 * k;
-    xs[k] = i < e ? g[i] : 0.0f;
-  }
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-  for (int k = 0; k < kNormSeg / 256; ++k) {
-    if (b + threadIdx.x + 256 * k >= e) break;
-    const float x = __fmul_rn(xs[k], A.scale);
-    t = fmaf(x, x, t);
-  }
+    for (int k = 0; k < 4; ++k) {
+      const float y = __fmul_rn(x[h][k], A.scale);
+      t = fmaf(y, y, t);
+    }
   for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
   __syncthreads();
@@ -215,15 +222,16 @@ __device__ __forceinline__ float adam32_elem(float g, float scale, float clipnor
 __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
   __shared__ float nrm[kNumVars];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // norm_v: lane chain over the partials lane, lane + 64, ... of v (zeros past the end), then the xor butterfly
   for (int v = wave; v < kNumVars; v += 4) {
     const int first = A.seg_first[v], cnt = A.seg_first[v + 1] - first;
+    float x[kNormSegMax / 64];
+#pragma unroll
+    for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < cnt ? A.partial[first + lane + 64 * i] : 0.0f;
     float t = 0.0f;
-    for (int c = 0; c < cnt; c += 64) {
-      const float x = c + lane < cnt ? A.partial[first + c + lane] : 0.0f;
-      const int m = cnt - c < 64 ? cnt - c : 64;
-      for (int j = 0; j < m; ++j)
-        t = __fadd_rn(t, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), j)));
-    }
+#pragma unroll
+    for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
+    for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
     if (lane == 0) {
       nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
       if (blockIdx.x == 0) A.norms[v] = nrm[v];
@@ -275,6 +283,7 @@ using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3>;
 using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
+static_assert((1605632 + kNormSeg - 1) / kNormSeg <= kNormSegMax, "norm partials per variable");
 
 void f32_workspace(qlx_model* m, int B) {
   if (B <= m->ws_batch) return;
@@ -456,15 +465,15 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   const float* p = m->d_params;
   float* G = m->d_grads;
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
-  // algorithmic FLOPs (backward-data + weight gradient of the layer; the padded taps the dgrad tiles multiply are
-  // not counted)
-  {  // conv3: dz2 tiles + weight-gradient chunk tiles
-    PConv3DgradS Pd{grid(B * 81, 32, 64, 64, 1), w.fdz3, p + voff(4), w.fa2, w.fdz2, B * 81};
+  // algorithmic FLOPs (backward-data + weight gradient of the layer; the pixel-major dgrad tiles multiply only the
+  // valid taps, so MFMA work = algorithmic work)
+  {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
+    PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
-  {  // conv2: dz1 tiles (4 parity classes) + weight-gradient chunk tiles
-    PConv2DgradS Pd{grid(B * 100, 64, 32, 32, 4), w.fdz2, p + voff(2), w.fa1, w.fdz1, B * 100};
+  {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
+    PConv2DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }

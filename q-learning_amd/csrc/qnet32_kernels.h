@@ -246,6 +246,14 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   }
 }
 
+// a policy with RAW_ORDER = true takes its blocks in hardware order (no XCD grouping)
+template <class P, class = void>
+struct RawOrder : std::false_type {};
+template <class P>
+struct RawOrder<P, std::void_t<decltype(P::RAW_ORDER)>> : std::integral_constant<bool, P::RAW_ORDER> {};
+template <class P>
+__device__ __forceinline__ int block_order(int h, int G) { return RawOrder<P>::value ? h : xcd_logical(h, G); }
+
 template <class P>
 constexpr size_t gemm_lds_bytes() {
   return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ, MfOf<P>::value>::FLOATS + Opnd<P::BN, P::B_KMAJ, MfOf<P>::value>::FLOATS) * sizeof(float);
@@ -266,7 +274,7 @@ struct Grid {
 template <class P>
 __global__ __launch_bounds__(256) void k_gemm32(const P p) {
   extern __shared__ float lds[];
-  gemm_body(p, xcd_logical(blockIdx.x, gridDim.x), lds);
+  gemm_body(p, block_order<P>(blockIdx.x, gridDim.x), lds);
 }
 
 // two independent GEMMs in one grid (hardware blocks [S::BLOCKS, S::BLOCKS + G1) run P1), plus `side` leading blocks
@@ -280,8 +288,8 @@ __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, c
   // tiles - dispatched first); inside each problem the XCD-grouped tile order
   const int G = gridDim.x - S::BLOCKS, h = b - S::BLOCKS;
   const int g1 = p1.g.blocks();
-  if (h < g1) gemm_body(p1, xcd_logical(h, g1), lds);
-  else gemm_body(p2, xcd_logical(h - g1, G - g1), lds);
+  if (h < g1) gemm_body(p1, block_order<P1>(h, g1), lds);
+  else gemm_body(p2, block_order<P2>(h - g1, G - g1), lds);
 }
 
 struct NoSide {
@@ -450,6 +458,155 @@ struct PConv3DgradT {
 };
 using PConv3Dgrad = PConv3DgradT<>;
 using PConv3DgradS = PConv3DgradT<32, 64, 2, 2>;
+
+// Pixel-major backward data.  A block owns one input pixel (all samples of a row tile): its valid taps are uniform, so
+// the k loop runs over those taps only - the same chain (valid (kh, kw, oc) lexicographic) as the row-major policies
+// without their zero taps.  Pixels are numbered heavy first (most valid taps: long tiles start first) and the blocks
+// keep the hardware order (RAW_ORDER: every XCD gets its share of the heavy pixels).
+// 1-D heavy-first order of the 9 input rows of conv3 dgrad (valid kh: 3 for ih 2..6, 2 for 1 and 7, 1 for 0 and 8)
+__host__ __device__ inline int px3_order(int z) { return z < 5 ? z + 2 : (z == 5 ? 1 : (z == 6 ? 7 : (z == 7 ? 0 : 8))); }
+// ... and of the 10 class rows of conv2 dgrad (valid th: 2 for i 1..8, 1 for 0 and 9)
+__host__ __device__ inline int px2_order(int z) { return z < 8 ? z + 1 : (z == 8 ? 0 : 9); }
+
+// conv3 backward-data, pixel-major: z = pixel (ih, iw) of the 9 x 9 grid; rows b; k = valid (kh, kw) x oc
+template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PConv3DgradPx {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false, RAW_ORDER = true;
+  Grid g;             // {ceil(B / BM), 64 / BN, 81}
+  const float* dz3;   // [B][7][7][64]
+  const float* w2;    // [3][3][64][64]
+  const float* a2;
+  float* dz2;
+  int B;
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  struct Px {
+    int ih, iw, kh0, kw0, nkw, ntap;
+  };
+  __host__ __device__ static Px px(int z) {
+    Px q;
+    q.ih = px3_order(z / 9);
+    q.iw = px3_order(z % 9);
+    q.kh0 = q.ih > 6 ? q.ih - 6 : 0;
+    q.kw0 = q.iw > 6 ? q.iw - 6 : 0;
+    const int kh1 = q.ih < 2 ? q.ih : 2, kw1 = q.iw < 2 ? q.iw : 2;
+    q.nkw = kw1 - q.kw0 + 1;
+    q.ntap = (kh1 - q.kh0 + 1) * q.nkw;
+    return q;
+  }
+  __host__ __device__ int nslabs(int z) const { return 2 * px(z).ntap; }
+  __device__ f32x4 ldA(int z, int s, int row, int k) const {
+    if (row >= B) return zero4();
+    const Px q = px(z);
+    const int t = s >> 1, kh = q.kh0 + t / q.nkw, kw = q.kw0 + t % q.nkw;
+    return ld4(dz3 + ((size_t)(row * 7 + q.ih - kh) * 7 + q.iw - kw) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ f32x4 ldB(int z, int s, int col, int k) const {   // W2[kh][kw][c = col][oc]
+    const Px q = px(z);
+    const int t = s >> 1, kh = q.kh0 + t / q.nkw, kw = q.kw0 + t % q.nkw;
+    return ld4(w2 + ((size_t)(kh * 3 + kw) * 64 + col) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ void epi(int z, int row, int col, f32x4 v) const {
+    const Px q = px(z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < B) {
+        const size_t o = ((size_t)((row + r) * 9 + q.ih) * 9 + q.iw) * 64 + col;
+        dz2[o] = a2[o] > 0.0f ? v[r] : 0.0f;
+      }
+  }
+};
+
+// conv2 backward-data, pixel-major over the class grid: z = (i, j) of 10 x 10; rows b; cols (py, px, c) = 128 (the four
+// output parity classes share the A operand: dz2[b][i - th][j - tw]); k = valid (th, tw) x oc, which is the valid
+// (kh = py + 2 th, kw = px + 2 tw, oc) lexicographic order of every class
+template <int BM_ = 32, int BN_ = 128, int WM_ = 2, int WN_ = 2>
+struct PConv2DgradPx {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false, RAW_ORDER = true;
+  Grid g;             // {ceil(B / BM), 128 / BN, 100}
+  const float* dz2;   // [B][9][9][64]
+  const float* w1;    // [4][4][32][64]
+  const float* a1;
+  float* dz1;         // [B][20][20][32]
+  int B;
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  struct Px {
+    int i, j, th0, tw0, ntw, ntap;
+  };
+  __host__ __device__ static Px px(int z) {
+    Px q;
+    q.i = px2_order(z / 10);
+    q.j = px2_order(z % 10);
+    q.th0 = q.i == 9 ? 1 : 0;
+    q.tw0 = q.j == 9 ? 1 : 0;
+    const int th1 = q.i == 0 ? 0 : 1, tw1 = q.j == 0 ? 0 : 1;
+    q.ntw = tw1 - q.tw0 + 1;
+    q.ntap = (th1 - q.th0 + 1) * q.ntw;
+    return q;
+  }
+  __host__ __device__ int nslabs(int z) const { return 2 * px(z).ntap; }
+  __device__ f32x4 ldA(int z, int s, int row, int k) const {
+    if (row >= B) return zero4();
+    const Px q = px(z);
+    const int t = s >> 1, th = q.th0 + t / q.ntw, tw = q.tw0 + t % q.ntw;
+    return ld4(dz2 + ((size_t)(row * 9 + q.i - th) * 9 + q.j - tw) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ f32x4 ldB(int z, int s, int col, int k) const {   // W1[kh][kw][c][oc], col = (py, px, c)
+    const Px q = px(z);
+    const int t = s >> 1, th = q.th0 + t / q.ntw, tw = q.tw0 + t % q.ntw;
+    const int cls = col >> 5, kh = (cls >> 1) + 2 * th, kw = (cls & 1) + 2 * tw;
+    return ld4(w1 + ((size_t)(kh * 4 + kw) * 32 + (col & 31)) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ void epi(int z, int row, int col, f32x4 v) const {
+    const Px q = px(z);
+    const int cls = col >> 5, ih = 2 * q.i + (cls >> 1), iw = 2 * q.j + (cls & 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < B) {
+        const size_t o = ((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31);
+        dz1[o] = a1[o] > 0.0f ? v[r] : 0.0f;
+      }
+  }
+};
+
+// conv2 backward-data, all four parity classes in one GEMM: rows (b, i, j) of the 10 x 10 class grid, cols (py, px, c),
+// k = (th, tw, oc) with zero taps (the row-major form of PConv2DgradPx)
+template <int BM_ = 64, int BN_ = 128, int WM_ = 2, int WN_ = 2>
+struct PConv2DgradAll {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false;
+  Grid g;             // {ceil(100 B / BM), 128 / BN, 1}
+  const float* dz2;
+  const float* w1;
+  const float* a1;
+  float* dz1;
+  int M;              // B * 100
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return 8; }
+  __device__ f32x4 ldA(int, int s, int row, int k) const {
+    if (row >= M) return zero4();
+    const int t = s >> 1, th = t >> 1, tw = t & 1;
+    const int b = row / 100, p = row - b * 100, i = p / 10, j = p - i * 10;
+    const int oh = i - th, ow = j - tw;
+    if (oh < 0 || oh >= 9 || ow < 0 || ow >= 9) return zero4();
+    return ld4(dz2 + ((size_t)(b * 9 + oh) * 9 + ow) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const {
+    const int t = s >> 1, cls = col >> 5, kh = (cls >> 1) + 2 * (t >> 1), kw = (cls & 1) + 2 * (t & 1);
+    return ld4(w1 + ((size_t)(kh * 4 + kw) * 32 + (col & 31)) * 64 + (s & 1) * 32 + k);
+  }
+  __device__ void epi(int, int row, int col, f32x4 v) const {
+    const int cls = col >> 5;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) {
+        const int rr = row + r, b = rr / 100, p = rr - b * 100, i = p / 10, j = p - i * 10;
+        const size_t o = ((size_t)(b * 20 + 2 * i + (cls >> 1)) * 20 + 2 * j + (cls & 1)) * 32 + (col & 31);
+        dz1[o] = a1[o] > 0.0f ? v[r] : 0.0f;
+      }
+  }
+};
 
 // conv2 backward-data by output parity class z = (py, px): rows (b, i, j) with ih = 2 i + py, iw = 2 j + px
 // (10 x 10 per class); taps t = (th, tw): kh = py + 2 th, kw = px + 2 tw, source dz2[b][i - th][j - tw];

@@ -115,9 +115,11 @@ int main(int argc, char** argv) {
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   replay(PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad");
   replay(PConv3DgradS{grid(B * 81, 32, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad S");
+  replay(PConv3DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 1, 81}, dz3, w2, a2, dz2, B}, "conv3_dgrad px");
   replay(PConv3Wgrad{grid(576, 64, 64, 64, z3), a2, dz3, s3, B}, "conv3_wgrad");
   replay(PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad");
   replay(PConv2DgradS{grid(B * 100, 64, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad S");
+  replay(PConv2DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
   printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
   return 0;

@@ -308,6 +308,25 @@ int main(int argc, char** argv) {
     run1("conv3_dgrad t32x64 w2x2", PConv3DgradT<32, 64, 2, 2>{grid(B * 81, 32, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_dgrad t128x64 w2x2", PConv3DgradT<128, 64, 2, 2>{grid(B * 81, 128, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_wgrad t64x32 w2x2", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 32, 2, 2>{grid(576, 64, 64, 32, B / 16), a2, dz3, slab, B}, flop);
+    printf("--- pixel-major backward data\n");
+    for (int BB : {1024, 8192}) {
+      if (BB > Bmax) break;
+      const double f3 = 2.0 * BB * 49 * 64 * 576, f2 = 2.0 * BB * 81 * 64 * 512;
+      printf("B = %d\n", BB);
+      run1("conv3_dgrad px t32x64 w2x2", PConv3DgradPx<32, 64, 2, 2>{grid(BB, 32, 64, 64, 81), dz3, W2, a2, dz2, BB}, f3);
+      run1("conv3_dgrad px t64x64 w2x2", PConv3DgradPx<64, 64, 2, 2>{grid(BB, 64, 64, 64, 81), dz3, W2, a2, dz2, BB}, f3);
+      run1("conv3_dgrad px t64x32 w2x2", PConv3DgradPx<64, 32, 2, 2>{grid(BB, 64, 64, 32, 81), dz3, W2, a2, dz2, BB}, f3);
+      run1("conv3_dgrad px t128x64 w2x2", PConv3DgradPx<128, 64, 2, 2>{grid(BB, 128, 64, 64, 81), dz3, W2, a2, dz2, BB}, f3);
+      run1("conv2_dgrad px t32x128 w2x2", PConv2DgradPx<32, 128, 2, 2>{grid(BB, 32, 128, 128, 100), dz2, W1, a1, dz1, BB}, f2);
+      run1("conv2_dgrad px t64x64 w2x2", PConv2DgradPx<64, 64, 2, 2>{grid(BB, 64, 128, 64, 100), dz2, W1, a1, dz1, BB}, f2);
+      run1("conv2_dgrad px t32x64 w2x2", PConv2DgradPx<32, 64, 2, 2>{grid(BB, 32, 128, 64, 100), dz2, W1, a1, dz1, BB}, f2);
+      run1("conv2_dgrad px t64x128 w2x2", PConv2DgradPx<64, 128, 2, 2>{grid(BB, 64, 128, 128, 100), dz2, W1, a1, dz1, BB}, f2);
+      run1("conv2_dgrad all t64x128 w2x2", PConv2DgradAll<64, 128, 2, 2>{grid(BB * 100, 64, 128, 128, 1), dz2, W1, a1, dz1, BB * 100}, f2);
+      run1("conv2_dgrad all t64x64 w2x2", PConv2DgradAll<64, 64, 2, 2>{grid(BB * 100, 64, 128, 64, 1), dz2, W1, a1, dz1, BB * 100}, f2);
+      run1("conv2_dgrad all t128x64 w2x2", PConv2DgradAll<128, 64, 2, 2>{grid(BB * 100, 128, 128, 64, 1), dz2, W1, a1, dz1, BB * 100}, f2);
+      run1("conv2_dgrad (shipped S)", PConv2DgradS{grid(BB * 100, 64, 32, 32, 4), dz2, W1, a1, dz1, BB * 100}, f2);
+      run1("conv3_dgrad (shipped S)", PConv3DgradS{grid(BB * 81, 32, 64, 64, 1), dz3, W2, a2, dz2, BB * 81}, f3);
+    }
     printf("--- MF 32 (v_mfma_f32_32x32x2_f32) variants\n");
     for (int BB : {1024, 8192}) {
       double f2 = 2.0 * BB * 81 * 64 * 512, f3 = 2.0 * BB * 49 * 64 * 576, f1 = 2.0 * BB * 3136 * 512;
@@ -322,14 +341,9 @@ int main(int argc, char** argv) {
       if (BB > 1024) continue;
       run1("fc1_dgrad t64x64 w2x2 mf32", PFc1DgradT<64, 64, 2, 2, 32>{grid(BB, 64, 3136, 64, 1), dz4, W3, a3, dz3, BB}, f1);
       run1("fc1_dgrad t128x32 w4x1 mf32", PFc1DgradT<128, 32, 4, 1, 32>{grid(BB, 128, 3136, 32, 1), dz4, W3, a3, dz3, BB}, f1);
-      run1("fc1_wgrad t64x64 w2x2 mf32", PFc1WgradT<64, 64, 2, 2, 32>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, BB}, f1);
-      run1("fc1_wgrad t32x128 w1x4 mf32", PFc1WgradT<32, 128, 1, 4, 32>{grid(3136, 32, 512, 128, 1), a3, dz4, gw, gw, BB}, f1);
       run1("conv3_dgrad t64x64 w2x2 mf32", PConv3DgradT<64, 64, 2, 2, 32>{grid(BB * 81, 64, 64, 64, 1), dz3, W2, a2, dz2, BB * 81}, f3);
       run1("conv3_dgrad t128x32 w4x1 mf32", PConv3DgradT<128, 32, 4, 1, 32>{grid(BB * 81, 128, 64, 32, 1), dz3, W2, a2, dz2, BB * 81}, f3);
-      run1("conv3_wgrad t64x64 w2x2 mf32", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 64, 2, 2, 32>{grid(576, 64, 64, 64, BB / 16), a2, dz3, slab, BB}, f3);
       run1("conv2_dgrad t128x32 w4x1 mf32", PConv2DgradT<128, 32, 4, 1, 32>{grid(BB * 100, 128, 32, 32, 4), dz2, W1, a1, dz1, BB * 100}, f2);
-      run1("conv2_wgrad t64x64 w2x2 mf32", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 64, 2, 2, 32>{grid(512, 64, 64, 64, BB / 16), a1, dz2, slab, BB}, f2);
-      run1("conv2_wgrad t128x64 w2x2 mf32", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16, 128, 64, 2, 2, 32>{grid(512, 128, 64, 64, BB / 16), a1, dz2, slab, BB}, f2);
     }
 #undef V
   }
