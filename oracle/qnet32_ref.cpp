@@ -7,7 +7,8 @@
 // this build's definition of the arithmetic, stated here once and followed by the GPU kernels
 // (q-learning_amd/csrc/qnet32_kernels.h).  tests/test_oracle_qnet.py pins this restatement against float64 torch.
 //   conv1 .. conv3  z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
-//   dense           z = sum over k ascending (Flatten order h, w, c)
+//   dense 3136->512 z = sum over k ascending (Flatten order h, w, c)
+//   dense 512->3    z = ((C0 + C1) + C2) + C3, Cw = chain over k in [128 w, 128 w + 128) ascending
 //   every sum: acc = 0; acc = fmaf(x, w, acc) in that order; then + bias, ReLU (v > 0 ? v : 0)
 //   Huber head      e = q_a - y, h = w (|e| <= 1 ? (0.5 e) e : |e| - 0.5), g = (w clip(e, -1, 1)) / B,
 //                   loss = (sum over b ascending of h) / B
@@ -103,6 +104,21 @@ static void dense_fwd(const float* x, int B, int K, int N, const float* W, const
   }
 }
 
+// dense 512 -> 3 head: q[b][n] = (((C0 + C1) + C2) + C3) + b4[n], Cw = fmaf chain over k in [128 w, 128 w + 128)
+static void head_fwd(const float* x, int B, const float* W, const float* bias, float* y) {
+#pragma omp parallel for schedule(static)
+  for (int b = 0; b < B; ++b)
+    for (int n = 0; n < kActions; ++n) {
+      float c[4];
+      for (int w = 0; w < 4; ++w) {
+        float acc = 0.0f;
+        for (int k = 128 * w; k < 128 * w + 128; ++k) acc = fma32(x[(size_t)b * 512 + k], W[(size_t)k * kActions + n], acc);
+        c[w] = acc;
+      }
+      y[(size_t)b * kActions + n] = ((((c[0] + c[1]) + c[2]) + c[3]) + bias[n]);
+    }
+}
+
 void qnet32_forward(const QNet& q, const uint8_t* x8, int B, Acts& a) {
   a.a1.assign((size_t)B * 20 * 20 * 32, 0.0f);
   a.a2.assign((size_t)B * 9 * 9 * 64, 0.0f);
@@ -113,7 +129,7 @@ void qnet32_forward(const QNet& q, const uint8_t* x8, int B, Acts& a) {
   conv_fwd(kC2, a.a1.data(), B, q.w[2].data(), q.w[3].data(), a.a2.data());
   conv_fwd(kC3, a.a2.data(), B, q.w[4].data(), q.w[5].data(), a.a3.data());
   dense_fwd(a.a3.data(), B, 3136, 512, q.w[6].data(), q.w[7].data(), true, a.a4.data());
-  dense_fwd(a.a4.data(), B, 512, kActions, q.w[8].data(), q.w[9].data(), false, a.q.data());
+  head_fwd(a.a4.data(), B, q.w[8].data(), q.w[9].data(), a.q.data());
 }
 
 // conv weight gradient of one layer, chunked: dW [K*K*C][OC] and db [OC] from input `in` (fp32 NHWC, or the u8

@@ -111,6 +111,7 @@ struct Fc2Args {
   float* hsample;          // training head: per-sample Huber value
   const float* weights;    // training head (optional): per-sample loss weights (prioritized-replay IS weights)
   float* td_abs;           // training head (optional): |q_a - y| out
+  float* dz4_out;          // fp32 training head (optional): the dense-3 backward dz4 [B][512], fused
 };
 // fc2 kernel arguments for the model's last forward; consumes pending fc1 partials (the fc2 launch that
 // follows materialises a4)

@@ -35,80 +35,92 @@ static int64_t voff(int v) {
 // W4^T a4^T (one wave per 16 samples: A = W4^T rows n < 3, B = a4 columns; each output is the k-ordered chain), the
 // three q of a sample in one lane.
 //   MODE 0: q;  1: q + argmax (predict_action);  2: Bellman target y = r + max_a q * gamma (or q at the online net's
-//   argmax, double DQN), y = r if done;  3: training head (Huber value h, dloss/dq_a g, |e|)
+//   argmax, double DQN), y = r if done;  3: training head (Huber value h, dloss/dq_a g, |e|) and, with dz4_out, the
+//   dense-3 backward dz4[b][k] = (a4 > 0) ? W4[k][a_b] * g_b : 0 (dq is g_b at a_b and 0 elsewhere, so the fmaf chain
+//   over n of W4[k][n] dq[b][n] is the single rounded product)
+// Block = 16 samples; wave w chains the k quarter [128 w, 128 w + 128) on v_mfma_f32_16x16x4_f32 (A = W4^T rows n < 3,
+// B = a4 columns), q = (((C0 + C1) + C2) + C3) + b4: four 32-step chains side by side instead of one 128-step chain.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
-  __shared__ float w4s[512 * 4];   // W4 [k][n], n padded to 4 (column 3 = 0)
-  for (int i = threadIdx.x; i < 512 * 4; i += 256) w4s[i] = (i & 3) < 3 ? A.w4[(i >> 2) * 3 + (i & 3)] : 0.0f;
-  __syncthreads();
+  __shared__ f32x4 part[4][16];
+  __shared__ float gsh[16];
+  __shared__ int ash[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int s0 = (blockIdx.x * 4 + wave) * 16;
-  if (s0 >= A.B) return;   // wave-uniform, no barrier follows
+  const int s0 = blockIdx.x * 16;
   const int j = lane & 15, g = lane >> 4, n = lane & 15;
   const int b = s0 + j;
   const bool valid = b < A.B;
-  const float* x = A.a4f + (size_t)(valid ? b : s0) * 512 + g;   // B operand: a4[b][4 t + g]
+  const float* x = A.a4f + (size_t)(valid ? b : s0) * 512 + 128 * wave + g;   // a4[b][128 w + 4 t + g]
+  const float* wp = A.w4 + (128 * wave + g) * 3 + (n < 3 ? n : 0);             // W4[128 w + 4 t + g][n]
+  float wv[32], xv[32];
+#pragma unroll
+  for (int t = 0; t < 32; ++t) wv[t] = wp[t * 12];
+#pragma unroll
+  for (int t = 0; t < 32; ++t) xv[t] = x[4 * t];
   f32x4 acc = zero4();
-  // the lane's 128 operands are all in flight at once (a wave's whole chain waits for one memory latency)
-  float xv[128];
 #pragma unroll
-  for (int t = 0; t < 128; ++t) xv[t] = valid ? x[4 * t] : 0.0f;
+  for (int t = 0; t < 32; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(n < 3 ? wv[t] : 0.0f, xv[t], acc, 0, 0, 0);
+  if (g == 0) part[wave][j] = acc;   // lane (j, 0): rows n = 0 .. 3 of sample j
+  __syncthreads();
+  if (wave == 0 && g == 0 && valid) {
+    const f32x4 c0 = part[0][j], c1 = part[1][j], c2 = part[2][j], c3 = part[3][j];
+    float qv[3];
 #pragma unroll
-  for (int t = 0; t < 128; ++t) {
-    const float wv = n < 3 ? w4s[(4 * t + g) * 4 + n] : 0.0f;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, xv[t], acc, 0, 0, 0);
-  }
-  if (g != 0 || !valid) return;   // lane (j, 0) holds rows n = 0 .. 3 of sample j
-  const float q0 = __fadd_rn(acc[0], A.b4[0]), q1 = __fadd_rn(acc[1], A.b4[1]), q2 = __fadd_rn(acc[2], A.b4[2]);
-  if (A.q) { A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2; }
-  if (MODE == 1) {   // tf.argmax: first maximal index
-    int best = 0;
-    float bv = q0;
-    if (q1 > bv) { best = 1; bv = q1; }
-    if (q2 > bv) best = 2;
-    A.argmax[b] = (uint8_t)best;
-  } else if (MODE == 2) {
-    float mx;
-    if (A.q_select) {
-      const float* qs = A.q_select + b * 3;
+    for (int r = 0; r < 3; ++r) qv[r] = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(c0[r], c1[r]), c2[r]), c3[r]), A.b4[r]);
+    const float q0 = qv[0], q1 = qv[1], q2 = qv[2];
+    if (A.q) { A.q[b * 3 + 0] = q0; A.q[b * 3 + 1] = q1; A.q[b * 3 + 2] = q2; }
+    if (MODE == 1) {   // tf.argmax: first maximal index
       int best = 0;
-      float bv = qs[0];
-      if (qs[1] > bv) { best = 1; bv = qs[1]; }
-      if (qs[2] > bv) best = 2;
-      mx = best == 0 ? q0 : (best == 1 ? q1 : q2);
-    } else {
-      mx = fmaxf(fmaxf(q0, q1), q2);
+      float bv = q0;
+      if (q1 > bv) { best = 1; bv = q1; }
+      if (q2 > bv) best = 2;
+      A.argmax[b] = (uint8_t)best;
+    } else if (MODE == 2) {
+      float mx;
+      if (A.q_select) {
+        const float* qs = A.q_select + b * 3;
+        int best = 0;
+        float bv = qs[0];
+        if (qs[1] > bv) { best = 1; bv = qs[1]; }
+        if (qs[2] > bv) best = 2;
+        mx = best == 0 ? q0 : (best == 1 ? q1 : q2);
+      } else {
+        mx = fmaxf(fmaxf(q0, q1), q2);
+      }
+      const float r = A.rewards[b];
+      // add_arrays(reward, array_mul(max_future, gamma)) (self_driving_tf_q_learner.rs:189-199,298-315): two roundings
+      A.y_out[b] = A.dones[b] ? r : __fadd_rn(r, __fmul_rn(mx, A.gamma));
+    } else if (MODE == 3) {
+      const int a = A.actions[b];
+      const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
+      const float e = __fsub_rn(qa, A.y[b]);
+      const float ae = fabsf(e);
+      const float wgt = A.weights ? A.weights[b] : 1.0f;   // prioritized replay: the IS weight scales h and dloss/dq
+      const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
+      const float gb = __fmul_rn(wgt, ge) / (float)A.B;
+      A.gsample[b] = gb;
+      A.hsample[b] = __fmul_rn(wgt, ae <= 1.0f ? __fmul_rn(__fmul_rn(0.5f, e), e) : __fsub_rn(ae, 0.5f));
+      if (A.td_abs) A.td_abs[b] = ae;
+      gsh[j] = gb;
+      ash[j] = a;
     }
-    const float r = A.rewards[b];
-    // add_arrays(reward, array_mul(max_future, gamma)) (self_driving_tf_q_learner.rs:189-199,298-315): two roundings
-    A.y_out[b] = A.dones[b] ? r : __fadd_rn(r, __fmul_rn(mx, A.gamma));
-  } else if (MODE == 3) {
-    const int a = A.actions[b];
-    const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
-    const float e = __fsub_rn(qa, A.y[b]);
-    const float ae = fabsf(e);
-    const float wgt = A.weights ? A.weights[b] : 1.0f;   // prioritized replay: the IS weight scales h and dloss/dq
-    const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
-    A.gsample[b] = __fmul_rn(wgt, ge) / (float)A.B;
-    A.hsample[b] = __fmul_rn(wgt, ae <= 1.0f ? __fmul_rn(__fmul_rn(0.5f, e), e) : __fsub_rn(ae, 0.5f));
-    if (A.td_abs) A.td_abs[b] = ae;
   }
-}
-
-// dz4[b][k] = (a4 > 0) ? W4[k][a_b] * g_b : 0  (the dense-3 backward: dq is g_b at a_b and 0 elsewhere, so the
-// fmaf chain over n of W4[k][n] dq[b][n] is the single rounded product)
-__global__ __launch_bounds__(256) void k_dz4_32(const float* a4, const float* w4, const uint8_t* act, const float* gs, int B,
-                                                float* dz4) {
-  const int i = blockIdx.x * 256 + threadIdx.x;   // float4 index
-  if (i >= B * 128) return;
-  const int b = i >> 7, k = (i & 127) * 4;
-  const f32x4 x = ld4(a4 + (size_t)i * 4);
-  const int a = act[b];
-  const float g = gs[b];
-  f32x4 d;
+  if (MODE == 3 && A.dz4_out) {   // the block's 16 x 512 dz4 as float4s, 8 per thread (a4 rows are cache-hot)
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) d[j] = x[j] > 0.0f ? __fmul_rn(w4[(k + j) * 3 + a], g) : 0.0f;
-  *reinterpret_cast<f32x4*>(dz4 + (size_t)i * 4) = d;
+    for (int r = 0; r < 8; ++r) {
+      const int f = threadIdx.x + 256 * r, jj = f >> 7, k = 4 * (f & 127), bb = s0 + jj;
+      if (bb < A.B) {
+        const f32x4 xa = ld4(A.a4f + (size_t)bb * 512 + k);
+        const int a = ash[jj];
+        const float gb = gsh[jj];
+        f32x4 d;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = xa[e] > 0.0f ? __fmul_rn(A.w4[(k + e) * 3 + a], gb) : 0.0f;
+        *reinterpret_cast<f32x4*>(A.dz4_out + (size_t)bb * 512 + k) = d;
+      }
+    }
+  }
 }
 
 // Conv weight gradients: dW = sum over sample chunks z in order of the chunk partials (t = 0; t = t + P_z), written into
@@ -420,7 +432,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
 }
 
 void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s) {
-  const dim3 g((B + 63) / 64), blk(256);   // 16 samples per wave
+  const dim3 g((B + 15) / 16), blk(256);   // 16 samples per block
   switch (mode) {
     case 0: hipLaunchKernelGGL(k_head32<0>, g, blk, 0, s, a); break;
     case 1: hipLaunchKernelGGL(k_head32<1>, g, blk, 0, s, a); break;
@@ -447,10 +459,8 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
     a.hsample = w.hs;
     a.weights = weights;
     a.td_abs = td_abs;
+    a.dz4_out = w.fdz4;
     f32_head(3, a, B, s);
-    hipLaunchKernelGGL(k_dz4_32, dim3((B * 128 + 255) / 256), dim3(256), 0, s, w.fa4, p + voff(8), actions, w.gs, B, w.fdz4);
-    QLX_HIP(hipGetLastError());
-    debug_sync(s, "k_dz4_32");
   }
   {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its leading blocks
     PFc1WgradS Pw{grid(3136, 64, 512, 32, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
