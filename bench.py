@@ -39,6 +39,9 @@ PEAK_HBM_GBS = 8000.0                            # HBM3E
 # per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
 FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
 TRANSITION_BYTES = 56_454          # logical (a, s, s', r, done) of one sampled transition
+# with the Bellman-target memo (learner.hip ycache_fill: the frozen target net's y computed once per transition at
+# insertion) a sampled transition delivers (a, s, y); s' is read once, by the memo pass over the new transitions
+MEMO_SAMPLED_BYTES = 1 + 4 * 7056 + 4
 ADAM_BYTES = 53_941_344            # clip_by_norm + Adam per update: g read twice, w / m / v read and written
 # profiler scopes of each precision: the GEMM-shaped kernels (FLOP work) and their per-layer grouping
 GEMM_SCOPES = {
@@ -68,6 +71,9 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=1)
     ap.add_argument("--double-dqn", action="store_true", help="extension (config C5): double-DQN targets")
     ap.add_argument("--per", action="store_true", help="extension (config C5): proportional prioritized replay")
+    ap.add_argument("--no-target-memo", action="store_true",
+                    help="evaluate the frozen target net per sampled batch (QLX_TARGET_CACHE=0) instead of once per "
+                         "transition at insertion (same values; the reference's per-batch work)")
     ap.add_argument("--control-only", action="store_true",
                     help="exercise the rank spawn + gloo control plane only (no GPU; CPU test of the N > 1 path)")
     return ap.parse_args()
@@ -306,17 +312,24 @@ class Run:
         upd = self.updates / max(self.steps, 1) / max(self.ctl.world, 1)   # updates per vector step on one GPU
         B = self.args.batch
         t_samp = sum(c[k]["total_us_per_step"] for k in SAMPLE_SCOPES[self.precision][:3] if k in c)
-        if "f32_conv1_fwd_big" in c:   # the target chunks' share (U*B of the U*B + n_envs samples per vector step)
-            t_samp += c["f32_conv1_fwd_big"]["total_us_per_step"] * upd * B / (upd * B + self.args.envs)
-        samp_gbs = rate(upd * B * TRANSITION_BYTES, t_samp, 1e3)
+        memo = "target_memo" in c
+        if memo:
+            tb, note = MEMO_SAMPLED_BYTES, ("logical bytes of a sampled transition (a, s, y: the target memo holds y) "
+                                            "delivered into the net / time of index draw + gather + the online pass's "
+                                            "conv1 frame fetch")
+        else:
+            tb, note = TRANSITION_BYTES, ("logical transition bytes (a, s, s', r, done) delivered into the net / time "
+                                          "of index draw + gather + conv1 frame-fetch launches")
+            if "f32_conv1_fwd_big" in c:   # the target chunks' share (U*B of the U*B + n_envs samples per vector step)
+                t_samp += c["f32_conv1_fwd_big"]["total_us_per_step"] * upd * B / (upd * B + self.args.envs)
+        samp_gbs = rate(upd * B * tb, t_samp, 1e3)
         t_adam = sum(c[k]["total_us_per_step"] for k in ADAM_SCOPES[self.precision] if k in c)
         adam_gbs = rate(upd * ADAM_BYTES, t_adam, 1e3)
         return {
             "mfma_per_layer": layers,
             "replay_sampling": {"gbs": round(samp_gbs, 1), "frac": round(samp_gbs / PEAK_HBM_GBS, 4),
-                                "bytes_per_transition": TRANSITION_BYTES, "scopes": list(SAMPLE_SCOPES[self.precision]),
-                                "note": "logical transition bytes (a, s, s', r, done) delivered into the net / time of "
-                                        "index draw + gather + conv1 frame-fetch launches"},
+                                "bytes_per_transition": tb,
+                                "scopes": list(SAMPLE_SCOPES[self.precision][:3 if memo else 4]), "note": note},
             "clip_adam": {"gbs": round(adam_gbs, 1), "frac": round(adam_gbs / PEAK_HBM_GBS, 4),
                           "bytes_per_update": ADAM_BYTES, "scopes": list(ADAM_SCOPES[self.precision])},
         }
@@ -355,6 +368,8 @@ def control_check(ctl):
 
 def main():
     args = parse()
+    if args.no_target_memo:
+        os.environ["QLX_TARGET_CACHE"] = "0"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
     ctl = Control()
@@ -398,6 +413,7 @@ def main():
                                + (" + prioritized replay" if args.per else ""),
                    "envs_per_gpu": N, "batch": B, "replay_capacity": args.replay, "update_after_actions": head.ua,
                    "parallelism": f"dp{ctl.world}" if ctl.world > 1 else "single", "rccl_world": ctl.world,
+                   "target_memo": "target_memo" in head.comps,
                    "env_dtype": "fp32 physics, u8 frames",
                    "qnet_dtype": "fp32 (exact-fp32 MFMA v_mfma_f32_16x16x4_f32)" if args.precision == "fp32"
                    else "bf16 MFMA operands, fp32 accumulate + master weights"},

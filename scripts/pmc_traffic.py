@@ -18,17 +18,19 @@ SCOPES = {
     "fp32": {
         "f32_conv1_fwd": "k_conv1_fwd32<0>",
         "f32_conv1_fwd_big": "k_conv1_fwd32<1>",
-        "f32_conv2_fwd": "PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>",
-        "f32_conv2_fwd_big": "PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2>",
-        "f32_conv3_fwd": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>",
-        "f32_conv3_fwd_big": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2>",
-        "f32_fc1_fwd": "PFc1FwdT<32, 32, 2, 2>",
-        "f32_fc1_fwd_big": "PFc1FwdT<32, 64, 2, 2>",
+        "f32_conv2_fwd": "PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2,",
+        "f32_conv2_fwd_big": "PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2,",
+        "f32_conv3_fwd": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2,",
+        "f32_conv3_fwd_big": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2,",
+        "f32_fc1_fwd": "k_gemm32<qlx::q32::PFc1FwdT<32, 32, 2, 2,",
+        "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<32, 64, 2, 2,",
         "f32_fc1_bwd": "k_gemm32_pair<qlx::q32::PFc1WgradT",
         "f32_conv3_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<9, 9",
         "f32_conv2_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<20, 20",
         "f32_conv1_wgrad": "k_conv1_wgrad32",
         "f32_norms": "k_norm32",
+        "f32_head": "k_head32<3>",
+        "f32_wgrad_reduce": "k_wreduce32",
         "f32_adam": "k_adam32",
     },
     "bf16": {
