@@ -15,7 +15,8 @@
 //   dense-3 bwd     dz4[b][k] = a4 > 0 ? W4[k][a_b] g_b : 0; dW4[k][n] = chain over b of a4[b][k] dq[b][n]
 //   dense-512 bwd   dW3[k][n] = chain over b of a3[b][k] dz4[b][n]; dz3 = a3 > 0 ? chain over n : 0
 //   conv dgrad      dz_in[b][ih][iw][c] = a_in > 0 ? chain over the valid taps (kh, kw, oc) lexicographic : 0
-//   conv wgrad      per sample chunk z of SC_l samples: P_z = chain over (b, oh, ow) ascending; dW = ((0 + P_0) + P_1) ..
+//   conv wgrad      per sample chunk z of SC_l samples: P_z = chain over (b, oh, ow) ascending; chunks in groups of 16:
+//                   S_q = chain over z in [16 q, 16 q + 16), dW = chain over q of S_q
 //                   bias: P_z = ((C0 + C1) + C2) + C3, Cq = chain over the chunk-local rows r = q mod 4 ascending
 //   dense-512 db3   ((C0 + C1) + C2) + C3, Cq = chain over b = q mod 4 ascending
 //   clip_by_norm    per variable: segments of 2048 elements; lane l < 256 chains fmaf(g, g, t) over the segment's
@@ -165,21 +166,23 @@ static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const 
               }
         }
   }
-  for (int i = 0; i < KK * c.OC; ++i) {
+  // chunk partials in groups of 16: S_q = chain over the group's chunks, dW = chain over q of S_q
+  auto combine = [&](size_t i) {
     float t = 0.0f;
-    for (int z = 0; z < nz; ++z) t = t + part[(size_t)z * (KK + 1) * c.OC + i];
-    dW[i] = t;
-  }
+    for (int q = 0; q * 16 < nz; ++q) {
+      float sq = 0.0f;
+      for (int z = 16 * q; z < std::min(nz, 16 * q + 16); ++z) sq = sq + part[(size_t)z * (KK + 1) * c.OC + i];
+      t = t + sq;
+    }
+    return t;
+  };
+  for (int i = 0; i < KK * c.OC; ++i) dW[i] = combine(i);
   for (int z = 0; z < nz; ++z)   // bias partial of chunk z = ((C0 + C1) + C2) + C3
     for (int oc = 0; oc < c.OC; ++oc) {
       const float* C = Pq.data() + (size_t)z * 4 * c.OC;
       part[((size_t)z * (KK + 1) + KK) * c.OC + oc] = ((C[oc] + C[c.OC + oc]) + C[2 * c.OC + oc]) + C[3 * c.OC + oc];
     }
-  for (int oc = 0; oc < c.OC; ++oc) {
-    float t = 0.0f;
-    for (int z = 0; z < nz; ++z) t = t + part[((size_t)z * (KK + 1) + KK) * c.OC + oc];
-    db[oc] = t;
-  }
+  for (int oc = 0; oc < c.OC; ++oc) db[oc] = combine((size_t)KK * c.OC + oc);
 }
 
 // conv backward-data: din[b][ih][iw][c] = mask(a_in) * chain over the valid (kh, kw, oc) of dz[..][oc] W[kh][kw][c][oc]

@@ -123,46 +123,49 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
   }
 }
 
-// Conv weight gradients: dW = sum over sample chunks z in order of the chunk partials (t = 0; t = t + P_z), written into
-// the flat gradient.  Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order.  The last
-// row of each is the bias.
+// Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
+// [16 q, 16 q + 16)), S_q = chain over its chunks in order, dW = chain over q of S_q (each chain t = 0; t = t + x).
+// Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order, the last row of each the bias.
+// Block = 64 consecutive outputs x 16 group lanes (one wave per lane, 256-byte rows per load): wave g chains groups
+// g, g + 16, .. (16 partial loads in flight each); the group sums meet in LDS and wave 0 chains them.
+constexpr int kWGroup = 16;
+constexpr int kWGroupsMax = 128;   // chunks <= 2,048 (conv1 at the largest fp32 batch, 8,192)
 struct WRed {
   const float* slab[3];
   int nz[3];
-  int count[3];   // (M + 1) * OC
+  int count[3];   // (M + 1) * OC; segments 0 and 1 are multiples of 64
   int oc[3];
   float* gw[3];   // W gradient
   float* gb[3];   // b gradient
 };
-__global__ __launch_bounds__(256) void k_wreduce32(WRed R) {
-  int e = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(1024) void k_wreduce32(WRed R) {
+  __shared__ float gs[kWGroupsMax * 64];
+  const int o = threadIdx.x & 63, g0 = threadIdx.x >> 6;
+  int e = blockIdx.x * 64;
   int L = 0;
   while (L < 3 && e >= R.count[L]) { e -= R.count[L]; ++L; }
-  if (L >= 3) return;
-  const float* p = R.slab[L] + e;
+  if (L >= 3) return;   // block-uniform
+  const bool live = e + o < R.count[L];
   const size_t stride = (size_t)R.count[L];
-  const int nz = R.nz[L];
+  const int nz = R.nz[L], ng = (nz + kWGroup - 1) / kWGroup;
+  const float* p = R.slab[L] + e + (live ? o : 0);
+  for (int q = g0; q < ng; q += 16) {
+    float v[kWGroup];
+#pragma unroll
+    for (int j = 0; j < kWGroup; ++j) v[j] = q * kWGroup + j < nz ? p[(size_t)(q * kWGroup + j) * stride] : 0.0f;
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kWGroup; ++j) t = __fadd_rn(t, v[j]);   // + 0 past the last chunk leaves t unchanged
+    gs[q * 64 + o] = t;
+  }
+  __syncthreads();
+  if (g0 != 0 || !live) return;
   float t = 0.0f;
-  int z = 0;
-  for (; z + 32 <= nz; z += 32) {   // 32 partial loads in flight, then the in-order sum
-    float v[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = p[(size_t)(z + j) * stride];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) t = __fadd_rn(t, v[j]);
-  }
-  for (; z + 8 <= nz; z += 8) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = p[(size_t)(z + j) * stride];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t = __fadd_rn(t, v[j]);
-  }
-  for (; z < nz; ++z) t = __fadd_rn(t, p[(size_t)z * stride]);
-  const int oc = R.oc[L], m = e / oc, n = e - m * oc;
+  for (int q = 0; q < ng; ++q) t = __fadd_rn(t, gs[q * 64 + o]);
+  const int oc = R.oc[L], m = (e + o) / oc, n = (e + o) - m * oc;
   const int M = R.count[L] / oc - 1;
-  if (m == M) { R.gb[L][n] = t; return; }
-  R.gw[L][(size_t)m * oc + n] = t;
+  if (m == M) R.gb[L][n] = t;
+  else R.gw[L][(size_t)m * oc + n] = t;
 }
 
 // clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg = 2048;
@@ -503,7 +506,8 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     R.slab[1] = w.fslab2; R.nz[1] = z2; R.count[1] = 513 * 64; R.oc[1] = 64; R.gw[1] = G + voff(2); R.gb[1] = G + voff(3);
     R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
     const int total = R.count[0] + R.count[1] + R.count[2];
-    hipLaunchKernelGGL(k_wreduce32, dim3((total + 255) / 256), dim3(256), 0, s, R);
+    QLX_CHECK(std::max({z1, z2, z3}) <= kWGroup * kWGroupsMax, QLX_E_INVALID, "too many weight-gradient chunks");
+    hipLaunchKernelGGL(k_wreduce32, dim3((total + 63) / 64), dim3(1024), 0, s, R);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_wreduce32");
   }

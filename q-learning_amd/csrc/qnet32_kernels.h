@@ -47,6 +47,14 @@ struct Opnd {
   __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & (MF - 1)), KG * kk + lane / MF); }
 };
 
+// K-split groups of a policy: its member KSPLIT when it has one, else 1 (gemm_body)
+template <class P, class = void>
+struct KSplitOf : std::integral_constant<int, 1> {};
+template <class P>
+struct KSplitOf<P, std::void_t<decltype(P::KSPLIT)>> : std::integral_constant<int, P::KSPLIT> {};
+template <class P>
+constexpr int threads_of() { return P::WM * P::WN * 64 * KSplitOf<P>::value; }
+
 // MFMA shape of a policy: its member MF when it has one, else 16
 template <class P, class = void>
 struct MfOf : std::integral_constant<int, 16> {};
@@ -98,25 +106,34 @@ struct ACtxOf<P, true> { using type = typename P::ACtx; };
 //   acc[row][col] = sum over the slabs s = 0 .. nslabs(z) - 1 and k = 0 .. 31 of A(z, s, row, k) * B(z, s, col, k),
 // one fmaf chain per output in (s, k) order; then P::epi stores it.  With P::BIAS the tiles of row-tile 0 also
 // sum B's columns (bias gradient): four chains over the reduction index mod 4, combined ((C0 + C1) + C2) + C3.
+// With P::KSPLIT = G > 1 the block runs G wave groups, group g chaining the slabs [g ns / G, (g + 1) ns / G) into its
+// own accumulators (own LDS buffers, the same barriers); the tile is then ((C0 + C1) + ..) + C(G-1), summed by group 0
+// through LDS before its epilogue (ns must be a multiple of G).
 template <class P>
 __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   constexpr int MF = MfOf<P>::value;
   using OA = Opnd<P::BM, P::A_KMAJ, MF>;
   using OB = Opnd<P::BN, P::B_KMAJ, MF>;
   using Acc = typename MfAcc<MF>::type;
-  constexpr int T = P::WM * P::WN * 64;
+  constexpr int G = KSplitOf<P>::value;
+  static_assert(G == 1 || !P::BIAS, "K-split groups: no bias chains");
+  constexpr int T = P::WM * P::WN * 64;   // threads of one K group
   constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
   static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
   constexpr int NA = (OA::F4 + T - 1) / T, NB = (OB::F4 + T - 1) / T;
-  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int GROUP_LDS = 2 * (OA::FLOATS + OB::FLOATS);
+  static_assert(G == 1 || TM * TN * (MF * MF / 64) * T <= GROUP_LDS, "K-split hand-off fits the group's LDS");
+  const int kg = G > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6) / (P::WM * P::WN)) : 0;
+  const int tid = threadIdx.x - kg * T, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % P::WM, wn = wave / P::WM;
   int tm, tn, z;
   p.decode(lb, tm, tn, z);
   const int row0 = tm * P::BM, col0 = tn * P::BN;
-  const int ns = p.nslabs(z);
+  const int ns = p.nslabs(z) / G, s_base = kg * ns;   // this group's slabs: s_base + [0, ns)
   typename ACtxOf<P>::type actx{};
   if constexpr (HasACtx<P>::value) actx = p.a_ctx(z, row0, tid);
+  lds += kg * GROUP_LDS;
   float* As0 = lds;
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
@@ -131,8 +148,8 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
       if (OA::F4 % T == 0 || idx < OA::F4) {
         int r, k;
         OA::coord(idx, r, k);
-        if constexpr (HasACtx<P>::value) ra[i] = p.ldA_c(actx, i, z, s, row0 + r, k);
-        else ra[i] = p.ldA(z, s, row0 + r, k);
+        if constexpr (HasACtx<P>::value) ra[i] = p.ldA_c(actx, i, z, s_base + s, row0 + r, k);
+        else ra[i] = p.ldA(z, s_base + s, row0 + r, k);
       }
     }
 #pragma unroll
@@ -141,7 +158,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
       if (OB::F4 % T == 0 || idx < OB::F4) {
         int r, k;
         OB::coord(idx, r, k);
-        rb[i] = p.ldB(z, s, col0 + r, k);
+        rb[i] = p.ldB(z, s_base + s, col0 + r, k);
       }
     }
   };
@@ -219,6 +236,27 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     iter(s, ra0, rb0, ra1, rb1);
     if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
   }
+  if constexpr (G > 1) {   // groups 1 .. G - 1 hand their accumulators to group 0 through their own LDS (free now)
+    constexpr int E = MF * MF / 64;
+    if (kg > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < E; ++e) lds[((i * TN + j) * E + e) * T + tid] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (kg > 0) return;
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < E; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], lds[g * GROUP_LDS + ((i * TN + j) * E + e) * T + tid]);
+  }
   // accumulator layout: MF 16: lane l holds rows 4 (l / 16) .. + 3 of column l % 16; MF 32: element 4 q + e is row
   // 8 q + 4 (l / 32) + e of column l % 32
 #pragma unroll
@@ -256,7 +294,8 @@ __device__ __forceinline__ int block_order(int h, int G) { return RawOrder<P>::v
 
 template <class P>
 constexpr size_t gemm_lds_bytes() {
-  return 2 * (size_t)(Opnd<P::BM, P::A_KMAJ, MfOf<P>::value>::FLOATS + Opnd<P::BN, P::B_KMAJ, MfOf<P>::value>::FLOATS) * sizeof(float);
+  return (size_t)KSplitOf<P>::value * 2 *
+         (size_t)(Opnd<P::BM, P::A_KMAJ, MfOf<P>::value>::FLOATS + Opnd<P::BN, P::B_KMAJ, MfOf<P>::value>::FLOATS) * sizeof(float);
 }
 
 // grid layout shared by the policies: tile index fastest (col tile, then row tile), then z
@@ -272,7 +311,7 @@ struct Grid {
 };
 
 template <class P>
-__global__ __launch_bounds__(256) void k_gemm32(const P p) {
+__global__ __launch_bounds__(threads_of<P>()) void k_gemm32(const P p) {
   extern __shared__ float lds[];
   gemm_body(p, block_order<P>(blockIdx.x, gridDim.x), lds);
 }
@@ -281,6 +320,7 @@ __global__ __launch_bounds__(256) void k_gemm32(const P p) {
 // running S
 template <class P1, class P2, class S>
 __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, const S side) {
+  static_assert(KSplitOf<P1>::value == 1 && KSplitOf<P2>::value == 1, "pair launches: 256 threads");
   extern __shared__ float lds[];
   const int b = blockIdx.x;
   if (b < S::BLOCKS) { side.run(b, lds); return; }

@@ -166,10 +166,16 @@ static double time_us(F f, int reps = 15) {
 
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
+// K-split wave groups on any policy (gemm_body KSPLIT)
+template <class Base, int K>
+struct KSplit : Base {
+  static constexpr int KSPLIT = K;
+};
+
 template <class P>
 static void run1(const char* name, const P& p, double flop) {
   CK(hipFuncSetAttribute((const void*)k_gemm32<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<P>()));
-  const double us = time_us([&] { hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), 0, p); });
+  const double us = time_us([&] { hipLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(threads_of<P>()), gemm_lds_bytes<P>(), 0, p); });
   printf("%-34s blocks %6d lds %6zu  %9.2f us  %7.2f TF  %5.1f %%\n", name, p.g.blocks(), gemm_lds_bytes<P>(), us,
          flop / us / 1e6, flop / us / 1e6 / 157.3 * 100);
 }
@@ -308,6 +314,28 @@ int main(int argc, char** argv) {
     run1("conv3_dgrad t32x64 w2x2", PConv3DgradT<32, 64, 2, 2>{grid(B * 81, 32, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_dgrad t128x64 w2x2", PConv3DgradT<128, 64, 2, 2>{grid(B * 81, 128, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_wgrad t64x32 w2x2", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 32, 2, 2>{grid(576, 64, 64, 32, B / 16), a2, dz3, slab, B}, flop);
+    printf("--- K-split wave groups, B = 1024 and 8192\n");
+    for (int BB : {1024, 8192}) {
+      const double f1 = 2.0 * BB * 3136 * 512, f2 = 2.0 * BB * 81 * 64 * 512, f3 = 2.0 * BB * 49 * 64 * 576;
+      printf("B = %d\n", BB);
+      run1("fc1_fwd t32x32 ks1", PFc1FwdT<32, 32, 2, 2>{grid(BB, 32, 512, 32, 1), a3, W3, W3, a4, BB}, f1);
+      run1("fc1_fwd t32x32 ks2", KSplit<PFc1FwdT<32, 32, 2, 2>, 2>{{grid(BB, 32, 512, 32, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("fc1_fwd t64x32 ks2", KSplit<PFc1FwdT<64, 32, 2, 2>, 2>{{grid(BB, 64, 512, 32, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("fc1_fwd t32x64 ks2", KSplit<PFc1FwdT<32, 64, 2, 2>, 2>{{grid(BB, 32, 512, 64, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("fc1_fwd t64x64 ks2", KSplit<PFc1FwdT<64, 64, 2, 2>, 2>{{grid(BB, 64, 512, 64, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("fc1_fwd t32x32 ks4", KSplit<PFc1FwdT<32, 32, 2, 2>, 4>{{grid(BB, 32, 512, 32, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("fc1_fwd t64x64 ks4", KSplit<PFc1FwdT<64, 64, 2, 2>, 4>{{grid(BB, 64, 512, 64, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("conv2_fwd t64x32 ks1", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>{grid(BB * 81, 64, 64, 32, 1), a1, W1, W1, a2, BB * 81}, f2);
+      run1("conv2_fwd t64x32 ks2", KSplit<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>, 2>{{grid(BB * 81, 64, 64, 32, 1), a1, W1, W1, a2, BB * 81}}, f2);
+      run1("conv2_fwd t64x64 ks2", KSplit<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2>, 2>{{grid(BB * 81, 64, 64, 64, 1), a1, W1, W1, a2, BB * 81}}, f2);
+      run1("conv3_fwd t64x32 ks1", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>{grid(BB * 49, 64, 64, 32, 1), a2, W2, W2, a3, BB * 49}, f3);
+      run1("conv3_fwd t64x32 ks2", KSplit<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>, 2>{{grid(BB * 49, 64, 64, 32, 1), a2, W2, W2, a3, BB * 49}}, f3);
+      run1("conv3_fwd t64x64 ks2", KSplit<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2>, 2>{{grid(BB * 49, 64, 64, 64, 1), a2, W2, W2, a3, BB * 49}}, f3);
+      if (BB > 1024) continue;
+      run1("fc1_dgrad t32x64 ks1", PFc1DgradT<32, 64, 2, 2>{grid(BB, 32, 3136, 64, 1), dz4, W3, a3, dz3, BB}, f1);
+      run1("fc1_dgrad t32x64 ks2", KSplit<PFc1DgradT<32, 64, 2, 2>, 2>{{grid(BB, 32, 3136, 64, 1), dz4, W3, a3, dz3, BB}}, f1);
+      run1("fc1_dgrad t64x64 ks2", KSplit<PFc1DgradT<64, 64, 2, 2>, 2>{{grid(BB, 64, 3136, 64, 1), dz4, W3, a3, dz3, BB}}, f1);
+    }
     printf("--- pixel-major backward data\n");
     for (int BB : {1024, 8192}) {
       if (BB > Bmax) break;
