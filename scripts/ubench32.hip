@@ -166,6 +166,17 @@ static double time_us(F f, int reps = 15) {
 
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
+// row-tile-fastest block order (consecutive blocks share a column tile: an XCD's blocks keep one slice of B in its L2)
+template <class Base>
+struct RowFast : Base {
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const {
+    tm = lb % this->g.tiles_m;
+    const int q = lb / this->g.tiles_m;
+    tn = q % this->g.tiles_n;
+    z = q / this->g.tiles_n;
+  }
+};
+
 // K-split wave groups on any policy (gemm_body KSPLIT)
 template <class Base, int K>
 struct KSplit : Base {
@@ -314,6 +325,34 @@ int main(int argc, char** argv) {
     run1("conv3_dgrad t32x64 w2x2", PConv3DgradT<32, 64, 2, 2>{grid(B * 81, 32, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_dgrad t128x64 w2x2", PConv3DgradT<128, 64, 2, 2>{grid(B * 81, 128, 64, 64, 1), dz3, W2, a2, dz2, B * 81}, flop);
     run1("conv3_wgrad t64x32 w2x2", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 32, 2, 2>{grid(576, 64, 64, 32, B / 16), a2, dz3, slab, B}, flop);
+    printf("--- block order: column-tile fastest (shipped) vs row-tile fastest, B = 1024\n");
+    {
+      const int BB = 1024;
+      const double f1 = 2.0 * BB * 3136 * 512, f2 = 2.0 * BB * 81 * 64 * 512;
+      run1("fc1_fwd S colfast", PFc1FwdT<32, 32, 2, 2>{grid(BB, 32, 512, 32, 1), a3, W3, W3, a4, BB}, f1);
+      run1("fc1_fwd S rowfast", RowFast<PFc1FwdT<32, 32, 2, 2>>{{grid(BB, 32, 512, 32, 1), a3, W3, W3, a4, BB}}, f1);
+      run1("fc1_dgrad S colfast", PFc1DgradT<32, 64, 2, 2>{grid(BB, 32, 3136, 64, 1), dz4, W3, a3, dz3, BB}, f1);
+      run1("fc1_dgrad S rowfast", RowFast<PFc1DgradT<32, 64, 2, 2>>{{grid(BB, 32, 3136, 64, 1), dz4, W3, a3, dz3, BB}}, f1);
+      run1("fc1_wgrad S colfast", PFc1WgradT<64, 32, 2, 2>{grid(3136, 64, 512, 32, 1), a3, dz4, gw, gw, BB}, f1);
+      run1("fc1_wgrad S rowfast", RowFast<PFc1WgradT<64, 32, 2, 2>>{{grid(3136, 64, 512, 32, 1), a3, dz4, gw, gw, BB}}, f1);
+      run1("conv2_fwd S colfast", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>{grid(BB * 81, 64, 64, 32, 1), a1, W1, W1, a2, BB * 81}, f2);
+      run1("conv2_fwd S rowfast", RowFast<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>>{{grid(BB * 81, 64, 64, 32, 1), a1, W1, W1, a2, BB * 81}}, f2);
+    }
+    printf("--- weight-gradient sample-chunk size, B = 1024\n");
+    {
+      const int BB = 1024;
+      const double f3 = 2.0 * BB * 49 * 64 * 576, f2 = 2.0 * BB * 81 * 64 * 512;
+      run1("conv3_wgrad sc16 t64x64", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, BB / 16), a2, dz3, slab, BB}, f3);
+      run1("conv3_wgrad sc8 t64x64", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 8>{grid(576, 64, 64, 64, BB / 8), a2, dz3, slab, BB}, f3);
+      run1("conv3_wgrad sc4 t64x64", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 4>{grid(576, 64, 64, 64, BB / 4), a2, dz3, slab, BB}, f3);
+      run1("conv3_wgrad sc32 t64x64", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 32>{grid(576, 64, 64, 64, BB / 32), a2, dz3, slab, BB}, f3);
+      run1("conv2_wgrad sc16 t64x64", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, BB / 16), a1, dz2, slab, BB}, f2);
+      run1("conv2_wgrad sc8 t64x64", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 8>{grid(512, 64, 64, 64, BB / 8), a1, dz2, slab, BB}, f2);
+      run1("conv2_wgrad sc4 t64x64", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 4>{grid(512, 64, 64, 64, BB / 4), a1, dz2, slab, BB}, f2);
+      run1("conv2_wgrad sc32 t64x64", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 32>{grid(512, 64, 64, 64, BB / 32), a1, dz2, slab, BB}, f2);
+      run1("conv2_wgrad sc8 t128x64", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 8, 128, 64, 2, 2>{grid(512, 128, 64, 64, BB / 8), a1, dz2, slab, BB}, f2);
+      run1("conv3_wgrad sc8 t64x32", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 8, 64, 32, 2, 2>{grid(576, 64, 64, 32, BB / 8), a2, dz3, slab, BB}, f3);
+    }
     printf("--- K-split wave groups, B = 1024 and 8192\n");
     for (int BB : {1024, 8192}) {
       const double f1 = 2.0 * BB * 3136 * 512, f2 = 2.0 * BB * 81 * 64 * 512, f3 = 2.0 * BB * 49 * 64 * 576;
