@@ -98,6 +98,111 @@ __global__ __launch_bounds__(256) void k_gen32x32(const float* A, const float* B
       }
 }
 
+// experimental core 2: v_mfma_f32_32x32x2_f32 with an MFMA-fragment-major LDS image: operand row r holds its slab's 32 k as
+// [h = k % 2][j = k / 2] (+4 pad, pitch 36), so a lane's 16 values for the slab are contiguous: 4 ds_read_b128 per
+// fragment per slab, all issued at the slab's start, then 16 MFMAs back to back.  A row-major [M][K] (float4 along k ->
+// two 8-byte stores), B row-major [K][N] (a thread loads 4 k x 4 n and writes each n's 4 k as two 8-byte stores).
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void k_gen32p(const float* A, const float* Bm, float* C, int M, int N, int K) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32), T = 256, P = 36;
+  constexpr int AF = BM * P, BF = BN * P;
+  constexpr int NA = BM * BK / 4 / T;               // float4 of A per thread
+  constexpr int NBT = (BK / 4) * (BN / 4);          // B threads (each 4 k x 4 n)
+  static_assert(NA >= 1 && NBT <= T, "tile");
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave % WM, wn = wave / WM;
+  const int tiles_n = N / BN, lb = xcd_logical(blockIdx.x, gridDim.x), tm = lb / tiles_n, tn = lb % tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN, ns = K / BK;
+  f32x4 ra[NA], rb[4];
+  auto load = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) { const int idx = tid + i * T, r = idx >> 3, k = (idx & 7) * 4; ra[i] = ld4(A + (size_t)(row0 + r) * K + s * BK + k); }
+    if (tid < NBT) {
+      const int q = tid / (BN / 4), c = (tid % (BN / 4)) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rb[e] = ld4(Bm + (size_t)(s * BK + 4 * q + e) * N + col0 + c);
+    }
+  };
+  auto store = [&](int s) {
+    float* a = lds + (s & 1) * AF;
+    float* b = lds + 2 * AF + (s & 1) * BF;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T, r = idx >> 3, q = idx & 7;
+      *reinterpret_cast<f32x2*>(a + r * P + 2 * q) = f32x2{ra[i][0], ra[i][2]};
+      *reinterpret_cast<f32x2*>(a + r * P + 16 + 2 * q) = f32x2{ra[i][1], ra[i][3]};
+    }
+    if (tid < NBT) {
+      const int q = tid / (BN / 4), c = (tid % (BN / 4)) * 4;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        *reinterpret_cast<f32x2*>(b + (c + n) * P + 2 * q) = f32x2{rb[0][n], rb[2][n]};
+        *reinterpret_cast<f32x2*>(b + (c + n) * P + 16 + 2 * q) = f32x2{rb[1][n], rb[3][n]};
+      }
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  const int lr = lane & 31, lh = (lane >> 5) * 16;
+  auto compute = [&](int s) {
+    const float* a = lds + (s & 1) * AF;
+    const float* b = lds + 2 * AF + (s & 1) * BF;
+    f32x4 af[TM][4], bf[TN][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) af[i][q] = *reinterpret_cast<const f32x4*>(a + ((wm * TM + i) * 32 + lr) * P + lh + 4 * q);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bf[j][q] = *reinterpret_cast<const f32x4*>(b + ((wn * TN + j) * 32 + lr) * P + lh + 4 * q);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk >> 2][kk & 3], bf[j][kk >> 2][kk & 3], acc[i][j], 0, 0, 0);
+  };
+  load(0);
+  store(0);
+  if (ns > 1) load(1);
+  lds_barrier();
+  for (int s = 0; s < ns; ++s) {
+    compute(s);
+    if (s + 1 < ns) store(s + 1);
+    if (s + 2 < ns) load(s + 2);
+    lds_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row0 + (wm * TM + i) * 32 + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3), col = col0 + (wn * TN + j) * 32 + (lane & 31);
+        C[(size_t)row * N + col] = acc[i][j][e];
+      }
+}
+
+template <int BM, int BN, int WM, int WN>
+static void gen32p(int M, int N, int K, const float* A, const float* B, float* C) {
+  const size_t lds = 2 * (size_t)(BM + BN) * 36 * 4;
+  auto kern = k_gen32p<BM, BN, WM, WN>;
+  CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int G = (M / BM) * (N / BN);
+  const double us = time_us([&] { hipLaunchKernelGGL(kern, dim3(G), dim3(256), lds, 0, A, B, C, M, N, K); });
+  const double f = 2.0 * M * N * K;
+  printf("gen32p %dx%dx%d t%dx%d w%dx%d        blocks %6d lds %6zu  %9.2f us  %7.2f TF  %5.1f %%\n", M, N, K, BM, BN, WM, WN, G,
+         lds, us, f / us / 1e6, f / us / 1e6 / 157.3 * 100);
+}
+
 template <int BM, int BN, int WM, int WN, int PA>
 static void gen32(int M, int N, int K, const float* A, const float* B, float* C) {
   constexpr int PB = BN + (((32 - BN % 64) % 64) + 64) % 64;
@@ -420,6 +525,12 @@ int main(int argc, char** argv) {
     float* A = dbuf((size_t)65536 * 4 * 256, 20);
     float* B = dbuf((size_t)K * N, 21);
     float* C = dbuf((size_t)M * N, 22);
+    gen32p<64, 64, 2, 2>(M, N, K, A, B, C);
+    gen32p<128, 64, 2, 2>(M, N, K, A, B, C);
+    gen32p<128, 128, 2, 2>(M, N, K, A, B, C);
+    gen32p<64, 64, 2, 2>(65536, 64, 512, A, B, C);
+    gen32p<128, 64, 2, 2>(65536, 64, 512, A, B, C);
+    gen32p<128, 64, 4, 1>(65536, 64, 512, A, B, C);
     gen<64, 64, 2, 2>(M, N, K, A, B, C);
     gen32<64, 64, 2, 2, 36>(M, N, K, A, B, C);
     gen32<128, 64, 2, 2, 36>(M, N, K, A, B, C);
