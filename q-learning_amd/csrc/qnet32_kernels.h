@@ -69,6 +69,19 @@ struct MfAcc<32> { typedef f32x16 type; };
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+// Masked operand load for the policies: masked lanes load 16 zero bytes from q32_zero4, so the load is issued on every
+// path and nothing waits on its value before it is stored.  A branch around a load makes the compiler's vmcnt
+// bookkeeping path-dependent (it then waits for every outstanding load - including the next slab's - before storing
+// the current one), and a select on the loaded value pulls the wait up to the select; either collapses gemm_body's
+// two-slabs-in-flight register pipeline.
+#ifdef QLX_Q32_POLICIES_ONLY
+static const float q32_zero4[4] __attribute__((aligned(16))) = {0.0f, 0.0f, 0.0f, 0.0f};
+#else
+// (global address space, never written: a const variable would live in the constant space and turn the load into a
+// flat load, which also counts on lgkmcnt and so joins every LDS wait)
+static __attribute__((device)) float q32_zero4[4] __attribute__((aligned(16))) = {0.0f, 0.0f, 0.0f, 0.0f};
+#endif
+__device__ __forceinline__ f32x4 ld4m(const float* p, bool ok) { return ld4(ok ? p : q32_zero4); }
 __device__ __forceinline__ f32x4 u8x4(uint32_t w) {
   return f32x4{(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu), (float)((w >> 16) & 0xFFu), (float)(w >> 24)};
 }
@@ -219,9 +232,12 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
         }
     }
   };
-  // iteration s: x holds slab s + 1, y is free
+  // iteration s: x holds slab s + 1, y is free.  Every iteration issues its loads unconditionally (the last slab again
+  // past the end), so the number of loads in flight is the same on every path and the store of slab s + 1 waits only
+  // for slab s + 1's loads (vmcnt = this iteration's NA + NB), never for slab s + 2's (see ld4m)
   auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
-    if (s + 2 < ns) load(s + 2, ya, yb);
+    load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
+    __builtin_amdgcn_sched_barrier(0);   // the loads stay ahead of the slab's MFMAs (the scheduler would sink them)
     compute(s);
     if (s + 1 < ns) store(s + 1, xa, xb);
     lds_barrier();
@@ -229,12 +245,12 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   if (ns > 0) {
     load(0, ra1, rb1);
     store(0, ra1, rb1);
-  }
-  if (ns > 1) load(1, ra0, rb0);
-  lds_barrier();
-  for (int s = 0; s < ns; s += 2) {
-    iter(s, ra0, rb0, ra1, rb1);
-    if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
+    load(ns > 1 ? 1 : 0, ra0, rb0);
+    lds_barrier();
+    for (int s = 0; s < ns; s += 2) {
+      iter(s, ra0, rb0, ra1, rb1);
+      if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
+    }
   }
   if constexpr (G > 1) {   // groups 1 .. G - 1 hand their accumulators to group 0 through their own LDS (free now)
     constexpr int E = MF * MF / 64;
@@ -359,10 +375,11 @@ struct PConvFwd {
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return KS * KS * C / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
-    if (row >= M) return zero4();
+    const bool ok = row < M;
+    const int rr = ok ? row : 0;
     const int tap = (s * BK) / C, c0 = (s * BK) % C, kh = tap / KS, kw = tap % KS;
-    const int b = row / (OH * OW), p = row - b * (OH * OW), oh = p / OW, ow = p - oh * OW;
-    return ld4(in + ((size_t)(b * H + oh * S + kh) * W + ow * S + kw) * C + c0 + k);
+    const int b = rr / (OH * OW), p = rr - b * (OH * OW), oh = p / OW, ow = p - oh * OW;
+    return ld4m(in + ((size_t)(b * H + oh * S + kh) * W + ow * S + kw) * C + c0 + k, ok);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w + (size_t)(s * BK + k) * OC + col); }
   __device__ void epi(int, int row, int col, f32x4 v) const {
@@ -391,7 +408,7 @@ struct PFc1FwdT {
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 3136 / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
-    return row < M ? ld4(a3 + (size_t)row * 3136 + s * BK + k) : zero4();
+    return ld4m(a3 + (size_t)(row < M ? row : 0) * 3136 + s * BK + k, row < M);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w3 + (size_t)(s * BK + k) * 512 + col); }
   __device__ void epi(int, int row, int col, f32x4 v) const {
@@ -417,7 +434,7 @@ struct PFc1DgradT {
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 512 / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
-    return row < M ? ld4(dz4 + (size_t)row * 512 + s * BK + k) : zero4();
+    return ld4m(dz4 + (size_t)(row < M ? row : 0) * 512 + s * BK + k, row < M);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w3 + (size_t)col * 512 + s * BK + k); }
   __device__ void epi(int, int row, int col, f32x4 v) const {
@@ -447,11 +464,12 @@ struct PFc1WgradT {
   __host__ __device__ int nslabs(int) const { return (B + BK - 1) / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     const int b = s * BK + k;
-    return (b < B && row < 3136) ? ld4(a3 + (size_t)b * 3136 + row) : zero4();
+    const bool ok = b < B && row < 3136;
+    return ld4m(a3 + (ok ? (size_t)b * 3136 + row : 0), ok);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const {
     const int b = s * BK + k;
-    return b < B ? ld4(dz4 + (size_t)b * 512 + col) : zero4();
+    return ld4m(dz4 + (size_t)(b < B ? b : 0) * 512 + col, b < B);
   }
   __device__ void epi(int, int row, int col, f32x4 v) const {
 #pragma unroll
@@ -477,12 +495,12 @@ struct PConv3DgradT {
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 18; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
-    if (row >= M) return zero4();
     const int tap = s >> 1, kh = tap / 3, kw = tap - kh * 3, oc0 = (s & 1) * 32;
-    const int b = row / 81, p = row - b * 81, ih = p / 9, iw = p - ih * 9;
+    const int rr = row < M ? row : 0;
+    const int b = rr / 81, p = rr - b * 81, ih = p / 9, iw = p - ih * 9;
     const int oh = ih - kh, ow = iw - kw;
-    if (oh < 0 || oh >= 7 || ow < 0 || ow >= 7) return zero4();
-    return ld4(dz3 + ((size_t)(b * 7 + oh) * 7 + ow) * 64 + oc0 + k);
+    const bool ok = row < M && oh >= 0 && oh < 7 && ow >= 0 && ow < 7;
+    return ld4m(dz3 + (ok ? ((size_t)(b * 7 + oh) * 7 + ow) * 64 + oc0 + k : 0), ok);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const {   // W2[kh][kw][c = col][oc]
     return ld4(w2 + ((size_t)(s >> 1) * 64 + col) * 64 + (s & 1) * 32 + k);
@@ -536,10 +554,9 @@ struct PConv3DgradPx {
   }
   __host__ __device__ int nslabs(int z) const { return 2 * px(z).ntap; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
-    if (row >= B) return zero4();
     const Px q = px(z);
     const int t = s >> 1, kh = q.kh0 + t / q.nkw, kw = q.kw0 + t % q.nkw;
-    return ld4(dz3 + ((size_t)(row * 7 + q.ih - kh) * 7 + q.iw - kw) * 64 + (s & 1) * 32 + k);
+    return ld4m(dz3 + ((size_t)((row < B ? row : 0) * 7 + q.ih - kh) * 7 + q.iw - kw) * 64 + (s & 1) * 32 + k, row < B);
   }
   __device__ f32x4 ldB(int z, int s, int col, int k) const {   // W2[kh][kw][c = col][oc]
     const Px q = px(z);
@@ -587,10 +604,9 @@ struct PConv2DgradPx {
   }
   __host__ __device__ int nslabs(int z) const { return 2 * px(z).ntap; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
-    if (row >= B) return zero4();
     const Px q = px(z);
     const int t = s >> 1, th = q.th0 + t / q.ntw, tw = q.tw0 + t % q.ntw;
-    return ld4(dz2 + ((size_t)(row * 9 + q.i - th) * 9 + q.j - tw) * 64 + (s & 1) * 32 + k);
+    return ld4m(dz2 + ((size_t)((row < B ? row : 0) * 9 + q.i - th) * 9 + q.j - tw) * 64 + (s & 1) * 32 + k, row < B);
   }
   __device__ f32x4 ldB(int z, int s, int col, int k) const {   // W1[kh][kw][c][oc], col = (py, px, c)
     const Px q = px(z);
@@ -625,12 +641,12 @@ struct PConv2DgradAll {
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 8; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
-    if (row >= M) return zero4();
     const int t = s >> 1, th = t >> 1, tw = t & 1;
-    const int b = row / 100, p = row - b * 100, i = p / 10, j = p - i * 10;
+    const int rr = row < M ? row : 0;
+    const int b = rr / 100, p = rr - b * 100, i = p / 10, j = p - i * 10;
     const int oh = i - th, ow = j - tw;
-    if (oh < 0 || oh >= 9 || ow < 0 || ow >= 9) return zero4();
-    return ld4(dz2 + ((size_t)(b * 9 + oh) * 9 + ow) * 64 + (s & 1) * 32 + k);
+    const bool ok = row < M && oh >= 0 && oh < 9 && ow >= 0 && ow < 9;
+    return ld4m(dz2 + (ok ? ((size_t)(b * 9 + oh) * 9 + ow) * 64 + (s & 1) * 32 + k : 0), ok);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const {
     const int t = s >> 1, cls = col >> 5, kh = (cls >> 1) + 2 * (t >> 1), kw = (cls & 1) + 2 * (t & 1);
@@ -664,13 +680,13 @@ struct PConv2DgradT {
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 8; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
-    if (row >= M) return zero4();
     const int t = s >> 1, th = t >> 1, tw = t & 1, oc0 = (s & 1) * 32;
-    const int b = row / 100, p = row - b * 100, i = p / 10, j = p - i * 10;
+    const int rr = row < M ? row : 0;
+    const int b = rr / 100, p = rr - b * 100, i = p / 10, j = p - i * 10;
     const int oh = i - th, ow = j - tw;
-    if (oh < 0 || oh >= 9 || ow < 0 || ow >= 9) return zero4();
+    const bool ok = row < M && oh >= 0 && oh < 9 && ow >= 0 && ow < 9;
     (void)z;
-    return ld4(dz2 + ((size_t)(b * 9 + oh) * 9 + ow) * 64 + oc0 + k);
+    return ld4m(dz2 + (ok ? ((size_t)(b * 9 + oh) * 9 + ow) * 64 + oc0 + k : 0), ok);
   }
   __device__ f32x4 ldB(int z, int s, int col, int k) const {   // W1[kh][kw][c = col][oc]
     const int t = s >> 1, kh = (z >> 1) + 2 * (t >> 1), kw = (z & 1) + 2 * (t & 1);
@@ -710,16 +726,17 @@ struct PConvWgrad {
   }
   __host__ __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
-    const int r = s * BK + k;
-    if (r >= rows_in(z)) return zero4();
+    const int r0 = s * BK + k;
+    const bool ok = r0 < rows_in(z);
+    const int r = ok ? r0 : 0;
     const int tap = row / C, c = row - tap * C, kh = tap / KS, kw = tap - kh * KS;
     const int bl = r / P, p = r - bl * P, oh = p / OW, ow = p - oh * OW, b = z * SC + bl;
-    return ld4(in + ((size_t)(b * H + oh * S + kh) * W + ow * S + kw) * C + c);
+    return ld4m(in + ((size_t)(b * H + oh * S + kh) * W + ow * S + kw) * C + c, ok);
   }
   __device__ f32x4 ldB(int z, int s, int col, int k) const {
     const int r = s * BK + k;
-    if (r >= rows_in(z)) return zero4();
-    return ld4(dz + ((size_t)z * SC * P + r) * OC + col);
+    const bool ok = r < rows_in(z);
+    return ld4m(dz + ((size_t)z * SC * P + (ok ? r : 0)) * OC + col, ok);
   }
   __device__ void epi(int z, int row, int col, f32x4 v) const {
 #pragma unroll
@@ -807,6 +824,19 @@ constexpr int kC1SlotDw = 1776;                 // 84 rows x 21 dwords + 12 (ban
 constexpr int kC1Frames = 4 * kC1SlotDw * 4;    // 28,416 B of one sample's frames in LDS
 constexpr int kC1Chunks = 4 * kFramePix / 16;   // 1,764 s2d uint4 chunks in HBM
 
+// 16 bytes (s2d chunk pos) of a frame from the table; a null entry reads the zero frame.  The load is a global load
+// issued on every path: a load through a generic pointer compiles to a flat load, which also counts on lgkmcnt, so
+// every LDS wait of the MFMA loop would wait for the next sample's frames too (and a branch around it makes the vmcnt
+// bookkeeping conservative)
+typedef const __attribute__((address_space(1))) uint8_t gbyte;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4v gu4;
+__device__ __forceinline__ uint4 ldg_frame(const uint8_t* f, int pos) {
+  gbyte* p = f ? (gbyte*)f + pos * 16 : (gbyte*)q32_zero4;   // the byte pointer is cast first, so the load is global
+  const u32x4v v = *(gu4*)p;
+  return uint4{v.x, v.y, v.z, v.w};
+}
+
 // next sample's frames into registers (null table entry = the zero frame)
 __device__ __forceinline__ void c1_prefetch(const uint8_t* const* table, int b, uint4 (&pf)[7]) {
 #pragma unroll
@@ -815,8 +845,7 @@ __device__ __forceinline__ void c1_prefetch(const uint8_t* const* table, int b, 
     pf[j] = uint4{0, 0, 0, 0};
     if (q < kC1Chunks) {
       const int slot = q / 441, pos = q - slot * 441;
-      const uint8_t* f = table[b * 4 + slot];
-      if (f) pf[j] = *reinterpret_cast<const uint4*>(f + pos * 16);
+      pf[j] = ldg_frame(table[b * 4 + slot], pos);
     }
   }
 }
@@ -934,8 +963,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
       pf[j] = uint4{0, 0, 0, 0};
       if (q < kC1Chunks) {
         const int slot = q / 441, pos = q - slot * 441;
-        const uint8_t* f = table[b * 4 + slot];
-        if (f) pf[j] = *reinterpret_cast<const uint4*>(f + pos * 16);
+        pf[j] = ldg_frame(table[b * 4 + slot], pos);
       } else if (q < kC1Chunks + kC1DzChunks) {
         const int e = q - kC1Chunks, r = e >> 2, part = e & 3;
         pf[j] = *reinterpret_cast<const uint4*>(dz1 + ((size_t)b * 400 + r) * 32 + hh * 16 + part * 4);
