@@ -837,16 +837,35 @@ __device__ __forceinline__ uint4 ldg_frame(const uint8_t* f, int pos) {
   return uint4{v.x, v.y, v.z, v.w};
 }
 
-// next sample's frames into registers (null table entry = the zero frame)
-__device__ __forceinline__ void c1_prefetch(const uint8_t* const* table, int b, uint4 (&pf)[7]) {
+// The four frame pointers of sample b (b uniform across the block).  Read through the constant address space, so they
+// are scalar loads: a vector load of a per-lane table entry makes every frame load wait for it with vmcnt(0), i.e. for
+// every store and load still in flight (a whole sample's a1 stores in the forward), and serialises the prefetch branches
+// behind one memory round trip each.
+typedef const __attribute__((address_space(4))) unsigned long long cu64;
+struct C1Ptrs {
+  const uint8_t* p[4];
+};
+__device__ __forceinline__ C1Ptrs c1_ptrs(const uint8_t* const* table, int b) {
+  cu64* t = (cu64*)(table + (size_t)b * 4);
+  return C1Ptrs{{(const uint8_t*)t[0], (const uint8_t*)t[1], (const uint8_t*)t[2], (const uint8_t*)t[3]}};
+}
+// (two levels of selects, so the per-lane choice stays v_cndmask and not a branch)
+__device__ __forceinline__ const uint8_t* c1_slot(const C1Ptrs& f, int slot) {
+  const uint8_t* lo = (slot & 1) ? f.p[1] : f.p[0];
+  const uint8_t* hi = (slot & 1) ? f.p[3] : f.p[2];
+  return (slot & 2) ? hi : lo;
+}
+
+// next sample's frames into registers (null table entry = the zero frame).  Every lane issues its loads (lanes past the
+// frames read the zero page) with no branch around them: a load in a divergent branch makes the compiler wait for all
+// loads in flight (vmcnt(0)) before the other path may reuse its registers.
+__device__ __forceinline__ void c1_prefetch(const C1Ptrs& f, uint4 (&pf)[7]) {
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     const int q = threadIdx.x + 256 * j;
-    pf[j] = uint4{0, 0, 0, 0};
-    if (q < kC1Chunks) {
-      const int slot = q / 441, pos = q - slot * 441;
-      pf[j] = ldg_frame(table[b * 4 + slot], pos);
-    }
+    const bool ok = q < kC1Chunks;
+    const int qq = ok ? q : 0, slot = qq / 441, pos = qq - slot * 441;
+    pf[j] = ldg_frame(ok ? c1_slot(f, slot) : nullptr, pos);
   }
 }
 // s2d chunk (slot, block row bx, block column by) = pixels x = 4 bx + xl, y = 4 by .. 4 by + 3 in component xl
@@ -898,13 +917,18 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
   int b = blockIdx.x;
   if (b >= B) return;
   uint4 pf[7];
-  c1_prefetch(table, b, pf);
+  c1_prefetch(c1_ptrs(table, b), pf);
+  // frame pointers one sample ahead of the frames (scalar registers)
+  C1Ptrs nxt = c1_ptrs(table, b + (int)gridDim.x < B ? b + (int)gridDim.x : b);
   c1_stage(c1w, pf);
   __syncthreads();
   for (int it = 0; b < B; b += gridDim.x, ++it) {
     const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
     const int nb = b + gridDim.x;
-    if (nb < B) c1_prefetch(table, nb, pf);
+    if (nb < B) {
+      c1_prefetch(nxt, pf);
+      nxt = c1_ptrs(table, nb + (int)gridDim.x < B ? nb + (int)gridDim.x : nb);
+    }
     f32x4 acc[13];
 #pragma unroll
     for (int j = 0; j < 13; ++j) acc[j] = zero4();
@@ -957,17 +981,20 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
   const int ao = (l15 & 3) * kC1SlotDw + (2 * wave + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
   uint4 pf[14];
   auto prefetch = [&](int b) {
+    const C1Ptrs f = c1_ptrs(table, b);
+    const uint64_t zp = (uint64_t)(gbyte*)q32_zero4;
+    const uint64_t dzb = (uint64_t)(dz1 + (size_t)b * 400 * 32 + hh * 16);
 #pragma unroll
-    for (int j = 0; j < 14; ++j) {
+    for (int j = 0; j < 14; ++j) {   // one unconditional 16-byte load per j: a frame chunk, a dz1 chunk or the zero page
       const int q = tid + 256 * j;
-      pf[j] = uint4{0, 0, 0, 0};
-      if (q < kC1Chunks) {
-        const int slot = q / 441, pos = q - slot * 441;
-        pf[j] = ldg_frame(table[b * 4 + slot], pos);
-      } else if (q < kC1Chunks + kC1DzChunks) {
-        const int e = q - kC1Chunks, r = e >> 2, part = e & 3;
-        pf[j] = *reinterpret_cast<const uint4*>(dz1 + ((size_t)b * 400 + r) * 32 + hh * 16 + part * 4);
-      }
+      const bool isf = q < kC1Chunks, isd = !isf && q < kC1Chunks + kC1DzChunks;
+      const int qf = isf ? q : 0, slot = qf / 441, pos = qf - slot * 441;
+      const int e = isd ? q - kC1Chunks : 0, r = e >> 2, part = e & 3;
+      const uint64_t fp = (uint64_t)c1_slot(f, slot);
+      const uint64_t fa = fp ? fp + (uint64_t)(pos * 16) : zp;
+      const uint64_t da = dzb + (uint64_t)((r * 32 + part * 4) * 4);
+      const u32x4v v = *(gu4*)(isf ? fa : (isd ? da : zp));
+      pf[j] = uint4{v.x, v.y, v.z, v.w};
     }
   };
   auto stage = [&]() {

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "qnet32_kernels.h"
@@ -315,6 +316,7 @@ static void gen(int M, int N, int K, const float* A, const float* B, float* C) {
 }
 
 int main(int argc, char** argv) {
+  const bool only_c1 = argc > 1 && std::string(argv[1]) == "conv1";   // just the two conv1 kernels
   const int Bs[2] = {1024, 8192};
   // layer buffers sized for the larger batch
   const int Bmax = 8192;
@@ -352,6 +354,7 @@ int main(int argc, char** argv) {
       printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_fwd (k_conv1_fwd32)", G, 2 * kC1Frames, us, f / us / 1e6,
              f / us / 1e6 / 157.3 * 100);
     }
+    if (!only_c1) {
     run1("conv2_fwd", PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>{grid(B * 81, 64, 64, 64, 1), a1, W1, W1, a2, B * 81},
          2.0 * B * 81 * 64 * 512);
     run1("conv3_fwd", PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>{grid(B * 49, 64, 64, 64, 1), a2, W2, W2, a3, B * 49},
@@ -388,6 +391,7 @@ int main(int argc, char** argv) {
     run1("conv2_dgrad", PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, W1, a1, dz1, B * 100}, 2.0 * B * 81 * 64 * 512);
     run1("conv2_wgrad", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, B / 16), a1, dz2, slab, B},
          2.0 * B * 81 * 64 * 512);
+    }
     {
       const int nz = B / 4, lds = kC1Frames + 400 * 16 * 4;
       CK(hipFuncSetAttribute((const void*)k_conv1_wgrad32, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -397,6 +401,7 @@ int main(int argc, char** argv) {
              f / us / 1e6, f / us / 1e6 / 157.3 * 100);
     }
   }
+  if (only_c1) return 0;
   printf("--- tile variants, B = 1024\n");
   {
     const int B = 1024;
