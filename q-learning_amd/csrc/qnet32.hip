@@ -421,7 +421,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
              2.0 * n * 81 * 64 * 512, s);
       launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd_big",
              2.0 * n * 49 * 64 * 576, s);
-      launch(m, PFc1Fwd{grid(n, 32, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
+      launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
              2.0 * n * 3136 * 512, s);
     } else {
       launch(m, PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, "f32_conv2_fwd",
@@ -486,7 +486,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
-    PConv2DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
+    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }

@@ -418,6 +418,8 @@ struct PFc1FwdT {
   }
 };
 using PFc1Fwd = PFc1FwdT<>;
+// chunk-size batches: 64 x 64 tiles on v_mfma_f32_32x32x2_f32 (scripts/ubench32.hip at B = 8192: 231 vs 247 us)
+using PFc1FwdB = PFc1FwdT<64, 64, 2, 2, 32>;
 using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n

@@ -98,6 +98,7 @@ int main(int argc, char** argv) {
   replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
   replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
   replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
+  replay(PFc1FwdB{grid(n, 64, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd B");
   replay(PConv2FwdS{grid(n * 81, 64, 64, 32, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd S");
   replay(PConv3FwdS{grid(n * 49, 64, 64, 32, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd S");
   replay(PFc1FwdS{grid(n, 32, 512, 32, 1), a3, w3, b3, a4, n}, "fc1_fwd S");
@@ -120,6 +121,7 @@ int main(int argc, char** argv) {
   replay(PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad");
   replay(PConv2DgradS{grid(B * 100, 64, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad S");
   replay(PConv2DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px");
+  replay(PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px 64");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
   printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
   return 0;
