@@ -27,7 +27,17 @@ constexpr int BK = 32;   // reduction depth staged per LDS slab
 // Operand tile in LDS for MFMA shape MF (16: v_mfma_f32_16x16x4_f32, 32: v_mfma_f32_32x32x2_f32).  RMAJ: t[row][k]
 // (pitch BK + 4); KMAJ: t[k][row] (pitch = rows padded to MF mod 64, so the MF rows x (64 / MF) k of a fragment read
 // hit distinct banks).  Writes are 16-byte float4 along the operand's contiguous source dimension.
-__host__ __device__ constexpr int kmaj_pitch(int rows, int mf) { return rows + (((mf - rows % 64) % 64) + 64) % 64; }
+// MF 16: the four lane groups of a fragment read k rows 0..3 of the image, i.e. offsets 0, p, 2p, 3p: any p = 16 or
+// 48 mod 64 puts them on four disjoint 16-bank ranges; the smallest such p >= rows (32 rows: 48, not 80, which lets
+// one more block per CU fit).  MF 32: two lane groups, p = 32 mod 64.
+__host__ __device__ constexpr int kmaj_pitch_min(int rows, int mf) { return rows + (((mf - rows % 64) % 64) + 64) % 64; }
+__host__ __device__ constexpr int kmaj_pitch(int rows, int mf) {
+  return mf == 16 && rows + ((48 - rows % 64) % 64 + 64) % 64 < kmaj_pitch_min(rows, mf)
+             ? rows + ((48 - rows % 64) % 64 + 64) % 64
+             : kmaj_pitch_min(rows, mf);
+}
+static_assert(kmaj_pitch(32, 16) == 48 && kmaj_pitch(64, 16) == 80 && kmaj_pitch(128, 16) == 144 && kmaj_pitch(64, 32) == 96,
+              "KMAJ pitches");
 
 template <int ROWS, bool KMAJ, int MF = 16>
 struct Opnd {
@@ -750,12 +760,12 @@ struct PConvWgrad {
 // dW4[k][n] = fmaf chain over b of a4[b][k] dq[b][n]; db4[n] = sum over b of dq[b][n]; loss = (sum over b of h_b) / B.
 // Leading blocks of the fc1 backward launch (independent of its GEMM tiles), block t = one 16-row tile of the GEMM
 // [a4^T ; 1] [dq | h] on v_mfma_f32_16x16x4_f32 (b on the lane groups, so each output is the b-ordered chain; the
-// all-ones row 512 gives db4 and the loss sum, fmaf(1, v, s) = s + v).  Per 512 samples the block's four waves load
-// the tile's a4 columns and [dq | h] into LDS with every load in flight at once (40 KB, the GEMM tiles' own LDS size),
+// all-ones row 512 gives db4 and the loss sum, fmaf(1, v, s) = s + v).  Per HB samples the block's four waves load
+// the tile's a4 columns and [dq | h] into LDS with every load in flight at once (40 KB),
 // then wave 0 runs the chain from LDS: two memory latencies per launch instead of one per few MFMAs.
 struct SideFc2 {
   static constexpr int BLOCKS = 33;   // 512 rows of a4^T + the ones row
-  static constexpr int HB = 512;      // samples per LDS pass
+  static constexpr int HB = 512;      // samples per LDS pass (40 KB; 256 measured slower: 73.4 vs 71.2 us per fc1 backward)
   static constexpr size_t LDS = (size_t)HB * 20 * sizeof(float);
   const float* a4;
   const uint8_t* act;
@@ -774,7 +784,7 @@ struct SideFc2 {
       __syncthreads();   // the previous pass's LDS reads are done
       if (t < 32) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {   // 2,048 float4: row bl = q / 4, quarter q % 4
+        for (int j = 0; j < HB * 4 / 256; ++j) {   // HB x 4 float4: row bl = q / 4, quarter q % 4
           const int q = tid + 256 * j, bl = q >> 2, b = b0 + bl;
           f32x4 v = zero4();
           if (b < B) v = ld4(a4 + (size_t)b * 512 + t * 16 + (q & 3) * 4);
@@ -782,7 +792,7 @@ struct SideFc2 {
         }
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < HB / 256; ++j) {
         const int bl = tid + 256 * j, b = b0 + bl;
         f32x4 v = zero4();
         if (b < B) {
