@@ -111,6 +111,15 @@ __device__ __forceinline__ int xcd_logical(int b, int G) {
   return x * q + (x < r ? x : r) + i;
 }
 
+// Scheduling strategy of a policy's slab loop: IGLP = n >= 0 asks the compiler for its MFMA / LDS interleave strategy n
+// (__builtin_amdgcn_iglp_opt), -1 leaves the default scheduler.  Default 1: measured in place at C3 (profiles/r02_v6),
+// conv2 / conv3 forward 61.5 / 46.1 -> 58.0 / 43.7 us, the fc1 / conv2 backward pairs 73.3 / 117.1 -> 69.5 / 112.9 us,
+// the chunk-size conv3 forward 281.5 -> 272 us; the fc1 forward runs slower with it (PFc1FwdT sets -1).
+template <class P, class = void>
+struct IglpOf : std::integral_constant<int, 1> {};
+template <class P>
+struct IglpOf<P, std::void_t<decltype(P::IGLP)>> : std::integral_constant<int, P::IGLP> {};
+
 // Optional per-tile A-operand context: a policy with a member type ACtx provides
 //   ACtx a_ctx(int z, int row0, int tid) const                       once per tile, per thread (e.g. the frame pointers of its rows)
 //   f32x4 ldA_c(const ACtx&, int i, int z, int s, int row, int k) const    instead of ldA (i = the thread's load index)
@@ -223,6 +232,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   auto compute = [&](int s) {
     const float* a = (s & 1) ? As1 : As0;
     const float* b = (s & 1) ? Bs1 : Bs0;
+    if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
 #pragma unroll
     for (int kk = 0; kk < BK / OA::KG; ++kk) {
       float af[TM], bf[TN];
@@ -408,6 +418,7 @@ using PConv3FwdS = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1FwdT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  static constexpr int IGLP = -1;   // default scheduler (iglp_opt(1): 40.4 -> 42.2 us at B = 1024, 236 -> 248 us at 8,192)
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* a3;

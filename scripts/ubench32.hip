@@ -401,7 +401,7 @@ int main(int argc, char** argv) {
              f / us / 1e6, f / us / 1e6 / 157.3 * 100);
     }
   }
-  if (only_c1) return 0;
+  if (only_c1 || (argc > 1 && std::string(argv[1]) == "layers")) return 0;   // "layers": just the per-layer list above
   printf("--- tile variants, B = 1024\n");
   {
     const int B = 1024;
