@@ -114,7 +114,8 @@ __device__ __forceinline__ int xcd_logical(int b, int G) {
 // Scheduling strategy of a policy's slab loop: IGLP = n >= 0 asks the compiler for its MFMA / LDS interleave strategy n
 // (__builtin_amdgcn_iglp_opt), -1 leaves the default scheduler.  Default 1: measured in place at C3 (profiles/r02_v6),
 // conv2 / conv3 forward 61.5 / 46.1 -> 58.0 / 43.7 us, the fc1 / conv2 backward pairs 73.3 / 117.1 -> 69.5 / 112.9 us,
-// the chunk-size conv3 forward 281.5 -> 272 us; the fc1 forward runs slower with it (PFc1FwdT sets -1).
+// the chunk-size conv3 forward 281.5 -> 272 us (strategy 0 for all: 1-4 % slower than 1 on these); the fc1 forward runs
+// slower with strategy 1 and best with 0 (PFc1FwdT); the conv1 kernels' MFMA loops gain nothing from either.
 template <class P, class = void>
 struct IglpOf : std::integral_constant<int, 1> {};
 template <class P>
@@ -418,7 +419,7 @@ using PConv3FwdS = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1FwdT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
-  static constexpr int IGLP = -1;   // default scheduler (iglp_opt(1): 40.4 -> 42.2 us at B = 1024, 236 -> 248 us at 8,192)
+  static constexpr int IGLP = 0;   // strategy 0 (default scheduler 40.4 / 236 us, strategy 1 42.2 / 248 us, 0 39.8 / 230 us at B = 1024 / 8,192)
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* a3;
