@@ -121,6 +121,14 @@ struct IglpOf : std::integral_constant<int, 1> {};
 template <class P>
 struct IglpOf<P, std::void_t<decltype(P::IGLP)>> : std::integral_constant<int, P::IGLP> {};
 
+// LOAD_FENCE = false: no scheduling barrier between a slab's global loads and its MFMAs (the scheduler may sink the
+// loads); measured per layer with iglp_opt in place: the fc1 forward 39.8 -> 38.3 us, the chunk-size conv2 forward 404 ->
+// 389 us, the conv3 backward pair 98.8 -> 97.7 us without it; every other layer 2-5 % slower without it.
+template <class P, class = void>
+struct LoadFenceOf : std::true_type {};
+template <class P>
+struct LoadFenceOf<P, std::void_t<decltype(P::LOAD_FENCE)>> : std::integral_constant<bool, P::LOAD_FENCE> {};
+
 // Optional per-tile A-operand context: a policy with a member type ACtx provides
 //   ACtx a_ctx(int z, int row0, int tid) const                       once per tile, per thread (e.g. the frame pointers of its rows)
 //   f32x4 ldA_c(const ACtx&, int i, int z, int s, int row, int k) const    instead of ldA (i = the thread's load index)
@@ -258,7 +266,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   // for slab s + 1's loads (vmcnt = this iteration's NA + NB), never for slab s + 2's (see ld4m)
   auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
     load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
-    __builtin_amdgcn_sched_barrier(0);   // the loads stay ahead of the slab's MFMAs (the scheduler would sink them)
+    if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);   // the loads stay ahead of the slab's MFMAs
     compute(s);
     if (s + 1 < ns) store(s + 1, xa, xb);
     lds_barrier();
@@ -386,6 +394,7 @@ template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 
           int MF_ = 16>
 struct PConvFwd {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  static constexpr bool LOAD_FENCE = !(H == 20 && BN_ == 64);   // the chunk-size conv2 forward runs without it
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* in;
@@ -419,6 +428,7 @@ using PConv3FwdS = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1FwdT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  static constexpr bool LOAD_FENCE = false;
   static constexpr int IGLP = 0;   // strategy 0 (default scheduler 40.4 / 236 us, strategy 1 42.2 / 248 us, 0 39.8 / 230 us at B = 1024 / 8,192)
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
@@ -554,6 +564,7 @@ __host__ __device__ inline int px2_order(int z) { return z < 8 ? z + 1 : (z == 8
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2>
 struct PConv3DgradPx {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool LOAD_FENCE = false;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false, RAW_ORDER = true;
   Grid g;             // {ceil(B / BM), 64 / BN, 81}
   const float* dz3;   // [B][7][7][64]
