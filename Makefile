@@ -36,11 +36,11 @@ $(OUT)/obj/replay.o: $(SRC)/replay.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OUT)/obj/qnet.o: $(SRC)/qnet.hip $(HDRS) | $(OUT)/obj
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(Q32SCHED) -c $< -o $@
 
 # fp32 Q-net: bit-exact against the oracle, so no contraction anywhere (every fma is an explicit fmaf / MFMA)
-# fp32 Q-net: the backend's max-ILP scheduling strategy (measured at C3: 195.5K -> 196.2K env-steps/s, every GEMM layer
-# equal or faster; max-memory-clause: 191.0K)
+# Q-net objects: the backend's max-ILP scheduling strategy (measured at C3: fp32 195.5K -> 196.2K env-steps/s, every GEMM
+# layer equal or faster; max-memory-clause 191.0K, iterative-ilp 196.6K; bf16 745.7K -> 749.3K)
 Q32SCHED := -mllvm --amdgpu-sched-strategy=max-ilp
 
 $(OUT)/obj/qnet32.o: $(SRC)/qnet32.hip $(HDRS) | $(OUT)/obj
