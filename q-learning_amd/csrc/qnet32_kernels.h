@@ -112,7 +112,7 @@ __device__ __forceinline__ int xcd_logical(int b, int G) {
 }
 
 // Scheduling strategy of a policy's slab loop: IGLP = n >= 0 asks the compiler for its MFMA / LDS interleave strategy n
-// (__builtin_amdgcn_iglp_opt), -1 leaves the default scheduler.  Default 1: measured in place at C3 (profiles/r02_v6),
+// (__builtin_amdgcn_iglp_opt), -1 leaves the default scheduler.  Default 1: measured in place at C3 (profiles/r02_v6 README),
 // conv2 / conv3 forward 61.5 / 46.1 -> 58.0 / 43.7 us, the fc1 / conv2 backward pairs 73.3 / 117.1 -> 69.5 / 112.9 us,
 // the chunk-size conv3 forward 281.5 -> 272 us (strategy 0 for all: 1-4 % slower than 1 on these); the fc1 forward runs
 // slower with strategy 1 and best with 0 (PFc1FwdT); the conv1 kernels' MFMA loops gain nothing from either.
