@@ -5,7 +5,9 @@
 // (create_ql_model_breakout_84x84x4_3_32.py:20-33,37-61; tf.float32 TensorSpecs) run by TF 2.12, whose reduction
 // order is internal to its CPU kernels and pinned by no reference test: the order is therefore part of
 // this build's definition of the arithmetic, stated here once and followed by the GPU kernels
-// (q-learning_amd/csrc/qnet32_kernels.h).  tests/test_oracle_qnet.py pins this restatement against float64 torch.
+// (q-learning_amd/csrc/qnet32_kernels.h).  tests/test_oracle_qnet32_pin.py pins this restatement against float64 torch
+// autograd of the Keras graph (activations, Q, loss, all ten gradients, norms, w / m / v after two Adam steps; B 4..256)
+// and against the double-accumulating restatement qnet_ref.cpp at B = 1024.
 //   conv1 .. conv3  z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
 //   dense 3136->512 z = sum over k ascending (Flatten order h, w, c)
 //   dense 512->3    z = ((C0 + C1) + C2) + C3, Cw = chain over k in [128 w, 128 w + 128) ascending

@@ -5,7 +5,8 @@ v_mfma_f32_16x16x4_f32, which is a k-ordered fmaf chain (scripts/mfma_f32_probe.
 accumulator per output over the whole reduction; oracle/qnet32_ref.cpp restates the same chains on the CPU
 (DESIGN.md §6 fixes every order).  So forward activations, Q values, the loss, all ten raw gradients, the clip_by_norm
 norms and the post-Adam weights / Adam slots must be equal bit for bit, at every batch size, for any number of
-consecutive steps.  tests/test_oracle_qnet.py pins the oracle itself against float64 torch (tolerance 1e-5).
+consecutive steps.  tests/test_oracle_qnet32_pin.py pins that oracle (qnet32_ref.cpp) against float64 torch autograd:
+activations / Q / loss 1e-5, gradients 1e-4, norms, and w / m / v after two Adam steps.
 """
 import ctypes
 
