@@ -12,8 +12,12 @@ forward, online forward, Huber, backward, [RCCL all-reduce], clip_by_norm + Adam
 Default workload (N = 1): config C3 of SURVEY.md §8(d) - 8,192 envs per GPU, replay 1,000,000 in HBM, B = 1024,
 fp32 Q-net (the reference's arithmetic).  Steady state regardless of --warmup: before anything is timed the replay
 is prefilled to capacity, which also runs the loop past the 50k-step pure-random phase, so the timed vector steps
-include the greedy acting forward, brick contacts and episode ends.  Then W untimed training vector steps, then K
-timed ones.  The bf16 fast path (labelled, not the headline) is measured beside it on the same workload.
+include the greedy acting forward, brick contacts and episode ends; then it keeps stepping (no updates) until episode
+ends are spread over the steps as in a long run (all envs launch together, so their first episodes end in waves): at
+least 3 finished episodes per env, then one mean episode length of vector steps each within +-50 % of the expected
+n_envs / mean-length episode ends.  Then W untimed training vector steps, then K timed ones (asserted to contain
+episode ends).  Beside the headline, measured in the same run: the same loop with the frozen target net evaluated per
+sampled batch as the reference does (value_no_target_memo), and the bf16 fast path (labelled, not the headline).
 
 Multi-GPU: with --gpus N > 1 and no WORLD_SIZE in the environment, this process starts
 `torch.distributed.run --nproc-per-node N` on itself before touching the GPU and exits with its code; each rank owns
@@ -34,7 +38,9 @@ sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md: f32-input MFMA, bf16)
-STEADY_RUN, MAX_DESYNC = 24, 4000                # steady state before timing: see Run._desync
+# steady state before timing (Run._steady): at least STEADY_EPISODES finished episodes per env on average, then a window
+# of one mean episode length in which every vector step's episode-end count is within +-STEADY_TOL of n_envs / mean length
+STEADY_EPISODES, STEADY_TOL, MAX_STEADY = 3.0, 0.5, 4000
 PEAK_HBM_GBS = 8000.0                            # HBM3E
 # per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
 FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
@@ -67,6 +73,9 @@ def parse():
     ap.add_argument("--replay", type=int, default=1_000_000, help="replay capacity per GPU (C3: 1M; C2: 100k)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32", help="headline Q-net arithmetic")
     ap.add_argument("--beside-steps", type=int, default=5, help="timed vector steps of the other precision (0 = skip)")
+    ap.add_argument("--nomemo-steps", type=int, default=5,
+                    help="timed vector steps of the headline precision with the target net evaluated per sampled batch "
+                         "(QLX_TARGET_CACHE=0, the reference's work; 0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=10_000, help="env-steps of the CPU baseline (C1: 10,000; 0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=1)
     ap.add_argument("--double-dqn", action="store_true", help="extension (config C5): double-DQN targets")
@@ -214,10 +223,9 @@ class Run:
             prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
             log(f"{precision}: prefill {prefill} vector steps")
             L.prefill(prefill)
-            # ... and episode ends spread over the steps: all envs launch together, so their first episodes end
-            # together (the first ball loss comes ~160 env-steps after launch); keep stepping (no updates) until
-            # episodes ended in each of the last STEADY_RUN vector steps, as they do in a long run
-            prefill += self._desync(L, p)
+            # ... and episode ends spread over the steps as in a long run (all envs launch together, so their first
+            # episodes end together)
+            prefill += self._steady(L)
             L.run(max(warmup, 1))
             L.sync()
             s = L.stats()
@@ -232,18 +240,32 @@ class Run:
         finally:
             L.close()
 
-    def _desync(self, L, p):
-        # the stop decision is global (min over ranks): every rank must run the same number of vector steps, since each
-        # one carries collectives (the episode-statistics all-reduce)
-        run, n, last = 0, 0, L.stats()["episode_count"]
-        while run < STEADY_RUN and n < MAX_DESYNC:
+    def _steady(self, L):
+        """Vector steps without updates until the episode ends are no longer in waves: at least STEADY_EPISODES finished
+        episodes per env on average, then a window of one mean episode length (in vector steps) in which every step's
+        episode-end count is within STEADY_TOL of the expected n_envs / mean length.  The decision is global (every rank
+        runs the same number of vector steps: each one carries collectives)."""
+        N, ctl = self.args.envs, self.ctl
+        s = L.stats()
+        last, steps0 = s["episode_count"], s["step_count"]
+        ends, n = [], 0
+        while n < MAX_STEADY:
             L.prefill(1)
             n += 1
-            e = L.stats()["episode_count"]
-            ended = self.ctl.min(1.0 if e > last else 0.0)
-            run = run + 1 if ended > 0 else 0
-            last = e
-        log(f"{self.precision}: {n} more vector steps until episodes end every step ({run} in a row)")
+            s = L.stats()
+            ends.append(s["episode_count"] - last)
+            last = s["episode_count"]
+            tot = ctl.sum(float(last))
+            mean_len = ctl.sum(float(s["step_count"])) / max(tot, 1.0)   # env-steps per finished episode = vector steps
+            expect = N / mean_len
+            win = int(mean_len + 0.999)
+            ok = tot >= STEADY_EPISODES * N * ctl.world and len(ends) >= win and \
+                all(abs(e - expect) <= STEADY_TOL * expect for e in ends[-win:])
+            if ctl.min(1.0 if ok else 0.0) > 0:
+                break
+        self.mean_len, self.expect_ends = mean_len, expect
+        log(f"{self.precision}: {n} more vector steps to steady episode ends (mean episode {mean_len:.1f} env-steps, "
+            f"{expect:.1f} ends expected per vector step, last window min/max {min(ends[-win:])}/{max(ends[-win:])})")
         return n
 
     def _profile(self):
@@ -282,6 +304,7 @@ class Run:
         self.env_steps = self.args.envs * steps * ctl.world
         self.updates = s1["update_count"] - s0["update_count"]
         self.episodes = int(ctl.sum(s1["episode_count"] - s0["episode_count"]))
+        self.ends_per_step = self.episodes / max(steps, 1)
         self.episodes_total = int(ctl.sum(s1["episode_count"]))
         self.last_loss = s1["last_loss"]
         self.running_reward = s1["running_reward"]
@@ -381,11 +404,24 @@ def main():
     import qlx
     flags = (qlx.DOUBLE_DQN if args.double_dqn else 0) | (qlx.PER if args.per else 0)
     head = Run(args, ctl, args.precision, args.steps, args.warmup, flags)
+    nomemo = None
+    if args.nomemo_steps > 0 and "target_memo" in head.comps:
+        # the reference's per-batch target work (same values, tests/test_gpu_learner.py), measured in this run
+        prev = os.environ.get("QLX_TARGET_CACHE")
+        os.environ["QLX_TARGET_CACHE"] = "0"
+        try:
+            nomemo = Run(args, ctl, args.precision, args.nomemo_steps, 1, flags)
+        finally:
+            if prev is None:
+                del os.environ["QLX_TARGET_CACHE"]
+            else:
+                os.environ["QLX_TARGET_CACHE"] = prev
+        assert "target_memo" not in nomemo.comps
     other = "bf16" if args.precision == "fp32" else "fp32"
     beside = Run(args, ctl, other, args.beside_steps, 1, flags) if args.beside_steps > 0 else None
     # the measured window is the steady-state loop: greedy acting and episode ends inside it
     assert "act_forward" in head.comps, "acting forward missing from the measured loop"
-    assert head.episodes_total > 0, "no episode ended"
+    assert head.episodes > 0, "no episode ended inside the timed window"
     if ctl.rank != 0:
         return
     N, B = args.envs, args.batch
@@ -423,16 +459,31 @@ def main():
         "roofline": head.roofline(),
         **head.report(),
         "steady_state": {"prefill_vector_steps": head.prefill, "episodes_in_window": head.episodes,
+                         "episode_ends_per_step": round(head.ends_per_step, 2),
+                         "expected_ends_per_step": round(head.expect_ends * ctl.world, 2),
+                         "mean_episode_env_steps": round(head.mean_len, 1),
                          "episodes_total": head.episodes_total, "epsilon": round(head.epsilon, 4),
                          "running_reward": head.running_reward, "last_loss": head.last_loss},
         "components_event_timed": comps,
     }
+    if nomemo is not None:
+        line["value_no_target_memo"] = round(nomemo.value(), 1)
+        line["no_target_memo"] = {
+            "value": round(nomemo.value(), 1), "unit": "env-steps/s", "steps": nomemo.steps,
+            "ms_per_step": round(nomemo.dt / nomemo.steps * 1e3, 3), "episodes_in_window": nomemo.episodes,
+            "grad_updates_per_sec": round(nomemo.updates / nomemo.dt, 2),
+            "note": "same loop and precision with the frozen target net evaluated per sampled batch (U*B target forwards "
+                    "per vector step, the reference's work: self_driving_tf_q_learner.rs:189-199) instead of once per "
+                    "transition at insertion; identical targets (tests/test_gpu_learner.py)"}
     if beside is not None:
         line[f"{other}_beside"] = {
             "value": round(beside.value(), 1), "unit": "env-steps/s", "steps": beside.steps,
             "ms_per_step": round(beside.dt / beside.steps * 1e3, 3),
             "grad_updates_per_sec": round(beside.updates / beside.dt, 2), "roofline": beside.roofline(),
-            "note": "bf16 MFMA operands: the labelled fast path, not the reference's arithmetic" if other == "bf16"
+            "note": "bf16 MFMA operands, fp32 accumulation and master weights: the labelled fast path, not the reference's "
+                    "arithmetic; its tolerance contract vs the fp32 oracle (DESIGN.md §6, tests/test_gpu_qnet_bf16.py): Q "
+                    "and activations <= 3e-2 max|ref|, loss <= 3e-2 relative, per-variable gradients relative L2 <= 0.15 "
+                    "with cosine >= 0.99" if other == "bf16"
             else "fp32: the reference's arithmetic"}
     if ctl.world == 1:
         log(f"cpu baseline: {args.cpu_sample} env-steps")

@@ -181,6 +181,8 @@ typedef struct qlx_params { /* Parameter (self_driving_tf_q_learner.rs:20-67) + 
   uint32_t qnet_precision;     /* QLX_PREC_F32 (0, the reference's arithmetic) or QLX_PREC_BF16 */
   uint64_t stats_after_steps;  /* every this many env-steps: checkpoint + learning_update_log (0 = never) */
   char checkpoint_file[256];   /* write_checkpoint target of those events and of solved() (empty = not written) */
+  float episode_reward_goal;   /* goal solved() tests (Environment::episode_reward_goal_mean, prelude.rs); 0 = the env's
+                                  own (Breakout: bricks - 1, breakout_environment.rs:203-206); other values mock it */
 } qlx_params;
 
 #define QLX_PREC_F32 0u

@@ -198,16 +198,16 @@ __global__ void k_slot_put(ReplayView r, uint64_t i0, uint32_t n, const float* y
   if (b < n) ycache[(r.total - r.len + i0 + b) % r.cap] = y[b];
 }
 
-// this rank's contribution to the global solved() test: running reward, has-history flag, episode count, and the
-// minimum episode reward of its FIFO (+inf when empty, so the min over ranks ignores it)
-__global__ void k_book_local(const Book* book, const float* hist, uint32_t hist_cap, float* gsum, float* gmin) {
+// this rank's contribution to the global solved() test: running reward, has-history flag, episode count (f64: exact sums),
+// and the minimum episode reward of its FIFO (+inf when empty, so the min over ranks ignores it)
+__global__ void k_book_local(const Book* book, const float* hist, uint32_t hist_cap, double* gsum, float* gmin) {
   if (threadIdx.x != 0) return;
   const Book b = *book;
   float mn = __builtin_huge_valf();
   for (uint32_t i = 0; i < b.hist_len; ++i) mn = fminf(mn, hist[(b.hist_head + i) % hist_cap]);
-  gsum[0] = b.running_reward;
-  gsum[1] = b.hist_len > 0 ? 1.0f : 0.0f;
-  gsum[2] = (float)b.episode_count;
+  gsum[0] = (double)b.running_reward;
+  gsum[1] = b.hist_len > 0 ? 1.0 : 0.0;
+  gsum[2] = (double)b.episode_count;
   gmin[0] = mn;
 }
 
@@ -258,10 +258,13 @@ struct qlx_learner {
   bool dp_overlap = true;              // QLX_DP_OVERLAP=0: one whole-gradient all-reduce after the backward
   hipEvent_t ev_dense = nullptr, ev_reduced = nullptr;
   int world = 1, rank = 0;
-  // global solved() over ranks: per vector step, {sum running_reward, sum has_history, sum episodes} and {min episode
-  // reward} all-reduced on the learner stream (d_gsum[3], d_gmin[1])
-  float* d_gsum = nullptr;
+  // global solved() over ranks: per vector step, {sum running_reward, sum has_history, sum episodes} (f64) and {min
+  // episode reward} all-reduced on the learner stream (d_gsum[3], d_gmin[1])
+  double* d_gsum = nullptr;
   float* d_gmin = nullptr;
+  // pinned host copies read after every vector step (the solved() check): Book + the global sums
+  qlx::Book* h_book = nullptr;
+  double* h_gsum = nullptr;
   // QLX_TARGET_OVERLAP=1: the batched target pass after its first chunk runs on tgt_stream beside the update chain;
   // update u waits for the event of its chunk (fp32, no double DQN)
   bool tgt_overlap = false;
@@ -278,6 +281,7 @@ struct qlx_learner {
   float* d_ytmp = nullptr;             // [ychunk]
   uint32_t ychunk = 0;
   uint64_t ycache_version = 0;         // target->version the memo was computed with
+  uint32_t ycap = 0;                   // allocated chunk of d_ytab / d_yrew / d_ydone / d_ytmp (>= ychunk)
   qlx::Profiler prof;
   // statistics events (write_checkpoint + learning_update_log, self_driving_tf_q_learner.rs:204-212,226-230)
   uint64_t stats_events = 0;
@@ -318,12 +322,29 @@ static void learner_targets_range(qlx_learner* L, uint32_t u0, uint32_t nu, cons
 // read back at every sampling: bit-identical to the per-batch target pass, which at replay ratio 8 evaluates each
 // transition's s' eight times on average.  A write of the target weights from outside (model_pack: dist_init's
 // broadcast, the model API) invalidates the memo and the next push recomputes every live slot.
-static void ycache_fill(qlx_learner* L, uint64_t i0, uint64_t n) {
+// The per-step fill runs chunks of at most ychunk (= min(n_envs, kF32FwdChunk)) transitions; the rebuild of every live slot
+// after a target-weight write runs kF32FwdChunk-sized chunks, growing the memo's chunk buffers and the target workspace
+// on first use (with n_envs = 1 and a 1M replay, chunks of n_envs would be 1M launches of each kernel).
+static void ycache_reserve(qlx_learner* L, uint32_t chunk) {
+  if (chunk <= L->ycap) return;
+  QLX_HIP(hipStreamSynchronize(L->stream));
+  for (void* p : {(void*)L->d_ytab, (void*)L->d_yrew, (void*)L->d_ydone, (void*)L->d_ytmp})
+    if (p) QLX_HIP(hipFree(p));
+  QLX_HIP(hipMalloc(&L->d_ytab, (size_t)chunk * 4 * sizeof(void*)));
+  QLX_HIP(hipMalloc(&L->d_yrew, chunk * sizeof(float)));
+  QLX_HIP(hipMalloc(&L->d_ydone, chunk));
+  QLX_HIP(hipMalloc(&L->d_ytmp, chunk * sizeof(float)));
+  model_workspace(L->target, (int)chunk);
+  L->ycap = chunk;
+}
+
+static void ycache_fill(qlx_learner* L, uint64_t i0, uint64_t n, uint32_t chunk) {
   hipStream_t s = L->stream;
   const ReplayView rv = replay_view(L->rb);
   qlx_model* tg = L->target;
-  for (uint64_t c0 = 0; c0 < n; c0 += L->ychunk) {
-    const uint32_t m = (uint32_t)std::min<uint64_t>(L->ychunk, n - c0);
+  ycache_reserve(L, chunk);
+  for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+    const uint32_t m = (uint32_t)std::min<uint64_t>(chunk, n - c0);
     hipLaunchKernelGGL(k_slot_tables, dim3((m + 255) / 256), dim3(256), 0, s, rv, i0 + c0, m, L->d_ytab, L->d_yrew, L->d_ydone);
     QLX_HIP(hipGetLastError());
     model_forward_trunk(tg, L->d_ytab, (int)m, s, false);
@@ -424,6 +445,24 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
   L->update_count += 1;
 }
 
+// global solved() inputs (data parallel): this rank's episode statistics, then a 3-double sum and a 1-float min all-reduce
+// on the learner stream
+static void learner_book_allreduce(qlx_learner* L) {
+  hipStream_t s = L->stream;
+  hipLaunchKernelGGL(k_book_local, dim3(1), dim3(64), 0, s, L->d_book, L->d_hist, (uint32_t)L->p.episode_reward_history_buffer_len,
+                     L->d_gsum, L->d_gmin);
+  QLX_HIP(hipGetLastError());
+  ncclResult_t r = ncclAllReduce(L->d_gsum, L->d_gsum, 3, ncclFloat64, ncclSum, L->comm, s);
+  QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  r = ncclAllReduce(L->d_gmin, L->d_gmin, 1, ncclFloat, ncclMin, L->comm, s);
+  QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+// the goal solved() tests: Environment::episode_reward_goal_mean (breakout_environment.rs:203-206) unless mocked
+static float learner_goal(const qlx_learner* L) {
+  return L->p.episode_reward_goal != 0.0f ? L->p.episode_reward_goal : (float)(kNumBricks - 1);
+}
+
 static void learner_vector_step(qlx_learner* L, bool train = true) {
   hipStream_t s = L->stream;
   const uint32_t N = L->N;
@@ -458,11 +497,12 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
   if (L->ycache) {   // y of the N new transitions (all live slots after a write of the target weights)
     ProfScope ps(&L->prof, "target_memo", s);
     if (L->target->version != L->ycache_version) {
-      ycache_fill(L, 0, L->rb->len());
+      const uint64_t len = L->rb->len();
+      ycache_fill(L, 0, len, (uint32_t)std::max<uint64_t>(L->ychunk, std::min<uint64_t>(len, kF32FwdChunk)));
       L->ycache_version = L->target->version;
     } else {
       const uint64_t len = L->rb->len(), fresh = std::min<uint64_t>(N, len);
-      ycache_fill(L, len - fresh, fresh);
+      ycache_fill(L, len - fresh, fresh, L->ychunk);
     }
   }
   {
@@ -472,15 +512,7 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
     env_launch_reset(L->env, L->d_reset, 1);
   }
   debug_sync(s, "episode book + reset");
-  if (L->comm && L->world > 1) {   // global solved(): tiny all-reduce of the episode statistics, every vector step
-    hipLaunchKernelGGL(k_book_local, dim3(1), dim3(64), 0, s, L->d_book, L->d_hist, (uint32_t)L->p.episode_reward_history_buffer_len,
-                       L->d_gsum, L->d_gmin);
-    QLX_HIP(hipGetLastError());
-    ncclResult_t r = ncclAllReduce(L->d_gsum, L->d_gsum, 3, ncclFloat, ncclSum, L->comm, s);
-    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    r = ncclAllReduce(L->d_gmin, L->d_gmin, 1, ncclFloat, ncclMin, L->comm, s);
-    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-  }
+  if (L->comm && L->world > 1) learner_book_allreduce(L);   // global solved(): every vector step
   // ---- training updates
   const uint64_t ua = L->p.update_after_actions;
   const uint64_t triggers = L->step_count / ua - step_before / ua;
@@ -586,6 +618,9 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       QLX_CHECK(st == QLX_OK, st, qlx_last_error());
       st = qlx_model_create(arch, p->init_seed, device, &L->target);   // same initial weights
       QLX_CHECK(st == QLX_OK, st, qlx_last_error());
+      // bf16: the target net's fc1 runs in one pass at every batch size, so the memo (chunks of n_envs) and the
+      // per-batch target pass (U * B samples) produce the same y bit for bit (the fp32 kernels never depend on B)
+      L->target->fc1_single = true;
       // everything runs on the learner's stream
       L->env->stream = L->stream; L->env->own_stream = false;
       L->rb->stream = L->stream; L->rb->own_stream = false;
@@ -612,6 +647,8 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       QLX_HIP(hipMalloc(&L->d_ep_reward, N * sizeof(float)));
       QLX_HIP(hipMalloc(&L->d_hist, p->episode_reward_history_buffer_len * sizeof(float)));
       QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
+      QLX_HIP(hipHostMalloc((void**)&L->h_book, sizeof(Book), hipHostMallocDefault));
+      QLX_HIP(hipHostMalloc((void**)&L->h_gsum, 3 * sizeof(double), hipHostMallocDefault));
       QLX_HIP(hipMalloc(&L->d_idx, (size_t)L->max_updates * B * sizeof(uint64_t)));
       const size_t UB = (size_t)L->max_updates * B;   // all batches of one vector step
       QLX_HIP(hipMalloc(&L->d_tab_s, UB * 4 * sizeof(void*)));
@@ -634,12 +671,8 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       if (L->ycache) {
         L->ychunk = std::min<uint32_t>(N, (uint32_t)kF32FwdChunk);
         QLX_HIP(hipMalloc(&L->d_ycache, p->history_buffer_len * sizeof(float)));
-        QLX_HIP(hipMalloc(&L->d_ytab, (size_t)L->ychunk * 4 * sizeof(void*)));
-        QLX_HIP(hipMalloc(&L->d_yrew, L->ychunk * sizeof(float)));
-        QLX_HIP(hipMalloc(&L->d_ydone, L->ychunk));
-        QLX_HIP(hipMalloc(&L->d_ytmp, L->ychunk * sizeof(float)));
+        ycache_reserve(L, L->ychunk);
         L->ycache_version = L->target->version;
-        model_workspace(L->target, (int)L->ychunk);
       } else {
         model_workspace(L->target, (int)(L->max_updates * B));   // batched target pass (learner_targets)
       }
@@ -687,6 +720,8 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
                     L->d_bdone, L->d_losses, L->d_targets, L->d_gsum, L->d_gmin, L->d_ycache, (void*)L->d_ytab,
                     L->d_yrew, L->d_ydone, L->d_ytmp};
     for (void* p : ptrs) (void)hipFree(p);
+    for (void* p : {(void*)L->h_book, (void*)L->h_gsum})
+      if (p) (void)hipHostFree(p);
     L->prio.release();
     (void)hipStreamDestroy(L->stream);
     delete L;
@@ -788,17 +823,18 @@ int32_t qlx_learner_stats_get(qlx_learner* L, qlx_learner_stats* out) {
     out->epsilon = e;
     out->running_reward = b.running_reward;
     // solved (:134-139): running_reward >= goal && min episode reward >= goal * pct
-    const float goal = (float)(kNumBricks - 1);
+    const float goal = learner_goal(L);
     float mn = hist.empty() ? 0.0f : hist[0];
     for (float v : hist) mn = std::min(mn, v);
     out->solved = (!hist.empty() && b.running_reward >= goal && mn >= goal * L->p.lowest_episode_reward_goal_threshold_pct) ? 1 : 0;
     if (L->comm && L->world > 1) {
       // data parallel: solved over all ranks' episodes (as of the last vector step) = mean of the ranks' running rewards
       // >= goal and the smallest episode reward of any rank's history >= goal * pct, every rank with a history
-      float gs[3], gm;
+      double gs[3];
+      float gm;
       QLX_HIP(hipMemcpy(gs, L->d_gsum, sizeof(gs), hipMemcpyDeviceToHost));
       QLX_HIP(hipMemcpy(&gm, L->d_gmin, sizeof(gm), hipMemcpyDeviceToHost));
-      out->solved = (gs[1] == (float)L->world && gs[0] / (float)L->world >= goal &&
+      out->solved = (gs[1] == (double)L->world && gs[0] / (double)L->world >= (double)goal &&
                      gm >= goal * L->p.lowest_episode_reward_goal_threshold_pct) ? 1 : 0;
     }
     float loss = 0.0f;
@@ -870,7 +906,7 @@ int32_t qlx_learner_update_log(qlx_learner* L, char* buf, size_t cap, size_t* le
     qlx_learner_stats st;
     int32_t rc = qlx_learner_stats_get(L, &st);
     QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
-    LogInputs in{st.episode_count, st.step_count, L->p.gamma, st.epsilon, (float)(kNumBricks - 1),
+    LogInputs in{st.episode_count, st.step_count, L->p.gamma, st.epsilon, learner_goal(L),
                  L->p.lowest_episode_reward_goal_threshold_pct, learner_episode_rewards(L), {}, kNames};
     action_counts(L->stream, L->rb->d_action, L->rb->len(), kActions, in.counts);
     copy_text(learning_log(in), buf, cap, len);
@@ -881,8 +917,9 @@ int32_t qlx_learner_update_log(qlx_learner* L, char* buf, size_t cap, size_t* le
 
 // One vector step, then the reference's statistics events (self_driving_tf_q_learner.rs:204-212, 226-230):
 // write_checkpoint (when checkpoint_file is set) + learning_update_log once per vector step that crossed a multiple of
-// stats_after_steps, and once more when an episode ended and solved() holds.  The log text goes to the callback (the
-// reference's log::info!) and stays readable through qlx_learner_last_log.  With stats_after_steps = 0 nothing runs.
+// stats_after_steps (stats_after_steps > 0), and once more when an episode ended and solved() holds (whatever
+// stats_after_steps is).  The log text goes to the callback (the reference's log::info!) and stays readable through
+// qlx_learner_last_log.
 static void learner_stats_event(qlx_learner* L) {
   if (L->p.checkpoint_file[0] && L->rank == 0) {   // data parallel: the weights are identical, rank 0 writes the file
     char path[257];
@@ -916,13 +953,21 @@ static void learner_step_full(qlx_learner* L, bool train) {
   const uint64_t before = L->step_count;
   learner_vector_step(L, train);
   const uint64_t S = L->p.stats_after_steps;
-  if (S == 0) return;
-  if (L->step_count / S != before / S) learner_stats_event(L);
-  Book b;   // solved() after an episode ended in this step (:226-230)
-  QLX_HIP(hipMemcpyAsync(&b, L->d_book, sizeof(Book), hipMemcpyDeviceToHost, L->stream));
+  if (S > 0 && L->step_count / S != before / S) learner_stats_event(L);
+  // solved() after an episode ended in this step (:226-230): one pinned copy of the episode counters (the global sums in
+  // data parallel, so every rank takes the same decision), and the full test only when an episode ended (on any rank) and
+  // the running reward has reached the goal
+  const bool dp = L->comm && L->world > 1;
+  QLX_HIP(hipMemcpyAsync(L->h_book, L->d_book, sizeof(Book), hipMemcpyDeviceToHost, L->stream));
+  if (dp) QLX_HIP(hipMemcpyAsync(L->h_gsum, L->d_gsum, 3 * sizeof(double), hipMemcpyDeviceToHost, L->stream));
   QLX_HIP(hipStreamSynchronize(L->stream));
-  if (b.episode_count != L->seen_episodes || (L->comm && L->world > 1)) {
-    L->seen_episodes = b.episode_count;
+  const uint64_t episodes = dp ? (uint64_t)L->h_gsum[2] : L->h_book->episode_count;
+  const bool ended = episodes != L->seen_episodes;
+  L->seen_episodes = episodes;
+  const float goal = learner_goal(L);
+  const bool may_solve = dp ? (L->h_gsum[1] == (double)L->world && L->h_gsum[0] / (double)L->world >= (double)goal)
+                            : (L->h_book->hist_len > 0 && L->h_book->running_reward >= goal);
+  if (ended && may_solve) {
     qlx_learner_stats st{};
     const int32_t rc = qlx_learner_stats_get(L, &st);
     QLX_CHECK(rc == QLX_OK, rc, qlx_last_error());
@@ -964,7 +1009,7 @@ int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const
     for (hipEvent_t* e : {&L->ev_dense, &L->ev_reduced}) QLX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     L->world = world;
     L->rank = rank;
-    QLX_HIP(hipMalloc(&L->d_gsum, 3 * sizeof(float)));
+    QLX_HIP(hipMalloc(&L->d_gsum, 3 * sizeof(double)));
     QLX_HIP(hipMalloc(&L->d_gmin, sizeof(float)));
     // rank 0's online weights, Adam slots and step count on every rank (one broadcast of the initial
     // weights), and the target net = the online net as in SelfDrivingQLearner::new (self_driving_tf_q_learner.rs:94-116)
@@ -985,6 +1030,13 @@ int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const
     QLX_HIP(hipStreamSynchronize(L->stream));
     QLX_HIP(hipMemcpy(&on->iterations, d_iter, sizeof(int64_t), hipMemcpyDeviceToHost));
     QLX_HIP(hipFree(d_iter));
+    // the global episode statistics as of now, so a stats query before the first vector step reads defined values
+    if (world > 1) {
+      learner_book_allreduce(L);
+      QLX_HIP(hipMemcpyAsync(L->h_gsum, L->d_gsum, 3 * sizeof(double), hipMemcpyDeviceToHost, L->stream));
+      QLX_HIP(hipStreamSynchronize(L->stream));
+      L->seen_episodes = (uint64_t)L->h_gsum[2];   // the solved() check now follows the global episode count
+    }
   });
 }
 

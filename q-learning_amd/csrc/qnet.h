@@ -82,6 +82,9 @@ struct qlx_model {
   // conv1 weight gradient as channel-half blocks (k_conv1_wgrad_h); QLX_CONV1_HALVES=0 at create time selects the
   // one-block-per-chunk k_conv1_wgrad (bit-identical gradients)
   bool conv1_halves = true;
+  // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
+  // sample's result does not depend on the batch it is evaluated in (the learner's target net)
+  bool fc1_single = false;
 };
 
 namespace qlx {

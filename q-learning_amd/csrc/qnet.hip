@@ -567,7 +567,7 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
   {  // fc1: M = B, N = 512, K = 3136.  Small batches split K into kFc1Split fp32 slabs (reduced with bias +
      // ReLU in fixed order) to fill the chip; from 64 M tiles on (B >= 8192) one pass with the epilogue fused
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
-    if (B >= 64 * 128) {
+    if (B >= 64 * 128 || m->fc1_single) {
       launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, 1, Epi4BiasRelu{w.a4, p + var_offset(7), 512}, s);
       w.a4_splits = 0;
     } else {

@@ -69,6 +69,7 @@ class Params(C.Structure):
         ("qnet_precision", C.c_uint32),
         ("stats_after_steps", C.c_uint64),
         ("checkpoint_file", C.c_char * 256),
+        ("episode_reward_goal", C.c_float),
     ]
 
 DOUBLE_DQN = 1

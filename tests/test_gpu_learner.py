@@ -146,22 +146,29 @@ def test_f32_c3_config():
     assert same(np.float32(loss), g["losses"][0])
 
 
+# (n_envs, B, update_after_actions, replay, vector steps, step of the target-weight write): a tiny shape, and a C2-like one
+# where the memo's chunks (n_envs = 1024 samples) and the per-batch pass (U * B = 8 * 1024) fall on different batch sizes
+MEMO_SHAPES = {"tiny": (64, 32, 8, 1000, 30, 18), "c2like": (1024, 1024, 128, 20_000, 8, 5)}
+
+
+@pytest.mark.parametrize("shape", sorted(MEMO_SHAPES))
 @pytest.mark.parametrize("prec", [0, 1])
-def test_target_memo_matches_per_batch_target_pass(monkeypatch, prec):
+def test_target_memo_matches_per_batch_target_pass(monkeypatch, prec, shape):
     """The per-slot Bellman-target memo (default while the target net is frozen, learner.hip ycache_fill) gives the
     same targets, losses and weights as the per-batch target pass (QLX_TARGET_CACHE=0) - bit for bit, also across
     the replay FIFO wrap and after the target weights are overwritten mid-run (the memo is rebuilt for every slot)."""
     qlx = _qlx()
+    N, B, ua, cap, steps, write_at = MEMO_SHAPES[shape]
 
     def run(cache):
         monkeypatch.setenv("QLX_TARGET_CACHE", "1" if cache else "0")
-        p = qlx.Parameter(n_envs=64, batch_size=32, history_buffer_len=1000, update_after_actions=8,
+        p = qlx.Parameter(n_envs=N, batch_size=B, history_buffer_len=cap, update_after_actions=ua,
                           epsilon_pure_random_steps=400, epsilon_greedy_steps=2000.0, max_steps_per_episode=200,
                           stats_after_steps=0, qnet_precision=prec)
         L = qlx.SelfDrivingQLearner(p)
         out = []
-        for v in range(30):
-            if v == 18:
+        for v in range(steps):
+            if v == write_at:
                 w = L.stabilized_model.get(9)
                 L.stabilized_model.set(9, (w + np.float32(0.01)).astype(np.float32))
             L.vector_step()
@@ -239,6 +246,31 @@ def test_stats_events_and_checkpoint(tmp_path):
                 assert same(m2.get(var), gpu.model.get(var))
             m2.close()
     assert seen >= 8 and with_episodes >= 2
+
+
+def test_solved_events_without_periodic_stats(tmp_path):
+    """stats_after_steps = 0 turns off only the periodic event: solved() is still checked after every vector step in which
+    an episode ended (self_driving_tf_q_learner.rs:226-230) and then writes the checkpoint and the log.  The goal is mocked
+    (episode_reward_goal, a test double of Environment::episode_reward_goal_mean) so the random-init net reaches it:
+    same event count as the oracle at every step, and the checkpoint holds the online weights of that moment."""
+    qlx = _qlx()
+    path = str(tmp_path / "solved.ckpt")
+    gpu, ref = make(32, 32, stats_after_steps=0, checkpoint_file=path, max_steps_per_episode=60, update_after_actions=8,
+                    episode_reward_goal=-1.0)
+    fired = 0
+    for v in range(40):
+        gpu.vector_step()
+        ref.vector_step()
+        assert gpu.stats_events() == ref.stats_events(), v
+        if gpu.stats_events() > fired:
+            fired = gpu.stats_events()
+            assert gpu.stats()["solved"] == 1 and "reward_distribution" in gpu.last_log()
+            m2 = qlx.DeepQLearningModel(seed=99)
+            m2.read_checkpoint(path)
+            for var in range(10):
+                assert same(m2.get(var), gpu.model.get(var))
+            m2.close()
+    assert fired >= 2
 
 
 def test_bf16_pure_random_phase_parity():
