@@ -215,10 +215,12 @@ class Run:
                           rank=ctl.rank, flags=flags, qnet_precision=prec)
         L = qlx.SelfDrivingQLearner(p, device=ctl.local)
         self.L = L
+        self.rccl_world = 1
         try:
             if ctl.world > 1:
                 uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
                 L.dist_init(ctl.world, ctl.rank, uid)
+            self.rccl_world = L.comm_size()   # read back from the communicator (ncclCommCount)
             # steady state: replay at capacity and past the pure-random phase, whatever --warmup is
             prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
             log(f"{precision}: prefill {prefill} vector steps")
@@ -448,7 +450,8 @@ def main():
                                f"acting" + (" + double-DQN" if args.double_dqn else "")
                                + (" + prioritized replay" if args.per else ""),
                    "envs_per_gpu": N, "batch": B, "replay_capacity": args.replay, "update_after_actions": head.ua,
-                   "parallelism": f"dp{ctl.world}" if ctl.world > 1 else "single", "rccl_world": ctl.world,
+                   "parallelism": f"dp{ctl.world}" if ctl.world > 1 else "single", "rccl_world": head.rccl_world,
+                   "global_batch_per_update": B * head.rccl_world,
                    "target_memo": "target_memo" in head.comps,
                    "env_dtype": "fp32 physics, u8 frames",
                    "qnet_dtype": "fp32 (exact-fp32 MFMA v_mfma_f32_16x16x4_f32)" if args.precision == "fp32"

@@ -243,6 +243,9 @@ qlx_model* qlx_learner_model(qlx_learner* l, int32_t which /* 0 online, 1 target
  * all-reduced (mean) before clip_by_norm + Adam. uid from qlx_dist_unique_id on rank 0. */
 int32_t qlx_dist_unique_id(uint8_t out[128]);
 int32_t qlx_learner_dist_init(qlx_learner* l, int32_t world, int32_t rank, const uint8_t uid[128]);
+/* Rank count of the learner's RCCL communicator as RCCL reports it (ncclCommCount); 1 without dist_init.  At world W
+ * every update averages W per-rank batches of batch_size samples: the global batch per update is W x batch_size. */
+int32_t qlx_learner_comm_size(qlx_learner* l, int32_t* world);
 /* Kernel timing with HIP events on the learner stream.  Scopes are named per kernel ("conv1_fwd",
  * "conv1_wgrad", "fc1_fwd", "adam", "env_step", "replay_push", ...) or per phase ("act_forward",
  * "gather", "sample"); each carries its algorithmic work (FLOPs for GEMM kernels, bytes for

@@ -215,6 +215,19 @@ float orc_qnet32_train(void* h, const uint8_t* x, const uint8_t* actions, const 
   qnet32_apply_adam(*q, g, norms_out);
   return loss;
 }
+// clip_by_norm + Adam of the fp32 chain definition applied to given raw gradients (all variables concatenated) times
+// scale, rounded once per element as the product does (learner.hip data parallel: the all-reduced sum times 1 / world,
+// qnet32.hip k_norm32 / k_adam32); iterations += 1
+void orc_qnet32_apply(void* h, const float* grads, float scale, float* norms_out) {
+  Grads g;
+  size_t off = 0;
+  for (int v = 0; v < kNumVars; ++v) {
+    g.g[v].resize(kVarSize[v]);
+    for (int i = 0; i < kVarSize[v]; ++i) g.g[v][i] = grads[off + i] * scale;
+    off += kVarSize[v];
+  }
+  qnet32_apply_adam(*(QNet*)h, g, norms_out);
+}
 
 // ---------------- learner ----------------
 void* orc_learner_new(const LearnerParams* p) { return new Learner(*p); }

@@ -1040,6 +1040,18 @@ int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const
   });
 }
 
+int32_t qlx_learner_comm_size(qlx_learner* L, int32_t* world) {
+  return guard([&] {
+    QLX_CHECK(L && world, QLX_E_INVALID, "null argument");
+    *world = 1;
+    if (!L->comm) return;
+    int n = 0;
+    const ncclResult_t r = ncclCommCount(L->comm, &n);
+    QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+    *world = n;
+  });
+}
+
 int32_t qlx_learner_profile(qlx_learner* L, int32_t enable) {
   return guard([&] {
     QLX_CHECK(L, QLX_E_INVALID, "null learner");

@@ -157,6 +157,7 @@ def lib():
         "qlx_sumtree_sample": ([vp, u64, u32, u32, u32, u64, C.c_float, u32, vp, vp], i32),
         "qlx_sumtree_update": ([vp, vp, vp, u32, C.c_float, C.c_float], i32),
         "qlx_dist_unique_id": ([vp], i32), "qlx_learner_dist_init": ([vp, i32, i32, vp], i32),
+        "qlx_learner_comm_size": ([vp, vp], i32),
         "qlx_learner_profile": ([vp, i32], i32),
         "qlx_learner_profile_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)], i32),
         "qlx_learner_profile_filter": ([vp, C.c_char_p], i32),
@@ -522,6 +523,12 @@ class SelfDrivingQLearner(_LearningStats):
     def dist_init(self, world, rank, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
         _check(lib().qlx_learner_dist_init(self.h, world, rank, buf))
+
+    def comm_size(self):
+        """ranks of the RCCL communicator (ncclCommCount), 1 without dist_init"""
+        n = C.c_int32()
+        _check(lib().qlx_learner_comm_size(self.h, C.byref(n)))
+        return n.value
 
     def profile(self, enable=True):
         _check(lib().qlx_learner_profile(self.h, 1 if enable else 0))

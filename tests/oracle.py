@@ -134,6 +134,7 @@ def lib():
         L.orc_qnet32_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.orc_qnet32_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
         L.orc_qnet32_train.restype = f32
+        L.orc_qnet32_apply.argtypes = [vp, vp, f32, vp]
         L.orc_learner_prefill.argtypes = [vp, u64]
         L.orc_learner_stats_events.argtypes = [vp]
         L.orc_learner_stats_events.restype = u64
@@ -348,6 +349,15 @@ class QNet:
             out.append(grads[off:off + VAR_SIZES[v]].reshape(VAR_SHAPES[v]))
             off += VAR_SIZES[v]
         return loss, out, norms
+
+
+def qnet32_apply(net, flat_grads, scale):
+    """clip_by_norm + Adam (fp32 chain definition) of net with flat_grads * scale; returns the clip norms"""
+    g = np.ascontiguousarray(flat_grads, dtype=np.float32)
+    assert g.size == sum(VAR_SIZES)
+    norms = np.zeros(10, np.float32)
+    lib().orc_qnet32_apply(net.h, _p(g), scale, _p(norms))
+    return norms
 
 
 def cluster_analysis(elements, eps, min_neighbors):

@@ -255,7 +255,7 @@ def test_solved_events_without_periodic_stats(tmp_path):
     same event count as the oracle at every step, and the checkpoint holds the online weights of that moment."""
     qlx = _qlx()
     path = str(tmp_path / "solved.ckpt")
-    gpu, ref = make(32, 32, stats_after_steps=0, checkpoint_file=path, max_steps_per_episode=60, update_after_actions=8,
+    gpu, ref = make(32, 32, stats_after_steps=0, checkpoint_file=path, max_steps_per_episode=15, update_after_actions=8,
                     episode_reward_goal=-1.0)
     fired = 0
     for v in range(40):
