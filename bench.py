@@ -13,8 +13,9 @@ Default workload (N = 1): config C3 of SURVEY.md §8(d) - 8,192 envs per GPU, re
 fp32 Q-net (the reference's arithmetic).  Steady state regardless of --warmup: before anything is timed the replay
 is prefilled to capacity, which also runs the loop past the 50k-step pure-random phase, so the timed vector steps
 include the greedy acting forward, brick contacts and episode ends; then it keeps stepping (no updates) until episode
-ends are spread over the steps as in a long run (all envs launch together, so their first episodes end in waves): at
-least 3 finished episodes per env, then one mean episode length of vector steps each within +-50 % of the expected
+ends are spread over the steps as in a long run (all envs launch together and the untrained policy's episodes have
+nearly one length, so their ends come in waves): after the first wave the envs' next episodes are started at staggered
+steps (Run._steady), then one mean episode length of vector steps must each hold within +-50 % of the expected
 n_envs / mean-length episode ends.  Then W untimed training vector steps, then K timed ones (asserted to contain
 episode ends).  Beside the headline, measured in the same run: the same loop with the frozen target net evaluated per
 sampled batch as the reference does (value_no_target_memo), and the bf16 fast path (labelled, not the headline).
@@ -38,9 +39,9 @@ sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md: f32-input MFMA, bf16)
-# steady state before timing (Run._steady): at least STEADY_EPISODES finished episodes per env on average, then a window
-# of one mean episode length in which every vector step's episode-end count is within +-STEADY_TOL of n_envs / mean length
-STEADY_EPISODES, STEADY_TOL, MAX_STEADY = 3.0, 0.5, 4000
+# steady state before timing (Run._steady): a window of one mean episode length in which every vector step's episode-end
+# count is within +-STEADY_TOL of n_envs / mean length
+STEADY_TOL, MAX_STEADY = 0.5, 4000
 PEAK_HBM_GBS = 8000.0                            # HBM3E
 # per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
 FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
@@ -243,31 +244,48 @@ class Run:
             L.close()
 
     def _steady(self, L):
-        """Vector steps without updates until the episode ends are no longer in waves: at least STEADY_EPISODES finished
-        episodes per env on average, then a window of one mean episode length (in vector steps) in which every step's
-        episode-end count is within STEADY_TOL of the expected n_envs / mean length.  The decision is global (every rank
-        runs the same number of vector steps: each one carries collectives)."""
+        """Vector steps without updates until episode ends are spread over the steps as in a long run.  All envs launch
+        together and the untrained policy's episodes have nearly one length, so left alone their ends come in waves that
+        persist for thousands of vector steps (measured: 0..275 ends per step after 4,000).  So: (1) step until the first
+        wave has passed (one finished episode per env on average) and take the mean episode length T from it; (2) a
+        staggered start - over T steps, step k ends the current episode of the envs e = k (mod T) (the
+        max_steps_per_episode path, qlx_learner_end_episodes); (3) step until one window of T vector steps has every
+        step's episode-end count within STEADY_TOL of n_envs / T.  Decisions are global (every rank runs the same number
+        of vector steps: each one carries collectives)."""
+        import numpy as np
         N, ctl = self.args.envs, self.ctl
-        s = L.stats()
-        last, steps0 = s["episode_count"], s["step_count"]
-        ends, n = [], 0
+        n = 0
         while n < MAX_STEADY:
+            s = L.stats()
+            if ctl.sum(float(s["episode_count"])) >= N * ctl.world:
+                break
             L.prefill(1)
             n += 1
-            s = L.stats()
-            ends.append(s["episode_count"] - last)
-            last = s["episode_count"]
-            tot = ctl.sum(float(last))
-            mean_len = ctl.sum(float(s["step_count"])) / max(tot, 1.0)   # env-steps per finished episode = vector steps
-            expect = N / mean_len
-            win = int(mean_len + 0.999)
-            ok = tot >= STEADY_EPISODES * N * ctl.world and len(ends) >= win and \
-                all(abs(e - expect) <= STEADY_TOL * expect for e in ends[-win:])
-            if ctl.min(1.0 if ok else 0.0) > 0:
+        s = L.stats()
+        mean_len = ctl.sum(float(s["step_count"])) / max(ctl.sum(float(s["episode_count"])), 1.0)
+        T = max(1, int(round(mean_len)))
+        eids = np.arange(N)
+        for k in range(T):
+            L.end_episodes((eids % T) == k)
+            L.prefill(1)
+            n += 1
+        expect = N / mean_len
+        last, ends, ok = L.stats()["episode_count"], [], False
+        for _ in range(2 * T + 1):
+            L.prefill(1)
+            n += 1
+            e = L.stats()["episode_count"]
+            ends.append(e - last)
+            last = e
+            mine = len(ends) >= T and all(abs(x - expect) <= STEADY_TOL * expect for x in ends[-T:])
+            if ctl.min(1.0 if mine else 0.0) > 0:
+                ok = True
                 break
-        self.mean_len, self.expect_ends = mean_len, expect
+        self.mean_len, self.expect_ends, self.steady_ok = mean_len, expect, ok
+        self.steady_window = (min(ends[-T:]), max(ends[-T:]))
         log(f"{self.precision}: {n} more vector steps to steady episode ends (mean episode {mean_len:.1f} env-steps, "
-            f"{expect:.1f} ends expected per vector step, last window min/max {min(ends[-win:])}/{max(ends[-win:])})")
+            f"staggered over {T}; {expect:.1f} ends expected per vector step, last window min/max "
+            f"{self.steady_window[0]}/{self.steady_window[1]}, steady {ok})")
         return n
 
     def _profile(self):
@@ -464,7 +482,8 @@ def main():
         "steady_state": {"prefill_vector_steps": head.prefill, "episodes_in_window": head.episodes,
                          "episode_ends_per_step": round(head.ends_per_step, 2),
                          "expected_ends_per_step": round(head.expect_ends * ctl.world, 2),
-                         "mean_episode_env_steps": round(head.mean_len, 1),
+                         "mean_episode_env_steps": round(head.mean_len, 1), "steady": head.steady_ok,
+                         "steady_window_min_max_ends": list(head.steady_window),
                          "episodes_total": head.episodes_total, "epsilon": round(head.epsilon, 4),
                          "running_reward": head.running_reward, "last_loss": head.last_loss},
         "components_event_timed": comps,

@@ -211,6 +211,11 @@ int32_t qlx_learner_run(qlx_learner* l, uint64_t n_vector_steps);
 /* Vector steps without updates (act, env step, replay push, episode books; epsilon and step_count advance): fills the
  * replay before a measurement or a parity check at a given replay occupancy.  Not in the reference loop. */
 int32_t qlx_learner_prefill(qlx_learner* l, uint64_t n_vector_steps);
+/* End the current episode of every env with mask[e] != 0 now, as reaching max_steps_per_episode does (learn_episode
+ * :214-224: the episode's reward enters the reward history, episode_count advances, the env resets); no transition is
+ * added.  mask: host array [n_envs].  Lets a measurement start the envs' episodes at staggered steps (all envs launch
+ * together, so with a short-lived policy their episodes otherwise end in waves).  Not in the reference loop. */
+int32_t qlx_learner_end_episodes(qlx_learner* l, const uint8_t* mask);
 /* learn_till_mastered (self_driving_tf_q_learner.rs:127-132): vector steps until solved() or max_vector_steps. */
 int32_t qlx_learner_learn_till_mastered(qlx_learner* l, uint64_t max_vector_steps, uint64_t* steps_run);
 /* Statistics events so far (write_checkpoint + learning_update_log every stats_after_steps env-steps and on solved,

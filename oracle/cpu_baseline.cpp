@@ -25,13 +25,14 @@ int main(int argc, char** argv) {
   p.n_envs = n_envs; p.batch_size = batch;
   p.env_seed = 0x51A5EED; p.learner_seed = 1; p.init_seed = 2; p.rank = 0;
   Learner l(p);
+  l.pack_like_reference = true;   // the reference's per-element f32 tensor packing (learner_ref.h)
   const auto t0 = std::chrono::steady_clock::now();
   uint64_t done_steps = 0;
   while (done_steps < steps) { l.vector_step(); done_steps += n_envs; }
   const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   printf("{\"env_steps\": %llu, \"updates\": %llu, \"seconds\": %.6f, \"env_steps_per_sec\": %.3f, "
-         "\"updates_per_sec\": %.3f, \"threads\": %d, \"episodes\": %llu}\n",
+         "\"updates_per_sec\": %.3f, \"threads\": %d, \"episodes\": %llu, \"pack_sink\": %.1f}\n",
          (unsigned long long)done_steps, (unsigned long long)l.update_count, sec, done_steps / sec,
-         l.update_count / sec, omp_get_max_threads(), (unsigned long long)l.episode_count);
+         l.update_count / sec, omp_get_max_threads(), (unsigned long long)l.episode_count, l.pack_sink);
   return 0;
 }

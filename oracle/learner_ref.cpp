@@ -67,6 +67,34 @@ Learner::Learner(const LearnerParams& prm) : p(prm), replay(prm.history_buffer_l
   epsilon = p.epsilon_max;
 }
 
+// Tensor<f32>::set(&[b, x, y, hist]) of the tensorflow crate: index from the dims with a bounds check per axis; the pixel
+// from ImageBuffer::get_pixel(x, y) (bounds-checked, row-major y * width + x), loops hist / y / x as the reference nests
+// them (breakout_environment.rs:63-74)
+void Learner::pack_reference(const std::vector<StateRef>& states) {
+  const uint64_t dims[4] = {(uint64_t)states.size(), (uint64_t)kFrame, (uint64_t)kFrame, (uint64_t)kSlots};
+  std::vector<float> tensor((size_t)dims[0] * dims[1] * dims[2] * dims[3]);
+  for (size_t b = 0; b < states.size(); ++b)
+    for (int hist = 0; hist < kSlots; ++hist) {
+      const uint8_t* v = states[b]->data();   // the u8 view [x][y][slot] holds each frame image's pixels
+      for (uint32_t y = 0; y < (uint32_t)kFrame; ++y)
+        for (uint32_t x = 0; x < (uint32_t)kFrame; ++x) {
+          if (x >= (uint32_t)kFrame || y >= (uint32_t)kFrame) abort();   // get_pixel bounds
+          const uint8_t pixel = v[((size_t)x * kFrame + y) * kSlots + hist];
+          const uint64_t idx[4] = {b, x, y, (uint64_t)hist};
+          uint64_t index = 0, d = 1;
+          for (int i = 3; i >= 0; --i) {
+            if (!(dims[i] > idx[i])) abort();
+            index += idx[i] * d;
+            d *= dims[i];
+          }
+          tensor[index] = (float)pixel;
+        }
+    }
+  double s = 0.0;
+  for (size_t i = 0; i < tensor.size(); i += 97) s += tensor[i];
+  pack_sink += s;
+}
+
 void Learner::vector_step(bool train) {
   const uint32_t N = p.n_envs;
   last_actions.assign(N, 0);
@@ -84,6 +112,7 @@ void Learner::vector_step(bool train) {
   if (any_greedy) {
     std::vector<uint8_t> x((size_t)N * kStateBytes);
     for (uint32_t e = 0; e < N; ++e) std::memcpy(&x[(size_t)e * kStateBytes], state[e]->data(), kStateBytes);
+    if (pack_like_reference) pack_reference(state);   // to_multi_dim_array of each acting state (:36-53)
     Acts a;
     fwd(online, x.data(), (int)N, a);
     last_q = a.q;
@@ -175,6 +204,11 @@ void Learner::targets(const uint64_t* idx, float* y) const {
   const int B = (int)p.batch_size;
   std::vector<uint8_t> xn((size_t)B * kStateBytes);
   for (int b = 0; b < B; ++b) std::memcpy(&xn[(size_t)b * kStateBytes], replay.buf[idx[b]].s_next->data(), kStateBytes);
+  if (pack_like_reference) {   // batch_to_multi_dim_array(state_next batch) (q_learning_model.rs:137)
+    std::vector<StateRef> sn(B);
+    for (int b = 0; b < B; ++b) sn[b] = replay.buf[idx[b]].s_next;
+    const_cast<Learner*>(this)->pack_reference(sn);
+  }
   Acts at;
   fwd(target, xn.data(), B, at);   // batch_predict_max_future_reward
   Acts an;
@@ -200,6 +234,11 @@ void Learner::update(const uint64_t* idx, const float* isw, const float* y) {
     const Transition& t = replay.buf[idx[b]];
     std::memcpy(&xs[(size_t)b * kStateBytes], t.s->data(), kStateBytes);
     act[b] = t.action;
+  }
+  if (pack_like_reference) {   // batch_to_multi_dim_array(state batch) (q_learning_model.rs:171)
+    std::vector<StateRef> sb(B);
+    for (int b = 0; b < B; ++b) sb[b] = replay.buf[idx[b]].s;
+    pack_reference(sb);
   }
   Acts ao;
   fwd(online, xs.data(), B, ao);

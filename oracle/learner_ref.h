@@ -131,6 +131,14 @@ struct Learner {
 
   uint64_t stats_events = 0;            // write_checkpoint + learning_update_log events so far
 
+  // CPU baseline only (oracle/cpu_baseline): also build the reference's f32 input tensors element by element, as
+  // BreakoutState::batch_to_multi_dim_array / to_multi_dim_array do (breakout_environment.rs:36-77), for s' of every
+  // target pass, s of every train step and each greedy acting state; the restated Q-net reads the u8 view (same values),
+  // so the tensors feed a checksum only.  Off for parity runs (no effect on any result).
+  bool pack_like_reference = false;
+  double pack_sink = 0.0;
+  void pack_reference(const std::vector<StateRef>& states) ;
+
   explicit Learner(const LearnerParams& prm);
   // train = false: act, step, push and keep the books only (replay prefill: no updates, no update_count)
   void vector_step(bool train = true);

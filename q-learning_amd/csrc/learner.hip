@@ -754,6 +754,22 @@ int32_t qlx_learner_prefill(qlx_learner* L, uint64_t n) {
   });
 }
 
+int32_t qlx_learner_end_episodes(qlx_learner* L, const uint8_t* mask) {
+  return guard([&] {
+    QLX_CHECK(L && mask, QLX_E_INVALID, "null argument");
+    QLX_HIP(hipSetDevice(L->device));
+    hipStream_t s = L->stream;
+    // the episode bookkeeping of one vector step with zero rewards and the mask as the end condition
+    QLX_HIP(hipMemcpyAsync(L->d_reset, mask, L->N, hipMemcpyHostToDevice, s));
+    QLX_HIP(hipMemsetAsync(L->d_rewards, 0, L->N * sizeof(float), s));
+    launch_episode_book(s, L->N, L->d_rewards, L->d_reset, L->env->d_ep_steps, L->p.max_steps_per_episode, L->d_ep_reward, L->d_hist,
+                        (uint32_t)L->p.episode_reward_history_buffer_len, L->d_book, L->d_dones);
+    env_launch_reset(L->env, L->d_dones, 1);
+    QLX_HIP(hipMemsetAsync(L->d_dones, 0, L->N, s));
+    QLX_HIP(hipStreamSynchronize(s));
+  });
+}
+
 int32_t qlx_learner_learn_till_mastered(qlx_learner* L, uint64_t max_vector_steps, uint64_t* steps_run) {
   return guard([&] {
     QLX_CHECK(L, QLX_E_INVALID, "null learner");

@@ -138,7 +138,7 @@ def lib():
         "qlx_params_default": ([vp], None),
         "qlx_learner_create": ([C.POINTER(Params), i32, C.POINTER(vp)], i32), "qlx_learner_destroy": ([vp], i32),
         "qlx_learner_vector_step": ([vp], i32), "qlx_learner_run": ([vp, u64], i32), "qlx_learner_sync": ([vp], i32),
-        "qlx_learner_prefill": ([vp, u64], i32), "qlx_learner_stats_events": ([vp], u64),
+        "qlx_learner_prefill": ([vp, u64], i32), "qlx_learner_end_episodes": ([vp, vp], i32), "qlx_learner_stats_events": ([vp], u64),
         "qlx_learner_learn_till_mastered": ([vp, u64, C.POINTER(u64)], i32),
         "qlx_learner_last_log": ([vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)], i32),
         "qlx_learner_stats_get": ([vp, C.POINTER(LearnerStats)], i32),
@@ -472,6 +472,12 @@ class SelfDrivingQLearner(_LearningStats):
     def prefill(self, n):
         """n vector steps without updates (replay fill before a measurement / parity check)"""
         _check(lib().qlx_learner_prefill(self.h, n))
+
+    def end_episodes(self, mask):
+        """end the current episode of every env with mask[e] (the max_steps_per_episode path; no transition added)"""
+        m = np.ascontiguousarray(mask, dtype=np.uint8)
+        assert m.shape == (self.param.n_envs,)
+        _check(lib().qlx_learner_end_episodes(self.h, _p(m)))
 
     def learn_till_mastered(self, max_vector_steps):
         n = C.c_uint64()

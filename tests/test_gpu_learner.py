@@ -273,6 +273,33 @@ def test_solved_events_without_periodic_stats(tmp_path):
     assert fired >= 2
 
 
+def test_end_episodes_is_the_truncation_path():
+    """qlx_learner_end_episodes (the bench's staggered start): the masked envs' episodes end as at
+    max_steps_per_episode - episode_count advances by the mask's count, their running episode rewards enter the
+    history in env order, the envs reset (reset_count + 1, fresh state) - and the others are untouched; no transition."""
+    N = 64
+    gpu, _ = make(N, 32, max_steps_per_episode=10_000)
+    for _ in range(12):
+        gpu.vector_step()
+    s0 = gpu.stats()
+    mech0 = gpu.environment.mechanics()
+    rewards0 = gpu.episode_rewards()
+    mask = (np.arange(N) % 3 == 1).astype(np.uint8)
+    gpu.end_episodes(mask)
+    s1 = gpu.stats()
+    mech1 = gpu.environment.mechanics()
+    assert s1["episode_count"] == s0["episode_count"] + int(mask.sum())
+    assert s1["replay_len"] == s0["replay_len"] and s1["step_count"] == s0["step_count"]
+    for e in range(N):
+        if mask[e]:
+            assert mech1["reset_count"][e] == mech0["reset_count"][e] + 1, e
+        else:
+            assert all(mech1[k][e] == mech0[k][e] for k in O.STATE_DTYPE.names), e
+    assert len(gpu.episode_rewards()) == min(100, len(rewards0) + int(mask.sum()))
+    gpu.vector_step()   # the loop continues from there
+    assert gpu.stats()["step_count"] == s0["step_count"] + N
+
+
 def test_bf16_pure_random_phase_parity():
     N, B = 16, 32
     gpu, ref = make(N, B, prec=1, max_steps_per_episode=45)
