@@ -39,9 +39,10 @@ sys.path.insert(0, os.path.join(ROOT, "q-learning_amd"))
 
 METRIC = "env-steps/sec + grad-updates/sec, Breakout 84×84×4, 1/2/4/8 MI355X"
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md: f32-input MFMA, bf16)
-# steady state before timing (Run._steady): a window of one mean episode length in which every vector step's episode-end
-# count is within +-STEADY_TOL of n_envs / mean length
-STEADY_TOL, MAX_STEADY = 0.5, 4000
+# steady state before timing (Run._steady): a window of one mean episode length T whose episode ends per vector step average
+# within +-STEADY_MEAN_TOL of n_envs / T with a coefficient of variation <= STEADY_MAX_CV (waves: CV >> 1; a steady
+# stream of independent ends: ~1 / sqrt(n_envs / T))
+STEADY_MEAN_TOL, STEADY_MAX_CV, MAX_STEADY = 0.1, 0.5, 4000
 PEAK_HBM_GBS = 8000.0                            # HBM3E
 # per-sample algorithmic FLOPs of the Q-net: forward 18,689,024; per trained sample 68,202,496
 FWD_FLOP, TRAIN_FLOP = 18_689_024, 68_202_496
@@ -249,8 +250,9 @@ class Run:
         persist for thousands of vector steps (measured: 0..275 ends per step after 4,000).  So: (1) step until the first
         wave has passed (one finished episode per env on average) and take the mean episode length T from it; (2) a
         staggered start - over T steps, step k ends the current episode of the envs e = k (mod T) (the
-        max_steps_per_episode path, qlx_learner_end_episodes); (3) step until one window of T vector steps has every
-        step's episode-end count within STEADY_TOL of n_envs / T.  Decisions are global (every rank runs the same number
+        max_steps_per_episode path, qlx_learner_end_episodes); (3) step until one window of T vector steps has its
+        episode ends per step averaging within STEADY_MEAN_TOL of n_envs / T with a coefficient of variation of at most
+        STEADY_MAX_CV.  Decisions are global (every rank runs the same number
         of vector steps: each one carries collectives)."""
         import numpy as np
         N, ctl = self.args.envs, self.ctl
@@ -271,21 +273,28 @@ class Run:
             n += 1
         expect = N / mean_len
         last, ends, ok = L.stats()["episode_count"], [], False
-        for _ in range(2 * T + 1):
+        def window_stats(w):
+            w = np.asarray(w, np.float64)
+            return w.mean(), w.std() / max(w.mean(), 1e-9)
+        for _ in range(3 * T):
             L.prefill(1)
             n += 1
             e = L.stats()["episode_count"]
             ends.append(e - last)
             last = e
-            mine = len(ends) >= T and all(abs(x - expect) <= STEADY_TOL * expect for x in ends[-T:])
+            mine = False
+            if len(ends) >= T:
+                mean, cv = window_stats(ends[-T:])
+                mine = abs(mean - expect) <= STEADY_MEAN_TOL * expect and cv <= STEADY_MAX_CV
             if ctl.min(1.0 if mine else 0.0) > 0:
                 ok = True
                 break
+        mean, cv = window_stats(ends[-T:])
         self.mean_len, self.expect_ends, self.steady_ok = mean_len, expect, ok
-        self.steady_window = (min(ends[-T:]), max(ends[-T:]))
+        self.steady_window = {"steps": T, "mean_ends": round(mean, 2), "cv": round(cv, 3), "min": int(min(ends[-T:])),
+                              "max": int(max(ends[-T:]))}
         log(f"{self.precision}: {n} more vector steps to steady episode ends (mean episode {mean_len:.1f} env-steps, "
-            f"staggered over {T}; {expect:.1f} ends expected per vector step, last window min/max "
-            f"{self.steady_window[0]}/{self.steady_window[1]}, steady {ok})")
+            f"staggered over {T}; {expect:.1f} ends expected per vector step; last window {self.steady_window}, steady {ok})")
         return n
 
     def _profile(self):
@@ -483,7 +492,7 @@ def main():
                          "episode_ends_per_step": round(head.ends_per_step, 2),
                          "expected_ends_per_step": round(head.expect_ends * ctl.world, 2),
                          "mean_episode_env_steps": round(head.mean_len, 1), "steady": head.steady_ok,
-                         "steady_window_min_max_ends": list(head.steady_window),
+                         "steady_window": head.steady_window,
                          "episodes_total": head.episodes_total, "epsilon": round(head.epsilon, 4),
                          "running_reward": head.running_reward, "last_loss": head.last_loss},
         "components_event_timed": comps,

@@ -170,18 +170,24 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R) {
 
 // clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg = 2048;
 // thread t chains t = fmaf(x, x, t) over its elements j S + 4 t .. + 3, then j S + 1024 + 4 t .. + 3 (x = g * scale);
-// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  Norm_v from its partials in k_adam32.
+// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  The last block to finish (a device-scope
+// counter) reduces the partials to the ten norms: norm_v from 64 lane chains over its partials j = lane mod 64 ascending
+// and one xor butterfly, so k_adam32 starts from ten finished values (one load) instead of every Adam block re-reducing
+// ~830 partials in three dependent load rounds.
 constexpr int kNormSeg = 2048;
-constexpr int kNormSegMax = 1024;   // partials per variable the Adam prologue reduces (16 per lane)
+constexpr int kNormSegMax = 1024;   // partials per variable the final reduction takes (16 per lane)
 struct NormArgs {
   const float* g;
   float scale;
   float* partial;
+  unsigned* count;   // zero between launches (the last block resets it)
+  float* norms;
   int seg_first[kNumVars + 1];
   int64_t off[kNumVars + 1];
 };
 __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   __shared__ float wsum[4];
+  __shared__ int last;
   int v = 0;
   while (v < kNumVars - 1 && (int)blockIdx.x >= A.seg_first[v + 1]) ++v;
   const int j = blockIdx.x - A.seg_first[v];
@@ -210,7 +216,30 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
   __syncthreads();
-  if (threadIdx.x == 0) A.partial[blockIdx.x] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]);
+  if (threadIdx.x == 0) {
+    // the partial goes out device-coherent, then the counter (acquire-release at agent scope: the last block sees every
+    // other block's partial)
+    __hip_atomic_store(A.partial + blockIdx.x, __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned prev = __hip_atomic_fetch_add(A.count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int v = wave; v < kNumVars; v += 4) {
+    const int first = A.seg_first[v], cnt = A.seg_first[v + 1] - first;
+    float x[kNormSegMax / 64];
+#pragma unroll
+    for (int i = 0; i < kNormSegMax / 64; ++i)
+      x[i] = lane + 64 * i < cnt ? __hip_atomic_load(A.partial + first + lane + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kNormSegMax / 64; ++i) s = __fadd_rn(s, x[i]);
+    for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o));
+    if (lane == 0) A.norms[v] = s > 0.0f ? sqrtf(s) : s;   // safe sqrt via where(l2sum > 0)
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(A.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct Adam32Args {
@@ -218,10 +247,8 @@ struct Adam32Args {
   float* m;
   float* v;
   const float* g;
-  const float* partial;
-  int seg_first[kNumVars + 1];
   int64_t off[kNumVars + 1];
-  float* norms;
+  const float* norms;   // k_norm32's ten clip norms
   float scale, alpha, beta1, beta2, eps, clipnorm;
 };
 
@@ -234,24 +261,17 @@ __device__ __forceinline__ float adam32_elem(float g, float scale, float clipnor
   return __fsub_rn(w, __fmul_rn(m, alpha) / __fadd_rn(sqrtf(v), eps));
 }
 
+// the variable of flat element i (branch-free: the number of variable starts at or below i, minus one)
+__device__ __forceinline__ int var_of(const Adam32Args& A, int64_t i) {
+  int v = 0;
+#pragma unroll
+  for (int k = 1; k < kNumVars; ++k) v += i >= A.off[k] ? 1 : 0;
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
   __shared__ float nrm[kNumVars];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // norm_v: lane chain over the partials lane, lane + 64, ... of v (zeros past the end), then the xor butterfly
-  for (int v = wave; v < kNumVars; v += 4) {
-    const int first = A.seg_first[v], cnt = A.seg_first[v + 1] - first;
-    float x[kNormSegMax / 64];
-#pragma unroll
-    for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < cnt ? A.partial[first + lane + 64 * i] : 0.0f;
-    float t = 0.0f;
-#pragma unroll
-    for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
-    for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
-    if (lane == 0) {
-      nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
-      if (blockIdx.x == 0) A.norms[v] = nrm[v];
-    }
-  }
+  if (threadIdx.x < kNumVars) nrm[threadIdx.x] = A.norms[threadIdx.x];
   __syncthreads();
   // four elements per thread and step (16-byte accesses; every variable but the last starts at a multiple of 4, so a
   // group never straddles two variables; the last group is finished element by element)
@@ -259,9 +279,7 @@ __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= n4; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i0 = q * 4;
     if (q < n4) {
-      int var = 0;
-      while (i0 >= A.off[var + 1]) ++var;
-      const float denom = fmaxf(nrm[var], A.clipnorm);
+      const float denom = fmaxf(nrm[var_of(A, i0)], A.clipnorm);
       const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
       f32x4 m = ld4(A.m + i0), v = ld4(A.v + i0), o;
 #pragma unroll
@@ -276,9 +294,7 @@ __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
       *reinterpret_cast<f32x4*>(A.v + i0) = v;
     } else {
       for (int64_t i = i0; i < count; ++i) {
-        int var = 0;
-        while (i >= A.off[var + 1]) ++var;
-        const float denom = fmaxf(nrm[var], A.clipnorm);
+        const float denom = fmaxf(nrm[var_of(A, i)], A.clipnorm);
         float m = A.m[i], v = A.v[i];
         A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
         A.m[i] = m;
@@ -319,6 +335,7 @@ void f32_workspace(qlx_model* m, int B) {
   for (int v = 0; v < kNumVars; ++v) nseg += segs_of(v);
   const size_t o_part = take((size_t)nseg * 4);
   const size_t o_loss = take(64);
+  const size_t o_count = take(64);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -330,6 +347,8 @@ void f32_workspace(qlx_model* m, int B) {
   w.done = (uint8_t*)(base + o_done);
   w.fpart = (float*)(base + o_part);
   w.loss = (float*)(base + o_loss);
+  w.fnorm_count = (unsigned*)(base + o_count);
+  QLX_HIP(hipMemset(w.fnorm_count, 0, 64));
   w.fchunk = C;
   m->ws_batch = B;
 }
@@ -480,15 +499,27 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   // algorithmic FLOPs (backward-data + weight gradient of the layer; the pixel-major dgrad tiles multiply only the
   // valid taps, so MFMA work = algorithmic work)
+  // pixel-major backward data as balanced pixel groups (chained sub-tiles; QLX_F32_PXG=0: one pixel per tile)
+  static const bool pxg = [] { const char* e = std::getenv("QLX_F32_PXG"); return !(e && e[0] == '0'); }();
   {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
-    PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+    if (pxg) {
+      PConv3DgradPxG<32, 64, 2, 2> Pd{{Grid{(B + 31) / 32, 1, PConv3DgradPxG<>::GROUPS}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B}};
+      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+    } else {
+      PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
+      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+    }
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
-    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
-    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    if (pxg) {
+      PConv2DgradPxG<64, 64, 2, 2> Pd{{Grid{(B + 63) / 64, 2, PConv2DgradPxG<>::GROUPS}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B}};
+      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    } else {
+      PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
+      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    }
   }
   {
     constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
@@ -532,6 +563,8 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
   A.g = m->d_grads;
   A.scale = scale;
   A.partial = m->w.fpart;
+  A.count = m->w.fnorm_count;
+  A.norms = m->d_norms;
   seg_tables(A.seg_first, A.off);
   hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
   QLX_HIP(hipGetLastError());
@@ -543,13 +576,15 @@ void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const float tf = (float)t;
   const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
   Adam32Args a;
-  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.partial = m->w.fpart; a.norms = m->d_norms;
-  seg_tables(a.seg_first, a.off);
+  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.norms = m->d_norms;
+  int seg_first[kNumVars + 1];
+  seg_tables(seg_first, a.off);
   a.scale = scale;
   a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
   ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
-  hipLaunchKernelGGL(k_adam32, dim3(2048), dim3(256), 0, s, a);
+  const int64_t groups = kNumParams / 4 + 1;   // float4 groups + the tail group
+  hipLaunchKernelGGL(k_adam32, dim3((unsigned)std::min<int64_t>(2048, (groups + 255) / 256)), dim3(256), 0, s, a);
   QLX_HIP(hipGetLastError());
   debug_sync(s, "k_adam32");
   m->iterations = t;

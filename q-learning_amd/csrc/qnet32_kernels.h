@@ -329,6 +329,144 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   }
 }
 
+// Chained sub-tiles: one block runs the tiles (tm, tn, z_0), (tm, tn, z_1), .. of its group zg = the z grid index
+// (P::sub_count(zg) <= P::NSUB sub-tiles, z_i = P::sub_z(zg, i)) as ONE slab pipeline over the concatenated slabs: the
+// loads of a sub-tile's first slabs are in flight while the previous sub-tile's last slabs are multiplied, and at a
+// sub-tile's last slab its accumulators go through P::epi and restart from zero.  Each output is still one chain over its
+// own tile's slabs in order, so the results equal gemm_body's on the same tiles bit for bit.  For short-K tiles (pixel-major
+// backward data: 1..9 valid taps) this removes the per-tile pipeline ramp and epilogue wait that dominate a short tile.
+template <class P>
+__device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) {
+  constexpr int MF = 16;
+  using OA = Opnd<P::BM, P::A_KMAJ, MF>;
+  using OB = Opnd<P::BN, P::B_KMAJ, MF>;
+  static_assert(KSplitOf<P>::value == 1 && !P::BIAS && !HasACtx<P>::value, "chained tiles: plain policies");
+  constexpr int T = P::WM * P::WN * 64;
+  constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
+  static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
+  constexpr int NA = (OA::F4 + T - 1) / T, NB = (OB::F4 + T - 1) / T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % P::WM, wn = wave / P::WM;
+  int tm, tn, zg;
+  p.decode(lb, tm, tn, zg);
+  const int row0 = tm * P::BM, col0 = tn * P::BN;
+  // sub-tile table (block-uniform): z and the first global slab of each sub-tile
+  const int nsub = p.sub_count(zg);
+  int subz[P::NSUB], cum[P::NSUB + 1];
+  cum[0] = 0;
+#pragma unroll
+  for (int i = 0; i < P::NSUB; ++i) {
+    subz[i] = i < nsub ? p.sub_z(zg, i) : 0;
+    cum[i + 1] = cum[i] + (i < nsub ? p.nslabs(subz[i]) : 0);
+  }
+  const int ns = cum[P::NSUB];
+  float* As0 = lds;
+  float* As1 = lds + OA::FLOATS;
+  float* Bs0 = lds + 2 * OA::FLOATS;
+  float* Bs1 = Bs0 + OB::FLOATS;
+  f32x4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
+  auto load = [&](int s, f32x4(&ra)[NA], f32x4(&rb)[NB]) {
+    int i = 0;
+#pragma unroll
+    for (int j = 1; j < P::NSUB; ++j) i += s >= cum[j] ? 1 : 0;
+    const int z = subz[i], sl = s - cum[i];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int idx = tid + q * T;
+      if (OA::F4 % T == 0 || idx < OA::F4) {
+        int r, k;
+        OA::coord(idx, r, k);
+        ra[q] = p.ldA(z, sl, row0 + r, k);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int idx = tid + q * T;
+      if (OB::F4 % T == 0 || idx < OB::F4) {
+        int r, k;
+        OB::coord(idx, r, k);
+        rb[q] = p.ldB(z, sl, col0 + r, k);
+      }
+    }
+  };
+  auto store = [&](int s, const f32x4(&ra)[NA], const f32x4(&rb)[NB]) {
+    float* as = (s & 1) ? As1 : As0;
+    float* bs = (s & 1) ? Bs1 : Bs0;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int idx = tid + q * T;
+      if (OA::F4 % T == 0 || idx < OA::F4) {
+        int r, k;
+        OA::coord(idx, r, k);
+        OA::put(as, r, k, ra[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int idx = tid + q * T;
+      if (OB::F4 % T == 0 || idx < OB::F4) {
+        int r, k;
+        OB::coord(idx, r, k);
+        OB::put(bs, r, k, rb[q]);
+      }
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  auto compute = [&](int s) {
+    const float* a = (s & 1) ? As1 : As0;
+    const float* b = (s & 1) ? Bs1 : Bs0;
+    if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
+#pragma unroll
+    for (int kk = 0; kk < BK / OA::KG; ++kk) {
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  int cur = 0;   // sub-tile of the slab being multiplied
+  auto flush = [&](int s) {   // after slab s: the sub-tile ends there -> epilogue, fresh accumulators
+    if (s + 1 != cum[cur + 1]) return;
+    const int z = subz[cur];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
+        acc[i][j] = zero4();
+      }
+    ++cur;
+  };
+  auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
+    load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
+    if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);
+    compute(s);
+    flush(s);
+    if (s + 1 < ns) store(s + 1, xa, xb);
+    lds_barrier();
+  };
+  if (ns > 0) {
+    load(0, ra1, rb1);
+    store(0, ra1, rb1);
+    load(ns > 1 ? 1 : 0, ra0, rb0);
+    lds_barrier();
+    for (int s = 0; s < ns; s += 2) {
+      iter(s, ra0, rb0, ra1, rb1);
+      if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
+    }
+  }
+}
+
 // a policy with RAW_ORDER = true takes its blocks in hardware order (no XCD grouping)
 template <class P, class = void>
 struct RawOrder : std::false_type {};
@@ -355,10 +493,21 @@ struct Grid {
   __host__ __device__ int blocks() const { return tiles_m * tiles_n * nz; }
 };
 
+// a policy with NSUB (chained sub-tiles per block) runs gemm_body_chain
+template <class P, class = void>
+struct HasChain : std::false_type {};
+template <class P>
+struct HasChain<P, std::void_t<decltype(P::NSUB)>> : std::true_type {};
+template <class P>
+__device__ __forceinline__ void body(const P& p, int lb, float* lds) {
+  if constexpr (HasChain<P>::value) gemm_body_chain(p, lb, lds);
+  else gemm_body(p, lb, lds);
+}
+
 template <class P>
 __global__ __launch_bounds__(threads_of<P>()) void k_gemm32(const P p) {
   extern __shared__ float lds[];
-  gemm_body(p, block_order<P>(blockIdx.x, gridDim.x), lds);
+  body(p, block_order<P>(blockIdx.x, gridDim.x), lds);
 }
 
 // two independent GEMMs in one grid (hardware blocks [S::BLOCKS, S::BLOCKS + G1) run P1), plus `side` leading blocks
@@ -373,8 +522,8 @@ __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, c
   // tiles - dispatched first); inside each problem the XCD-grouped tile order
   const int G = gridDim.x - S::BLOCKS, h = b - S::BLOCKS;
   const int g1 = p1.g.blocks();
-  if (h < g1) gemm_body(p1, block_order<P1>(h, g1), lds);
-  else gemm_body(p2, block_order<P2>(h - g1, G - g1), lds);
+  if (h < g1) body(p1, block_order<P1>(h, g1), lds);
+  else body(p2, block_order<P2>(h - g1, G - g1), lds);
 }
 
 struct NoSide {
@@ -561,7 +710,7 @@ __host__ __device__ inline int px3_order(int z) { return z < 5 ? z + 2 : (z == 5
 __host__ __device__ inline int px2_order(int z) { return z < 8 ? z + 1 : (z == 8 ? 0 : 9); }
 
 // conv3 backward-data, pixel-major: z = pixel (ih, iw) of the 9 x 9 grid; rows b; k = valid (kh, kw) x oc
-template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, bool DIRECT = false>
 struct PConv3DgradPx {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool LOAD_FENCE = false;
@@ -578,8 +727,8 @@ struct PConv3DgradPx {
   };
   __host__ __device__ static Px px(int z) {
     Px q;
-    q.ih = px3_order(z / 9);
-    q.iw = px3_order(z % 9);
+    q.ih = DIRECT ? z / 9 : px3_order(z / 9);   // DIRECT: z = ih * 9 + iw
+    q.iw = DIRECT ? z % 9 : px3_order(z % 9);
     q.kh0 = q.ih > 6 ? q.ih - 6 : 0;
     q.kw0 = q.iw > 6 ? q.iw - 6 : 0;
     const int kh1 = q.ih < 2 ? q.ih : 2, kw1 = q.iw < 2 ? q.iw : 2;
@@ -612,7 +761,7 @@ struct PConv3DgradPx {
 // conv2 backward-data, pixel-major over the class grid: z = (i, j) of 10 x 10; rows b; cols (py, px, c) = 128 (the four
 // output parity classes share the A operand: dz2[b][i - th][j - tw]); k = valid (th, tw) x oc, which is the valid
 // (kh = py + 2 th, kw = px + 2 tw, oc) lexicographic order of every class
-template <int BM_ = 32, int BN_ = 128, int WM_ = 2, int WN_ = 2>
+template <int BM_ = 32, int BN_ = 128, int WM_ = 2, int WN_ = 2, bool DIRECT = false>
 struct PConv2DgradPx {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false, RAW_ORDER = true;
@@ -628,8 +777,8 @@ struct PConv2DgradPx {
   };
   __host__ __device__ static Px px(int z) {
     Px q;
-    q.i = px2_order(z / 10);
-    q.j = px2_order(z % 10);
+    q.i = DIRECT ? z / 10 : px2_order(z / 10);   // DIRECT: z = i * 10 + j
+    q.j = DIRECT ? z % 10 : px2_order(z % 10);
     q.th0 = q.i == 9 ? 1 : 0;
     q.tw0 = q.j == 9 ? 1 : 0;
     const int th1 = q.i == 0 ? 0 : 1, tw1 = q.j == 0 ? 0 : 1;
@@ -658,6 +807,56 @@ struct PConv2DgradPx {
         const size_t o = ((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31);
         dz1[o] = a1[o] > 0.0f ? v[r] : 0.0f;
       }
+  }
+};
+
+// Pixel-major backward data with balanced pixel groups (chained sub-tiles, gemm_body_chain): a block runs a group of
+// pixels whose valid taps add up to a full tile's - conv3: 9 taps (interior pixels alone; a 6-tap edge pixel with its
+// 3-tap neighbour; per corner quadrant the 4 + 2 + 2 + 1 taps), 49 groups of 18 slabs; conv2: 4 taps over the 10 x 10 class
+// grid (interior alone; 2-tap edge pixels in pairs; the four 1-tap corners together), 81 groups of 8 slabs.  Every pixel
+// keeps its own chain (valid taps lexicographic), so dz is bit-identical to the one-pixel tiles.
+template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PConv3DgradPxG : PConv3DgradPx<BM_, BN_, WM_, WN_, true> {
+  static constexpr int NSUB = 4, GROUPS = 49;
+  static constexpr bool RAW_ORDER = false;   // groups are equal: XCD-grouped order (a group's tiles share W2 taps in L2)
+  __host__ __device__ static int sub_count(int g) { return g < 25 ? 1 : (g < 45 ? 2 : 4); }
+  __host__ __device__ static int sub_z(int g, int i) {
+    int ih, iw;
+    if (g < 25) {
+      ih = 2 + g / 5; iw = 2 + g % 5;
+    } else if (g < 35) {   // (ih, 1) + (ih, 0) or (ih, 7) + (ih, 8)
+      const int t = g - 25;
+      ih = 2 + t / 2;
+      iw = (t & 1) ? 7 + i : 1 - i;
+    } else if (g < 45) {   // (1, iw) + (0, iw) or (7, iw) + (8, iw)
+      const int t = g - 35;
+      iw = 2 + t / 2;
+      ih = (t & 1) ? 7 + i : 1 - i;
+    } else {               // quadrant (a, b), (edge, b), (a, edge), (edge, edge)
+      const int q = g - 45, a = (q & 2) ? 7 : 1, b = (q & 1) ? 7 : 1;
+      ih = (i & 1) ? (a == 1 ? 0 : 8) : a;
+      iw = (i & 2) ? (b == 1 ? 0 : 8) : b;
+    }
+    return ih * 9 + iw;
+  }
+};
+template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PConv2DgradPxG : PConv2DgradPx<BM_, BN_, WM_, WN_, true> {
+  static constexpr int NSUB = 4, GROUPS = 81;
+  static constexpr bool RAW_ORDER = false;
+  __host__ __device__ static int sub_count(int g) { return g < 64 ? 1 : (g < 80 ? 2 : 4); }
+  __host__ __device__ static int sub_z(int g, int i) {
+    int ci, cj;
+    if (g < 64) {
+      ci = 1 + g / 8; cj = 1 + g % 8;
+    } else if (g < 80) {
+      const int t = g - 64, u = t >> 1, side = t & 1;
+      if (u < 4) { ci = side ? 9 : 0; cj = 1 + 2 * u + i; }
+      else { cj = side ? 9 : 0; ci = 1 + 2 * (u - 4) + i; }
+    } else {
+      ci = (i & 2) ? 9 : 0; cj = (i & 1) ? 9 : 0;
+    }
+    return ci * 10 + cj;
   }
 };
 

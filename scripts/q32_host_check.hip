@@ -33,8 +33,13 @@ static void replay(const P& p, const char* name) {
   constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
   volatile float sink = 0.0f;
   for (int lb = 0; lb < p.g.blocks(); ++lb) {
-    int tm, tn, z;
-    p.decode(lb, tm, tn, z);
+    int tm, tn, zg;
+    p.decode(lb, tm, tn, zg);
+    int nsub = 1;
+    if constexpr (HasChain<P>::value) nsub = p.sub_count(zg);
+    for (int si = 0; si < nsub; ++si) {
+    int z = zg;
+    if constexpr (HasChain<P>::value) z = p.sub_z(zg, si);
     const int row0 = tm * P::BM, col0 = tn * P::BN;
     const int ns = p.nslabs(z);
     for (int s = 0; s < ns; ++s) {
@@ -70,12 +75,32 @@ static void replay(const P& p, const char* name) {
       if (tm == 0)
         for (int t = 0; t < P::BN; ++t) p.epi_bias(z, col0 + t, 0.0f);
     }
+    }
   }
   printf("%-14s blocks %6d ok\n", name, p.g.blocks());
 }
 
 template <class T>
 static T* buf(size_t n) { return static_cast<T*>(std::calloc(n, sizeof(T))); }
+
+// a grouped pixel policy covers every pixel exactly once, and each group's taps add up to `taps`
+template <class P>
+static void check_groups(int npx, int taps, const char* name) {
+  std::vector<int> hits(npx, 0);
+  for (int g = 0; g < P::GROUPS; ++g) {
+    int t = 0;
+    for (int i = 0; i < P::sub_count(g); ++i) {
+      const int z = P::sub_z(g, i);
+      if (z < 0 || z >= npx) { printf("%s: group %d pixel %d out of range\n", name, g, z); exit(1); }
+      hits[z] += 1;
+      t += P::px(z).ntap;
+    }
+    if (t != taps) { printf("%s: group %d has %d taps\n", name, g, t); exit(1); }
+  }
+  for (int z = 0; z < npx; ++z)
+    if (hits[z] != 1) { printf("%s: pixel %d covered %d times\n", name, z, hits[z]); exit(1); }
+  printf("%-14s groups %d cover %d pixels once, %d taps each\n", name, P::GROUPS, npx, taps);
+}
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 32;       // training batch
@@ -117,11 +142,15 @@ int main(int argc, char** argv) {
   replay(PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad");
   replay(PConv3DgradS{grid(B * 81, 32, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad S");
   replay(PConv3DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 1, 81}, dz3, w2, a2, dz2, B}, "conv3_dgrad px");
+  check_groups<PConv3DgradPxG<>>(81, 9, "conv3 groups");
+  replay(PConv3DgradPxG<32, 64, 2, 2>{{Grid{(B + 31) / 32, 1, 49}, dz3, w2, a2, dz2, B}}, "conv3_dgrad pxg");
   replay(PConv3Wgrad{grid(576, 64, 64, 64, z3), a2, dz3, s3, B}, "conv3_wgrad");
   replay(PConv2Dgrad{grid(B * 100, PConv2Dgrad::BM, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad");
   replay(PConv2DgradS{grid(B * 100, 64, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad S");
   replay(PConv2DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px");
   replay(PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px 64");
+  check_groups<PConv2DgradPxG<>>(100, 4, "conv2 groups");
+  replay(PConv2DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 2, 81}, dz2, w1, a1, dz1, B}}, "conv2_dgrad pxg");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
   printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
   return 0;

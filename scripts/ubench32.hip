@@ -344,6 +344,32 @@ int main(int argc, char** argv) {
   const float* W1 = w + 8192 + 32;
   const float* W2 = W1 + 32768 + 64;
   const float* W3 = W2 + 36864 + 64;
+  if (argc > 1 && std::string(argv[1]) == "bwd") {   // pixel-major backward data: one pixel per tile vs pixel groups
+    for (int B : {1024, 8192}) {
+      const double f3 = 2.0 * B * 49 * 64 * 576, f2 = 2.0 * B * 81 * 64 * 512;
+      const int z3 = B / 16, z2 = B / 16;
+      printf("--- B = %d\n", B);
+      run1("conv3_dgrad px t32x64", PConv3DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 1, 81}, dz3, W2, a2, dz2, B}, f3);
+      run1("conv3_dgrad pxg t32x64", PConv3DgradPxG<32, 64, 2, 2>{{Grid{(B + 31) / 32, 1, 49}, dz3, W2, a2, dz2, B}}, f3);
+      run1("conv3_dgrad pxg t64x64", PConv3DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 1, 49}, dz3, W2, a2, dz2, B}}, f3);
+      run1("conv3_dgrad pxg t32x32", PConv3DgradPxG<32, 32, 2, 2>{{Grid{(B + 31) / 32, 2, 49}, dz3, W2, a2, dz2, B}}, f3);
+      run1("conv3_wgrad sc16", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, z3), a2, dz3, slab, B}, f3);
+      run2("conv3 pair px", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, z3), a2, dz3, slab, B},
+           PConv3DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 1, 81}, dz3, W2, a2, dz2, B}, 2 * f3);
+      run2("conv3 pair pxg", PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, z3), a2, dz3, slab, B},
+           PConv3DgradPxG<32, 64, 2, 2>{{Grid{(B + 31) / 32, 1, 49}, dz3, W2, a2, dz2, B}}, 2 * f3);
+      run1("conv2_dgrad px t64x64", PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, W1, a1, dz1, B}, f2);
+      run1("conv2_dgrad pxg t64x64", PConv2DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 2, 81}, dz2, W1, a1, dz1, B}}, f2);
+      run1("conv2_dgrad pxg t32x64", PConv2DgradPxG<32, 64, 2, 2>{{Grid{(B + 31) / 32, 2, 81}, dz2, W1, a1, dz1, B}}, f2);
+      run1("conv2_wgrad sc16", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, z2), a1, dz2, slab, B}, f2);
+      run2("conv2 pair px", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, z2), a1, dz2, slab, B},
+           PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, W1, a1, dz1, B}, 2 * f2);
+      run2("conv2 pair pxg", PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, z2), a1, dz2, slab, B},
+           PConv2DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 2, 81}, dz2, W1, a1, dz1, B}}, 2 * f2);
+      if (B > 1024) break;
+    }
+    return 0;
+  }
   for (int B : Bs) {
     printf("--- B = %d\n", B);
     {
