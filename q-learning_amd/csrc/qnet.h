@@ -38,7 +38,6 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float *fdz1 = nullptr, *fdz2 = nullptr, *fdz3 = nullptr, *fdz4 = nullptr;
   float *fslab1 = nullptr, *fslab2 = nullptr, *fslab3 = nullptr;
   float* fpart = nullptr;   // clip_by_norm segment partials
-  unsigned* fnorm_count = nullptr;   // k_norm32's finished-block counter (zero between launches)
   int fchunk = 0;
   void* fgrad = nullptr;
   int fgrad_batch = 0;

@@ -170,24 +170,20 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R) {
 
 // clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg = 2048;
 // thread t chains t = fmaf(x, x, t) over its elements j S + 4 t .. + 3, then j S + 1024 + 4 t .. + 3 (x = g * scale);
-// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  The last block to finish (a device-scope
-// counter) reduces the partials to the ten norms: norm_v from 64 lane chains over its partials j = lane mod 64 ascending
-// and one xor butterfly, so k_adam32 starts from ten finished values (one load) instead of every Adam block re-reducing
-// ~830 partials in three dependent load rounds.
+// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  Norm_v from its partials in k_adam32.
+// (Measured and reverted: the last block to finish - a device-scope counter - reducing the partials to the ten norms, so
+// Adam loads ten values: Adam 16.3 -> 12.5 us, but the per-block release fence took k_norm32 6.2 -> 24.6 us.)
 constexpr int kNormSeg = 2048;
-constexpr int kNormSegMax = 1024;   // partials per variable the final reduction takes (16 per lane)
+constexpr int kNormSegMax = 832;   // partials per variable (13 per lane; W3 has 784)
 struct NormArgs {
   const float* g;
   float scale;
   float* partial;
-  unsigned* count;   // zero between launches (the last block resets it)
-  float* norms;
   int seg_first[kNumVars + 1];
   int64_t off[kNumVars + 1];
 };
 __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   __shared__ float wsum[4];
-  __shared__ int last;
   int v = 0;
   while (v < kNumVars - 1 && (int)blockIdx.x >= A.seg_first[v + 1]) ++v;
   const int j = blockIdx.x - A.seg_first[v];
@@ -216,30 +212,7 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    // the partial goes out device-coherent, then the counter (acquire-release at agent scope: the last block sees every
-    // other block's partial)
-    __hip_atomic_store(A.partial + blockIdx.x, __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned prev = __hip_atomic_fetch_add(A.count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int v = wave; v < kNumVars; v += 4) {
-    const int first = A.seg_first[v], cnt = A.seg_first[v + 1] - first;
-    float x[kNormSegMax / 64];
-#pragma unroll
-    for (int i = 0; i < kNormSegMax / 64; ++i)
-      x[i] = lane + 64 * i < cnt ? __hip_atomic_load(A.partial + first + lane + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
-    float s = 0.0f;
-#pragma unroll
-    for (int i = 0; i < kNormSegMax / 64; ++i) s = __fadd_rn(s, x[i]);
-    for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o));
-    if (lane == 0) A.norms[v] = s > 0.0f ? sqrtf(s) : s;   // safe sqrt via where(l2sum > 0)
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(A.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) A.partial[blockIdx.x] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]);
 }
 
 struct Adam32Args {
@@ -247,8 +220,10 @@ struct Adam32Args {
   float* m;
   float* v;
   const float* g;
+  const float* partial;
+  int seg_first[kNumVars + 1];
   int64_t off[kNumVars + 1];
-  const float* norms;   // k_norm32's ten clip norms
+  float* norms;
   float scale, alpha, beta1, beta2, eps, clipnorm;
 };
 
@@ -271,7 +246,35 @@ __device__ __forceinline__ int var_of(const Adam32Args& A, int64_t i) {
 
 __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
   __shared__ float nrm[kNumVars];
-  if (threadIdx.x < kNumVars) nrm[threadIdx.x] = A.norms[threadIdx.x];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave == 0) {
+    // norm_v: lane chain over the partials lane, lane + 64, ... of v (zeros past the end), then the xor butterfly.  Every
+    // partial of all ten variables is loaded at once (13 for W3 + 1 per smaller variable per lane: one memory round).
+    float x[kNormSegMax / 64], y[kNumVars];
+    const int f6 = A.seg_first[6], c6 = A.seg_first[7] - f6;
+#pragma unroll
+    for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < c6 ? A.partial[f6 + lane + 64 * i] : 0.0f;
+#pragma unroll
+    for (int v = 0; v < kNumVars; ++v) {
+      const int f = A.seg_first[v], c = A.seg_first[v + 1] - f;
+      y[v] = v != 6 && lane < c ? A.partial[f + lane] : 0.0f;   // every variable but W3 has <= 64 partials
+    }
+#pragma unroll
+    for (int v = 0; v < kNumVars; ++v) {
+      float t = 0.0f;
+      if (v == 6) {
+#pragma unroll
+        for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
+      } else {
+        t = __fadd_rn(t, y[v]);
+      }
+      for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+      if (lane == 0) {
+        nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
+        if (blockIdx.x == 0) A.norms[v] = nrm[v];
+      }
+    }
+  }
   __syncthreads();
   // four elements per thread and step (16-byte accesses; every variable but the last starts at a multiple of 4, so a
   // group never straddles two variables; the last group is finished element by element)
@@ -315,6 +318,8 @@ using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
 static_assert((1605632 + kNormSeg - 1) / kNormSeg <= kNormSegMax, "norm partials per variable");
+static_assert((512 * 3 + kNormSeg - 1) / kNormSeg <= 64 && (32768 + kNormSeg - 1) / kNormSeg <= 64 &&
+              (36864 + kNormSeg - 1) / kNormSeg <= 64 && (8192 + kNormSeg - 1) / kNormSeg <= 64, "<= 64 partials but W3");
 
 void f32_workspace(qlx_model* m, int B) {
   if (B <= m->ws_batch) return;
@@ -335,7 +340,6 @@ void f32_workspace(qlx_model* m, int B) {
   for (int v = 0; v < kNumVars; ++v) nseg += segs_of(v);
   const size_t o_part = take((size_t)nseg * 4);
   const size_t o_loss = take(64);
-  const size_t o_count = take(64);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -347,8 +351,6 @@ void f32_workspace(qlx_model* m, int B) {
   w.done = (uint8_t*)(base + o_done);
   w.fpart = (float*)(base + o_part);
   w.loss = (float*)(base + o_loss);
-  w.fnorm_count = (unsigned*)(base + o_count);
-  QLX_HIP(hipMemset(w.fnorm_count, 0, 64));
   w.fchunk = C;
   m->ws_batch = B;
 }
@@ -499,7 +501,9 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   // algorithmic FLOPs (backward-data + weight gradient of the layer; the pixel-major dgrad tiles multiply only the
   // valid taps, so MFMA work = algorithmic work)
-  // pixel-major backward data as balanced pixel groups (chained sub-tiles; QLX_F32_PXG=0: one pixel per tile)
+  // conv3 pixel-major backward data as balanced pixel groups (chained sub-tiles; QLX_F32_PXG=0: one pixel per tile).  conv2
+  // keeps one pixel per tile: grouped, its dgrad ran 71 -> 97 us (scripts/ubench32.hip bwd; its 8-slab sub-tiles pay
+  // the in-loop epilogue's wait on the slab loads in flight, where conv3's 18-slab groups gain: pair 104.6 -> 97.6 us)
   static const bool pxg = [] { const char* e = std::getenv("QLX_F32_PXG"); return !(e && e[0] == '0'); }();
   {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
@@ -513,13 +517,8 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
-    if (pxg) {
-      PConv2DgradPxG<64, 64, 2, 2> Pd{{Grid{(B + 63) / 64, 2, PConv2DgradPxG<>::GROUPS}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B}};
-      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
-    } else {
-      PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
-      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
-    }
+    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
+    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
     constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
@@ -563,8 +562,6 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
   A.g = m->d_grads;
   A.scale = scale;
   A.partial = m->w.fpart;
-  A.count = m->w.fnorm_count;
-  A.norms = m->d_norms;
   seg_tables(A.seg_first, A.off);
   hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
   QLX_HIP(hipGetLastError());
@@ -576,9 +573,8 @@ void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const float tf = (float)t;
   const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
   Adam32Args a;
-  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.norms = m->d_norms;
-  int seg_first[kNumVars + 1];
-  seg_tables(seg_first, a.off);
+  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.partial = m->w.fpart; a.norms = m->d_norms;
+  seg_tables(a.seg_first, a.off);
   a.scale = scale;
   a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;

@@ -335,12 +335,19 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
 // sub-tile's last slab its accumulators go through P::epi and restart from zero.  Each output is still one chain over its
 // own tile's slabs in order, so the results equal gemm_body's on the same tiles bit for bit.  For short-K tiles (pixel-major
 // backward data: 1..9 valid taps) this removes the per-tile pipeline ramp and epilogue wait that dominate a short tile.
+// The sub-tile queue is kept as shifting scalars (no runtime-indexed arrays or captured references: those end up in
+// scratch memory): a load cursor and an epilogue cursor each advance through (z_i, end slab e_i) in order.
+struct ChainQ {
+  int z0, e0, z1, e1, z2, e2, z3, e3;
+  __device__ __forceinline__ void pop() { z0 = z1; e0 = e1; z1 = z2; e1 = e2; z2 = z3; e2 = e3; }
+};
 template <class P>
 __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) {
   constexpr int MF = 16;
   using OA = Opnd<P::BM, P::A_KMAJ, MF>;
   using OB = Opnd<P::BN, P::B_KMAJ, MF>;
   static_assert(KSplitOf<P>::value == 1 && !P::BIAS && !HasACtx<P>::value, "chained tiles: plain policies");
+  static_assert(P::NSUB == 4, "chained tiles: up to four sub-tiles");
   constexpr int T = P::WM * P::WN * 64;
   constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
   static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
@@ -351,42 +358,47 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
   int tm, tn, zg;
   p.decode(lb, tm, tn, zg);
   const int row0 = tm * P::BM, col0 = tn * P::BN;
-  // sub-tile table (block-uniform): z and the first global slab of each sub-tile
   const int nsub = p.sub_count(zg);
-  int subz[P::NSUB], cum[P::NSUB + 1];
-  cum[0] = 0;
-#pragma unroll
-  for (int i = 0; i < P::NSUB; ++i) {
-    subz[i] = i < nsub ? p.sub_z(zg, i) : 0;
-    cum[i + 1] = cum[i] + (i < nsub ? p.nslabs(subz[i]) : 0);
-  }
-  const int ns = cum[P::NSUB];
+  ChainQ q;
+  q.z0 = p.sub_z(zg, 0);
+  q.z1 = nsub > 1 ? p.sub_z(zg, 1) : q.z0;
+  q.z2 = nsub > 2 ? p.sub_z(zg, 2) : q.z0;
+  q.z3 = nsub > 3 ? p.sub_z(zg, 3) : q.z0;
+  q.e0 = p.nslabs(q.z0);
+  q.e1 = q.e0 + (nsub > 1 ? p.nslabs(q.z1) : 0);
+  q.e2 = q.e1 + (nsub > 2 ? p.nslabs(q.z2) : 0);
+  q.e3 = q.e2 + (nsub > 3 ? p.nslabs(q.z3) : 0);
+  const int ns = q.e3;
+  ChainQ lq = q, fq = q;   // load cursor, epilogue cursor
+  int lbase = 0;           // first slab of lq's current sub-tile
   float* As0 = lds;
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
   float* Bs1 = Bs0 + OB::FLOATS;
   f32x4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
+  // slab s of the concatenation (s never decreases between calls; past the end the last slab again)
   auto load = [&](int s, f32x4(&ra)[NA], f32x4(&rb)[NB]) {
-    int i = 0;
+    if (s >= lq.e0 && s < ns) {
+      lbase = lq.e0;
+      lq.pop();
+    }
+    const int z = lq.z0, sl = s - lbase;
 #pragma unroll
-    for (int j = 1; j < P::NSUB; ++j) i += s >= cum[j] ? 1 : 0;
-    const int z = subz[i], sl = s - cum[i];
-#pragma unroll
-    for (int q = 0; q < NA; ++q) {
-      const int idx = tid + q * T;
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T;
       if (OA::F4 % T == 0 || idx < OA::F4) {
         int r, k;
         OA::coord(idx, r, k);
-        ra[q] = p.ldA(z, sl, row0 + r, k);
+        ra[i] = p.ldA(z, sl, row0 + r, k);
       }
     }
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const int idx = tid + q * T;
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + i * T;
       if (OB::F4 % T == 0 || idx < OB::F4) {
         int r, k;
         OB::coord(idx, r, k);
-        rb[q] = p.ldB(z, sl, col0 + r, k);
+        rb[i] = p.ldB(z, sl, col0 + r, k);
       }
     }
   };
@@ -394,21 +406,21 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
     float* as = (s & 1) ? As1 : As0;
     float* bs = (s & 1) ? Bs1 : Bs0;
 #pragma unroll
-    for (int q = 0; q < NA; ++q) {
-      const int idx = tid + q * T;
+    for (int i = 0; i < NA; ++i) {
+      const int idx = tid + i * T;
       if (OA::F4 % T == 0 || idx < OA::F4) {
         int r, k;
         OA::coord(idx, r, k);
-        OA::put(as, r, k, ra[q]);
+        OA::put(as, r, k, ra[i]);
       }
     }
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const int idx = tid + q * T;
+    for (int i = 0; i < NB; ++i) {
+      const int idx = tid + i * T;
       if (OB::F4 % T == 0 || idx < OB::F4) {
         int r, k;
         OB::coord(idx, r, k);
-        OB::put(bs, r, k, rb[q]);
+        OB::put(bs, r, k, rb[i]);
       }
     }
   };
@@ -434,10 +446,10 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   };
-  int cur = 0;   // sub-tile of the slab being multiplied
-  auto flush = [&](int s) {   // after slab s: the sub-tile ends there -> epilogue, fresh accumulators
-    if (s + 1 != cum[cur + 1]) return;
-    const int z = subz[cur];
+  // after slab s: the epilogue of a sub-tile ending there, fresh accumulators
+  auto flush = [&](int s) {
+    if (s + 1 != fq.e0) return;
+    const int z = fq.z0;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -445,7 +457,7 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
         p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
         acc[i][j] = zero4();
       }
-    ++cur;
+    fq.pop();
   };
   auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
     load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
