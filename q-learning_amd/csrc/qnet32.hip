@@ -244,65 +244,71 @@ __device__ __forceinline__ int var_of(const Adam32Args& A, int64_t i) {
   return v;
 }
 
+// One float4 group (16-byte accesses) per thread: the grid covers count / 4 groups plus the tail group (elements past the
+// last full group, finished element by element).  Every variable but the last starts at a multiple of 4, so a group never
+// straddles two variables.  The group's g / w / m / v loads are issued first; wave 0 then loads all the clip-norm
+// partials (13 per lane for W3, one for each smaller variable: one memory round) and finishes the ten norms while the
+// element loads are in flight.
 __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
   __shared__ float nrm[kNumVars];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t count = A.off[kNumVars], n4 = count / 4;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, i0 = q * 4;
+  f32x4 g = zero4(), w = zero4(), m = zero4(), v = zero4();
+  if (q < n4) {
+    g = ld4(A.g + i0);
+    w = ld4(A.w + i0);
+    m = ld4(A.m + i0);
+    v = ld4(A.v + i0);
+  }
   if (wave == 0) {
-    // norm_v: lane chain over the partials lane, lane + 64, ... of v (zeros past the end), then the xor butterfly.  Every
-    // partial of all ten variables is loaded at once (13 for W3 + 1 per smaller variable per lane: one memory round).
+    // norm_v: lane chain over the partials lane, lane + 64, ... of v (zeros past the end), then the xor butterfly
     float x[kNormSegMax / 64], y[kNumVars];
     const int f6 = A.seg_first[6], c6 = A.seg_first[7] - f6;
 #pragma unroll
     for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < c6 ? A.partial[f6 + lane + 64 * i] : 0.0f;
 #pragma unroll
-    for (int v = 0; v < kNumVars; ++v) {
-      const int f = A.seg_first[v], c = A.seg_first[v + 1] - f;
-      y[v] = v != 6 && lane < c ? A.partial[f + lane] : 0.0f;   // every variable but W3 has <= 64 partials
+    for (int vv = 0; vv < kNumVars; ++vv) {
+      const int f = A.seg_first[vv], c = A.seg_first[vv + 1] - f;
+      y[vv] = vv != 6 && lane < c ? A.partial[f + lane] : 0.0f;   // every variable but W3 has <= 64 partials
     }
 #pragma unroll
-    for (int v = 0; v < kNumVars; ++v) {
+    for (int vv = 0; vv < kNumVars; ++vv) {
       float t = 0.0f;
-      if (v == 6) {
+      if (vv == 6) {
 #pragma unroll
         for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
       } else {
-        t = __fadd_rn(t, y[v]);
+        t = __fadd_rn(t, y[vv]);
       }
       for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
       if (lane == 0) {
-        nrm[v] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
-        if (blockIdx.x == 0) A.norms[v] = nrm[v];
+        nrm[vv] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
+        if (blockIdx.x == 0) A.norms[vv] = nrm[vv];
       }
     }
   }
   __syncthreads();
-  // four elements per thread and step (16-byte accesses; every variable but the last starts at a multiple of 4, so a
-  // group never straddles two variables; the last group is finished element by element)
-  const int64_t count = A.off[kNumVars], n4 = count / 4;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= n4; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i0 = q * 4;
-    if (q < n4) {
-      const float denom = fmaxf(nrm[var_of(A, i0)], A.clipnorm);
-      const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
-      f32x4 m = ld4(A.m + i0), v = ld4(A.v + i0), o;
+  if (q < n4) {
+    const float denom = fmaxf(nrm[var_of(A, i0)], A.clipnorm);
+    f32x4 o;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float mk = m[k], vk = v[k];
-        o[k] = adam32_elem(g[k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[k]);
-        m[k] = mk;
-        v[k] = vk;
-      }
-      *reinterpret_cast<f32x4*>(A.w + i0) = o;
-      *reinterpret_cast<f32x4*>(A.m + i0) = m;
-      *reinterpret_cast<f32x4*>(A.v + i0) = v;
-    } else {
-      for (int64_t i = i0; i < count; ++i) {
-        const float denom = fmaxf(nrm[var_of(A, i)], A.clipnorm);
-        float m = A.m[i], v = A.v[i];
-        A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
-        A.m[i] = m;
-        A.v[i] = v;
-      }
+    for (int k = 0; k < 4; ++k) {
+      float mk = m[k], vk = v[k];
+      o[k] = adam32_elem(g[k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[k]);
+      m[k] = mk;
+      v[k] = vk;
+    }
+    *reinterpret_cast<f32x4*>(A.w + i0) = o;
+    *reinterpret_cast<f32x4*>(A.m + i0) = m;
+    *reinterpret_cast<f32x4*>(A.v + i0) = v;
+  } else if (q == n4) {
+    for (int64_t i = i0; i < count; ++i) {
+      const float denom = fmaxf(nrm[var_of(A, i)], A.clipnorm);
+      float mi = A.m[i], vi = A.v[i];
+      A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mi, vi, A.w[i]);
+      A.m[i] = mi;
+      A.v[i] = vi;
     }
   }
 }
@@ -579,8 +585,8 @@ void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
   ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
-  const int64_t groups = kNumParams / 4 + 1;   // float4 groups + the tail group
-  hipLaunchKernelGGL(k_adam32, dim3((unsigned)std::min<int64_t>(2048, (groups + 255) / 256)), dim3(256), 0, s, a);
+  const int64_t groups = kNumParams / 4 + 1;   // float4 groups + the tail group: one per thread
+  hipLaunchKernelGGL(k_adam32, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, a);
   QLX_HIP(hipGetLastError());
   debug_sync(s, "k_adam32");
   m->iterations = t;

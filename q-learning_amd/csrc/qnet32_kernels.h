@@ -39,20 +39,32 @@ __host__ __device__ constexpr int kmaj_pitch(int rows, int mf) {
 static_assert(kmaj_pitch(32, 16) == 48 && kmaj_pitch(64, 16) == 80 && kmaj_pitch(128, 16) == 144 && kmaj_pitch(64, 32) == 96,
               "KMAJ pitches");
 
+// RMAJ with MF 16 (SWZ): rows with bit 3 set hold their k in the order k ^ 2 (the two k pairs of each float4 swapped).
+// ds_read_b32 is serviced in two 32-lane groups on 32 banks, (address / 4) mod 32: a fragment read's group is 16 rows x
+// 2 k, and with pitch 36 alone rows i and i + 8 land on one bank (2-way on every read); swapped, the group covers 32
+// distinct banks, and the float4 stores stay 16-byte (the swap is a register permutation).
 template <int ROWS, bool KMAJ, int MF = 16>
 struct Opnd {
   static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS, MF) : BK + 4;
   static constexpr int FLOATS = KMAJ ? BK * PITCH : ROWS * PITCH;
   static constexpr int F4 = ROWS * BK / 4;   // float4 per slab
   static constexpr int KG = 64 / MF;         // k per MFMA (lane groups)
+#ifdef QLX_Q32_NO_SWZ
+  static constexpr bool SWZ = false;
+#else
+  static constexpr bool SWZ = !KMAJ && MF == 16;
+#endif
   __host__ __device__ static void coord(int idx, int& row, int& k) {
     if (KMAJ) { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
     else { row = idx >> 3; k = (idx & 7) * 4; }
   }
   __device__ static void put(float* t, int row, int k, f32x4 v) {
+    if (SWZ && (row & 8)) v = f32x4{v[2], v[3], v[0], v[1]};
     *reinterpret_cast<f32x4*>(t + (KMAJ ? k * PITCH + row : row * PITCH + k)) = v;
   }
-  __device__ static float at(const float* t, int row, int k) { return KMAJ ? t[k * PITCH + row] : t[row * PITCH + k]; }
+  __device__ static float at(const float* t, int row, int k) {
+    return KMAJ ? t[k * PITCH + row] : t[row * PITCH + (SWZ ? (k ^ ((row & 8) >> 2)) : k)];
+  }
   // MFMA operand of the MF rows from r0, k step kk: lane l holds (r0 + l % MF, KG kk + l / MF)
   __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & (MF - 1)), KG * kk + lane / MF); }
 };
