@@ -39,20 +39,22 @@ __host__ __device__ constexpr int kmaj_pitch(int rows, int mf) {
 static_assert(kmaj_pitch(32, 16) == 48 && kmaj_pitch(64, 16) == 80 && kmaj_pitch(128, 16) == 144 && kmaj_pitch(64, 32) == 96,
               "KMAJ pitches");
 
-// RMAJ with MF 16 (SWZ): rows with bit 3 set hold their k in the order k ^ 2 (the two k pairs of each float4 swapped).
-// ds_read_b32 is serviced in two 32-lane groups on 32 banks, (address / 4) mod 32: a fragment read's group is 16 rows x
-// 2 k, and with pitch 36 alone rows i and i + 8 land on one bank (2-way on every read); swapped, the group covers 32
-// distinct banks, and the float4 stores stay 16-byte (the swap is a register permutation).
+// RMAJ with MF 16 and QLX_Q32_SWZ defined (SWZ): rows with bit 3 set hold their k in the order k ^ 2 (the two k pairs of
+// each float4 swapped).  ds_read_b32 is serviced in two 32-lane groups on 32 banks, (address / 4) mod 32: a fragment
+// read's group is 16 rows x 2 k, and with pitch 36 alone rows i and i + 8 land on one bank (2-way on every read);
+// swapped, the group covers 32 distinct banks with the float4 stores kept 16-byte (a register permutation).  Measured at
+// C3 (round 3): slower - fc1 forward 39.0 -> 43.1 us, conv2 / conv3 forward +1.7 / +1.5 us, 198.6K -> 194.9K env-steps/s -
+// so the read conflicts are not what limits these loops; off by default.
 template <int ROWS, bool KMAJ, int MF = 16>
 struct Opnd {
   static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS, MF) : BK + 4;
   static constexpr int FLOATS = KMAJ ? BK * PITCH : ROWS * PITCH;
   static constexpr int F4 = ROWS * BK / 4;   // float4 per slab
   static constexpr int KG = 64 / MF;         // k per MFMA (lane groups)
-#ifdef QLX_Q32_NO_SWZ
-  static constexpr bool SWZ = false;
-#else
+#ifdef QLX_Q32_SWZ
   static constexpr bool SWZ = !KMAJ && MF == 16;
+#else
+  static constexpr bool SWZ = false;
 #endif
   __host__ __device__ static void coord(int idx, int& row, int& k) {
     if (KMAJ) { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
