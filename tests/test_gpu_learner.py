@@ -301,11 +301,17 @@ def test_end_episodes_is_the_truncation_path():
 
 
 def test_bf16_pure_random_phase_parity():
+    """bf16 learner against the oracle in lockstep: before every vector step the oracle's online net takes the product's
+    weights + Adam slots, so the first update of each step starts from identical state and its loss is held to a
+    per-update bound (the later updates of a step start from weights that bf16 gradient noise has already moved: Adam's
+    sign-like first steps turn it into full lr-sized steps); env, replay, sampling exact throughout."""
     N, B = 16, 32
     gpu, ref = make(N, B, prec=1, max_steps_per_episode=45)
+    ref_online = ref.qnet(0)
     n_updates = 0
     rel_errs = []
     for v in range(30):
+        ref_online.load_state_from(gpu.model)
         gpu.vector_step()
         ref.vector_step()
         g, r = gpu.last(), ref.last()
@@ -318,12 +324,13 @@ def test_bf16_pure_random_phase_parity():
             # the target net is never synced (reference behaviour): identical weights on both sides
             assert np.abs(tg - tr).max() <= 3e-2 * max(1.0, np.abs(tr).max()), f"targets @ {v}"
             assert np.isfinite(g["losses"]).all()
-            rel_errs.extend((np.abs(g["losses"] - r["losses"]) / np.maximum(np.abs(r["losses"]), 0.1)).tolist())
+            # lockstep: the step's first update; |dloss| <= 0.1 max(|loss|, 0.1) (the bf16 forward's Q error, <= 3e-2
+            # max|Q|, times the Huber gradient |e| <= 1 of the residual; the measured max is printed)
+            rel = abs(g["losses"][0] - r["losses"][0]) / max(abs(r["losses"][0]), 0.1)
+            rel_errs.append(rel)
+            assert rel <= 0.1, (v, g["losses"][0], r["losses"][0])
     assert n_updates > 50
-    # online weights drift apart after the first update (Adam's sign-like first steps turn bf16 gradient
-    # noise into full lr-sized steps), so per-update losses are checked in lockstep below; here only the
-    # trajectory is compared loosely
-    assert np.mean(rel_errs) <= 0.3, np.mean(rel_errs)
+    print("bf16 lockstep loss error, max / mean of max(|loss|, 0.1):", max(rel_errs), np.mean(rel_errs))
     sg, sr = gpu.stats(), ref.counters()
     for k in ("step_count", "update_count", "episode_count", "replay_len"):
         assert sg[k] == sr[k], k
