@@ -407,8 +407,8 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
   const float* isw = L->per ? L->prio.d_w + (size_t)u_local * B : nullptr;
   float* td = L->per ? L->prio.d_td + (size_t)u_local * B : nullptr;
   float scale = 1.0f;
-  if (!L->comm) {
-    model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td);
+  if (!L->comm) {   // no all-reduce: the fp32 path may run the norms / Adam inside the backward launches
+    model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td, true);
   } else if (!L->dp_overlap) {   // one all-reduce of the whole gradient on the learner stream
     model_backward(on, tab_s, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td);
     ProfScope ps(&L->prof, "allreduce", s);

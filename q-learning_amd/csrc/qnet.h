@@ -82,6 +82,14 @@ struct qlx_model {
   // conv1 weight gradient as channel-half blocks (k_conv1_wgrad_h); QLX_CONV1_HALVES=0 at create time selects the
   // one-block-per-chunk k_conv1_wgrad (bit-identical gradients)
   bool conv1_halves = true;
+  // fp32: clip_by_norm + Adam of the dense variables run inside the conv backward launches (their norm partials as
+  // trailing blocks of the conv3 pair, the update beside the conv2 pair's tiles) and the conv variables' in one small
+  // launch after the weight-gradient reduction, when the caller allows it (no all-reduce between backward and Adam);
+  // QLX_F32_FUSED_ADAM=0 at create time keeps the separate k_norm32 + k_adam32 launches.  f32_update_fused: set by a
+  // backward that scheduled it, consumed by the next model_norms / model_adam
+  bool f32_fuse_enabled = true;
+  int f32_adam_pos = 1;   // QLX_F32_ADAM_POS: 0 leading blocks of the conv2 pair, 1 trailing blocks
+  bool f32_update_fused = false;
   // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
   // sample's result does not depend on the batch it is evaluated in (the learner's target net)
   bool fc1_single = false;
@@ -128,11 +136,13 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
 // weights (optional): per-sample loss weights; td_abs (optional): |q_a - y| per sample out.
 // = model_backward_dense (head, fc1: the dense gradients, 95 % of the bytes, are final after it) followed by
 // model_backward_conv (the conv trunk); a data-parallel caller all-reduces the dense bucket in between
+// fuse_update: no all-reduce will follow, so the fp32 path may schedule the norms / Adam of the variables whose gradient
+// is final inside the later backward launches (model_norms / model_adam then finish the rest)
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
-                    hipStream_t s, const float* weights = nullptr, float* td_abs = nullptr);
+                    hipStream_t s, const float* weights = nullptr, float* td_abs = nullptr, bool fuse_update = false);
 void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
                           const float* weights = nullptr, float* td_abs = nullptr);
-void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
+void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update = false);
 // per-variable norm partials for Adam: with scale == 1 (no all-reduce since the backward) the producers'
 // fused partials are used as they are; otherwise per-range sums of squares of the scaled gradients
 void model_norms(qlx_model* m, hipStream_t s, float scale);
@@ -144,7 +154,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
 void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s);   // mode 3 = training head
 void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
                         const float* weights, float* td_abs);
-void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s);
+void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update);
 void f32_norms(qlx_model* m, hipStream_t s, float scale);
 void f32_adam(qlx_model* m, hipStream_t s, float scale);
 }  // namespace qlx

@@ -600,9 +600,9 @@ Fc2Args fc2_args(qlx_model* m, int B) {
 // Huber loss (mean over the batch -> *loss_dev) and its raw, unclipped gradients into m->d_grads, after
 // model_forward_trunk on the same batch; actions / y are device arrays [B]
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
-                    hipStream_t s, const float* weights, float* td_abs) {
+                    hipStream_t s, const float* weights, float* td_abs, bool fuse_update) {
   model_backward_dense(m, B, actions, y, loss_dev, s, weights, td_abs);
-  model_backward_conv(m, table, B, s);
+  model_backward_conv(m, table, B, s, fuse_update);
 }
 
 // the head and dense part of the backward: Huber (+ dz4), dW4 / db4 / loss, dW3 / db3 and dz3
@@ -649,8 +649,8 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
 
 // the conv part of the backward (after model_backward_dense on the same batch): dz3 -> dz2 -> dz1 and the
 // three conv weight gradients into m->d_grads
-void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
-  if (m->f32) { f32_backward_conv(m, table, B, s); return; }
+void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update) {
+  if (m->f32) { f32_backward_conv(m, table, B, s, fuse_update); return; }
   ModelWs& w = m->w;
   float* G = m->d_grads;
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)
@@ -793,6 +793,10 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     m->f32 = arch == QLX_ARCH_NATURE_DQN;
     const char* ch = std::getenv("QLX_CONV1_HALVES");
     m->conv1_halves = !(ch && ch[0] == '0');
+    const char* fa = std::getenv("QLX_F32_FUSED_ADAM");
+    m->f32_fuse_enabled = !(fa && fa[0] == '0');
+    const char* ap = std::getenv("QLX_F32_ADAM_POS");
+    m->f32_adam_pos = ap && ap[0] == '0' ? 0 : 1;
     try {   // a failure part-way releases what was built
       m->device = device;
       QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
@@ -946,7 +950,7 @@ int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions
     QLX_HIP(hipMemcpyAsync(m->w.act, actions, B, hipMemcpyHostToDevice, s));
     QLX_HIP(hipMemcpyAsync(m->w.y, y, B * 4, hipMemcpyHostToDevice, s));
     model_forward_trunk(m, m->w.table, (int)B, s);
-    model_backward(m, m->w.table, (int)B, m->w.act, m->w.y, m->w.loss, s);
+    model_backward(m, m->w.table, (int)B, m->w.act, m->w.y, m->w.loss, s, nullptr, nullptr, true);
     if (grads_out) QLX_HIP(hipMemcpyAsync(grads_out, m->d_grads, kNumParams * 4, hipMemcpyDeviceToHost, s));
     model_norms(m, s, 1.0f);
     model_adam(m, s, 1.0f);

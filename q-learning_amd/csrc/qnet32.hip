@@ -182,18 +182,16 @@ struct NormArgs {
   int seg_first[kNumVars + 1];
   int64_t off[kNumVars + 1];
 };
-__global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
-  __shared__ float wsum[4];
-  int v = 0;
-  while (v < kNumVars - 1 && (int)blockIdx.x >= A.seg_first[v + 1]) ++v;
-  const int j = blockIdx.x - A.seg_first[v];
-  const int64_t n = A.off[v + 1] - A.off[v];
+// thread tl (0 .. 255) of segment j of variable v (elements off[v] ..): its fmaf chain over its eight elements, then its
+// wave's xor butterfly (every lane ends with the wave sum); segments past the variable's end chain zeros
+__device__ __forceinline__ float norm32_lane(const float* gall, const int64_t* off, float scale, int v, int j, int tl) {
+  const int64_t n = off[v + 1] - off[v];
   const int64_t b = (int64_t)j * kNormSeg;
-  const float* g = A.g + A.off[v];   // variable offsets are multiples of 4 floats (16-byte loads)
+  const float* g = gall + off[v];   // variable offsets are multiples of 4 floats (16-byte loads)
   f32x4 x[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int64_t i = b + 1024 * h + 4 * threadIdx.x;
+    const int64_t i = b + 1024 * h + 4 * tl;
     if (i + 4 <= n) {
       x[h] = ld4(g + i);
     } else {
@@ -206,14 +204,37 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float y = __fmul_rn(x[h][k], A.scale);
+      const float y = __fmul_rn(x[h][k], scale);
       t = fmaf(y, y, t);
     }
   for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+  return t;
+}
+
+// one 256-thread block = one segment partial: ((w0 + w1) + w2) + w3 of its four waves (wsum: 4 floats of LDS)
+__device__ __forceinline__ void norm32_block(const NormArgs& A, int blk, float* wsum) {
+  int v = 0;
+  while (v < kNumVars - 1 && blk >= A.seg_first[v + 1]) ++v;
+  const float t = norm32_lane(A.g, A.off, A.scale, v, blk - A.seg_first[v], threadIdx.x);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
   __syncthreads();
-  if (threadIdx.x == 0) A.partial[blockIdx.x] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]);
+  if (threadIdx.x == 0) A.partial[blk] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]);
 }
+
+__global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
+  __shared__ float wsum[4];
+  norm32_block(A, blockIdx.x, wsum);
+}
+
+// trailing blocks of a pair launch (k_gemm32_pair's T): the segment partials of the variables whose gradient is final
+// before that launch (the dense ones, after the fc1 backward), blocks first_seg ..
+struct NormTail {
+  static constexpr size_t LDS = 16;
+  NormArgs A;
+  int first_seg, nblocks;
+  __host__ __device__ int blocks() const { return nblocks; }
+  __device__ void run(int t, float* lds) const { norm32_block(A, first_seg + t, lds); }
+};
 
 struct Adam32Args {
   float* w;
@@ -244,6 +265,37 @@ __device__ __forceinline__ int var_of(const Adam32Args& A, int64_t i) {
   return v;
 }
 
+// norm_v for v = V0 .. 9 into nrm[v] (wave 0; lane chain over the partials lane, lane + 64, ... of v - zeros past the
+// end - then the xor butterfly).  Every partial is loaded at once (13 per lane for W3, one per lane for each smaller
+// variable: one memory round).  write: also store them to A.norms.
+template <int V0>
+__device__ __forceinline__ void norms_prologue(const Adam32Args& A, int lane, float* nrm, bool write) {
+  float x[kNormSegMax / 64], y[kNumVars];
+  const int f6 = A.seg_first[6], c6 = A.seg_first[7] - f6;
+#pragma unroll
+  for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < c6 ? A.partial[f6 + lane + 64 * i] : 0.0f;
+#pragma unroll
+  for (int vv = V0; vv < kNumVars; ++vv) {
+    const int f = A.seg_first[vv], c = A.seg_first[vv + 1] - f;
+    y[vv] = vv != 6 && lane < c ? A.partial[f + lane] : 0.0f;   // every variable but W3 has <= 64 partials
+  }
+#pragma unroll
+  for (int vv = V0; vv < kNumVars; ++vv) {
+    float t = 0.0f;
+    if (vv == 6) {
+#pragma unroll
+      for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
+    } else {
+      t = __fadd_rn(t, y[vv]);
+    }
+    for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+    if (lane == 0) {
+      nrm[vv] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
+      if (write) A.norms[vv] = nrm[vv];
+    }
+  }
+}
+
 // One float4 group (16-byte accesses) per thread: the grid covers count / 4 groups plus the tail group (elements past the
 // last full group, finished element by element).  Every variable but the last starts at a multiple of 4, so a group never
 // straddles two variables.  The group's g / w / m / v loads are issued first; wave 0 then loads all the clip-norm
@@ -261,33 +313,7 @@ __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
     m = ld4(A.m + i0);
     v = ld4(A.v + i0);
   }
-  if (wave == 0) {
-    // norm_v: lane chain over the partials lane, lane + 64, ... of v (zeros past the end), then the xor butterfly
-    float x[kNormSegMax / 64], y[kNumVars];
-    const int f6 = A.seg_first[6], c6 = A.seg_first[7] - f6;
-#pragma unroll
-    for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < c6 ? A.partial[f6 + lane + 64 * i] : 0.0f;
-#pragma unroll
-    for (int vv = 0; vv < kNumVars; ++vv) {
-      const int f = A.seg_first[vv], c = A.seg_first[vv + 1] - f;
-      y[vv] = vv != 6 && lane < c ? A.partial[f + lane] : 0.0f;   // every variable but W3 has <= 64 partials
-    }
-#pragma unroll
-    for (int vv = 0; vv < kNumVars; ++vv) {
-      float t = 0.0f;
-      if (vv == 6) {
-#pragma unroll
-        for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
-      } else {
-        t = __fadd_rn(t, y[vv]);
-      }
-      for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
-      if (lane == 0) {
-        nrm[vv] = t > 0.0f ? sqrtf(t) : t;   // safe sqrt via where(l2sum > 0)
-        if (blockIdx.x == 0) A.norms[vv] = nrm[vv];
-      }
-    }
-  }
+  if (wave == 0) norms_prologue<0>(A, lane, nrm, blockIdx.x == 0);
   __syncthreads();
   if (q < n4) {
     const float denom = fmaxf(nrm[var_of(A, i0)], A.clipnorm);
@@ -310,6 +336,95 @@ __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
       A.m[i] = mi;
       A.v[i] = vi;
     }
+  }
+}
+
+// Blocks of a pair launch (k_gemm32_pair's S or T) running clip_by_norm + Adam of the dense variables (W3, b3, W4, b4 -
+// 95 % of the update's Adam bytes) once their norm partials exist, so that HBM-bound work runs beside the conv backward's
+// MFMA tiles instead of after the whole backward.  Same arithmetic as k_adam32 on those elements.
+struct AdamDense {
+  static constexpr size_t LDS = 64;
+  Adam32Args A;
+  int nblocks;
+  __host__ __device__ int blocks() const { return nblocks; }
+  __device__ void run(int t, float* lds) const {
+    float* nrm = lds;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave == 0) norms_prologue<6>(A, lane, nrm, t == 0);
+    __syncthreads();
+    const int64_t o6 = A.off[6], count = A.off[kNumVars], n4 = (count - o6) / 4;   // o6 is a multiple of 4
+    for (int64_t q = (int64_t)t * blockDim.x + threadIdx.x; q <= n4; q += (int64_t)nblocks * blockDim.x) {
+      const int64_t i0 = o6 + q * 4;
+      if (q < n4) {
+        const float denom = fmaxf(nrm[var_of(A, i0)], A.clipnorm);
+        const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
+        f32x4 m = ld4(A.m + i0), v = ld4(A.v + i0), o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float mk = m[k], vk = v[k];
+          o[k] = adam32_elem(g[k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[k]);
+          m[k] = mk;
+          v[k] = vk;
+        }
+        *reinterpret_cast<f32x4*>(A.w + i0) = o;
+        *reinterpret_cast<f32x4*>(A.m + i0) = m;
+        *reinterpret_cast<f32x4*>(A.v + i0) = v;
+      } else {
+        for (int64_t i = i0; i < count; ++i) {
+          const float denom = fmaxf(nrm[var_of(A, i)], A.clipnorm);
+          float mi = A.m[i], vi = A.v[i];
+          A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mi, vi, A.w[i]);
+          A.m[i] = mi;
+          A.v[i] = vi;
+        }
+      }
+    }
+  }
+};
+
+// clip_by_norm + Adam of the six conv variables (W0 .. b2, 78K elements), one 1024-thread block per variable: its
+// segment partials (four 256-thread groups, each one k_norm32 block's arithmetic), the norm, the element update.  No
+// block depends on another, so the update's tail after the weight-gradient reduction is one small launch.
+__global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) {
+  __shared__ float wsum[4][4];
+  __shared__ float part[64];
+  __shared__ float nrm[kNumVars];
+  const int v = blockIdx.x, grp = threadIdx.x >> 8, tl = threadIdx.x & 255;
+  const int nseg = N.seg_first[v + 1] - N.seg_first[v];
+  for (int j0 = 0; j0 < nseg; j0 += 4) {   // block-uniform trip count
+    const int j = j0 + grp;
+    const float t = norm32_lane(N.g, N.off, N.scale, v, j < nseg ? j : 0, tl);
+    if ((tl & 63) == 0) wsum[grp][tl >> 6] = t;
+    __syncthreads();
+    if (tl == 0 && j < nseg) part[j] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[grp][0], wsum[grp][1]), wsum[grp][2]), wsum[grp][3]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 64) {   // <= 64 partials: each lane's chain is 0 + its partial
+    const int lane = threadIdx.x;
+    float t = __fadd_rn(0.0f, lane < nseg ? part[lane] : 0.0f);
+    for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
+    if (lane == 0) {
+      nrm[v] = t > 0.0f ? sqrtf(t) : t;
+      A.norms[v] = nrm[v];
+    }
+  }
+  __syncthreads();
+  const float denom = fmaxf(nrm[v], A.clipnorm);
+  const int64_t o = A.off[v], n4 = (A.off[v + 1] - o) / 4;   // conv variables are multiples of 4 long
+  for (int64_t q = threadIdx.x; q < n4; q += blockDim.x) {
+    const int64_t i0 = o + q * 4;
+    const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
+    f32x4 m = ld4(A.m + i0), vv = ld4(A.v + i0), out;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float mk = m[k], vk = vv[k];
+      out[k] = adam32_elem(g[k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[k]);
+      m[k] = mk;
+      vv[k] = vk;
+    }
+    *reinterpret_cast<f32x4*>(A.w + i0) = out;
+    *reinterpret_cast<f32x4*>(A.m + i0) = m;
+    *reinterpret_cast<f32x4*>(A.v + i0) = vv;
   }
 }
 
@@ -396,13 +511,14 @@ static void launch(qlx_model* m, const P& p, const char* scope, double work, hip
   debug_sync(s, scope);
 }
 
-template <class P1, class P2, class S>
-static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side, const char* scope, double work, hipStream_t s) {
-  const size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS});
+template <class P1, class P2, class S, class T = NoSide>
+static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side, const char* scope, double work, hipStream_t s,
+                        const T& tail = T{}) {
+  const size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS, T::LDS});
   hipEvent_t ea = nullptr, eb = nullptr;
   if (m->prof) m->prof->ext(scope, work, &ea, &eb);
-  hipExtLaunchKernelGGL((k_gemm32_pair<P1, P2, S>), dim3(S::BLOCKS + p1.g.blocks() + p2.g.blocks()), dim3(256), lds, s, ea, eb, 0u,
-                        p1, p2, side);
+  hipExtLaunchKernelGGL((k_gemm32_pair<P1, P2, S, T>), dim3(side.blocks() + p1.g.blocks() + p2.g.blocks() + tail.blocks()), dim3(256),
+                        lds, s, ea, eb, 0u, p1, p2, side, tail);
   QLX_HIP(hipGetLastError());
   debug_sync(s, scope);
 }
@@ -500,8 +616,51 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
   }
 }
 
-void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
+static void seg_tables(int* seg_first, int64_t* off) {
+  int sf = 0;
+  int64_t o = 0;
+  for (int v = 0; v < kNumVars; ++v) {
+    seg_first[v] = sf;
+    off[v] = o;
+    sf += segs_of(v);
+    o += kVarSize[v];
+  }
+  seg_first[kNumVars] = sf;
+  off[kNumVars] = o;
+}
+
+static NormArgs norm_args(qlx_model* m, float scale) {
+  NormArgs A;
+  A.g = m->d_grads;
+  A.scale = scale;
+  A.partial = m->w.fpart;
+  seg_tables(A.seg_first, A.off);
+  return A;
+}
+
+// Adam arguments of the update about to run (iterations + 1)
+static Adam32Args adam_args(qlx_model* m, float scale) {
+  const float tf = (float)(m->iterations + 1);
+  const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
+  Adam32Args a;
+  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.partial = m->w.fpart; a.norms = m->d_norms;
+  seg_tables(a.seg_first, a.off);
+  a.scale = scale;
+  a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
+  a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
+  return a;
+}
+
+constexpr int kAdamDenseBlocks = 512;   // blocks of the dense update inside the conv2 pair launch
+
+void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update) {
   ModelWs& w = m->w;
+  // the dense variables' clip norms and Adam beside the conv backward (qnet.h f32_fuse_enabled)
+  const bool fuse = fuse_update && m->f32_fuse_enabled;
+  m->f32_update_fused = fuse;
+  const NormArgs N = norm_args(m, 1.0f);
+  const NormTail ntail{N, N.seg_first[6], fuse ? N.seg_first[kNumVars] - N.seg_first[6] : 0};
+  const AdamDense adense{adam_args(m, 1.0f), fuse ? kAdamDenseBlocks : 0};
   const float* p = m->d_params;
   float* G = m->d_grads;
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
@@ -513,18 +672,19 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   static const bool pxg = [] { const char* e = std::getenv("QLX_F32_PXG"); return !(e && e[0] == '0'); }();
   {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-    if (pxg) {
+    if (pxg) {   // + the dense variables' norm partials as trailing blocks (their gradients are final)
       PConv3DgradPxG<32, 64, 2, 2> Pd{{Grid{(B + 31) / 32, 1, PConv3DgradPxG<>::GROUPS}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B}};
-      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s, ntail);
     } else {
       PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
-      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s, ntail);
     }
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
     PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
-    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    if (m->f32_adam_pos == 0) launch_pair(m, Pw, Pd, adense, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);   // + dense Adam
+    else launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s, adense);
   }
   {
     constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
@@ -549,26 +709,10 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   }
 }
 
-static void seg_tables(int* seg_first, int64_t* off) {
-  int sf = 0;
-  int64_t o = 0;
-  for (int v = 0; v < kNumVars; ++v) {
-    seg_first[v] = sf;
-    off[v] = o;
-    sf += segs_of(v);
-    o += kVarSize[v];
-  }
-  seg_first[kNumVars] = sf;
-  off[kNumVars] = o;
-}
-
 void f32_norms(qlx_model* m, hipStream_t s, float scale) {
+  if (m->f32_update_fused) return;   // the backward scheduled them (f32_backward_conv)
   ProfScope ps(m->prof, "f32_norms", s, 4.0 * kNumParams);
-  NormArgs A;
-  A.g = m->d_grads;
-  A.scale = scale;
-  A.partial = m->w.fpart;
-  seg_tables(A.seg_first, A.off);
+  const NormArgs A = norm_args(m, scale);
   hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
   QLX_HIP(hipGetLastError());
   debug_sync(s, "k_norm32");
@@ -576,14 +720,17 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
 
 void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const int64_t t = m->iterations + 1;
-  const float tf = (float)t;
-  const float b1p = std::pow(m->beta1, tf), b2p = std::pow(m->beta2, tf);
-  Adam32Args a;
-  a.w = m->d_params; a.m = m->d_m; a.v = m->d_v; a.g = m->d_grads; a.partial = m->w.fpart; a.norms = m->d_norms;
-  seg_tables(a.seg_first, a.off);
-  a.scale = scale;
-  a.alpha = m->lr * std::sqrt(1.0f - b2p) / (1.0f - b1p);
-  a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
+  const Adam32Args a = adam_args(m, scale);
+  if (m->f32_update_fused) {   // dense variables done beside the conv backward; the six conv variables here
+    QLX_CHECK(scale == 1.0f, QLX_E_STATE, "fused fp32 update with a gradient scale");
+    ProfScope ps(m->prof, "f32_conv_adam", s, 28.0 * kVarOffsetDense);
+    hipLaunchKernelGGL(k_conv_adam32, dim3(6), dim3(1024), 0, s, a, norm_args(m, 1.0f));
+    QLX_HIP(hipGetLastError());
+    debug_sync(s, "k_conv_adam32");
+    m->f32_update_fused = false;
+    m->iterations = t;
+    return;
+  }
   ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
   const int64_t groups = kNumParams / 4 + 1;   // float4 groups + the tail group: one per thread
   hipLaunchKernelGGL(k_adam32, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, a);

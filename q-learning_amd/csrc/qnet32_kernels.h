@@ -536,25 +536,26 @@ __global__ __launch_bounds__(threads_of<P>()) void k_gemm32(const P p) {
   body(p, block_order<P>(blockIdx.x, gridDim.x), lds);
 }
 
-// two independent GEMMs in one grid (hardware blocks [S::BLOCKS, S::BLOCKS + G1) run P1), plus `side` leading blocks
-// running S
-template <class P1, class P2, class S>
-__global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, const S side) {
+// two independent GEMMs in one grid (hardware blocks [side.blocks(), side.blocks() + G1) run P1), plus `side` leading
+// blocks running S and `tail` trailing blocks running T (independent work that fills CU slots beside / after the tiles)
+template <class P1, class P2, class S, class T>
+__global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, const S side, const T tail) {
   static_assert(KSplitOf<P1>::value == 1 && KSplitOf<P2>::value == 1, "pair launches: 256 threads");
   extern __shared__ float lds[];
-  const int b = blockIdx.x;
-  if (b < S::BLOCKS) { side.run(b, lds); return; }
+  const int b = blockIdx.x, ns = side.blocks();
+  if (b < ns) { side.run(b, lds); return; }
   // the problems take consecutive hardware blocks (so both spread over all eight XCDs, P1 - the longer weight-gradient
   // tiles - dispatched first); inside each problem the XCD-grouped tile order
-  const int G = gridDim.x - S::BLOCKS, h = b - S::BLOCKS;
-  const int g1 = p1.g.blocks();
+  const int h = b - ns;
+  const int g1 = p1.g.blocks(), g2 = p2.g.blocks();
   if (h < g1) body(p1, block_order<P1>(h, g1), lds);
-  else body(p2, block_order<P2>(h - g1, G - g1), lds);
+  else if (h < g1 + g2) body(p2, block_order<P2>(h - g1, g2), lds);
+  else tail.run(h - g1 - g2, lds);
 }
 
 struct NoSide {
-  static constexpr int BLOCKS = 0;
   static constexpr size_t LDS = 0;
+  __host__ __device__ int blocks() const { return 0; }
   __device__ void run(int, float*) const {}
 };
 
@@ -1013,6 +1014,7 @@ struct PConvWgrad {
 // then wave 0 runs the chain from LDS: two memory latencies per launch instead of one per few MFMAs.
 struct SideFc2 {
   static constexpr int BLOCKS = 33;   // 512 rows of a4^T + the ones row
+  __host__ __device__ int blocks() const { return BLOCKS; }
   static constexpr int HB = 512;      // samples per LDS pass (40 KB; 256 measured slower: 73.4 vs 71.2 us per fc1 backward)
   static constexpr size_t LDS = (size_t)HB * 20 * sizeof(float);
   const float* a4;

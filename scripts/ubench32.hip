@@ -301,7 +301,8 @@ template <class P1, class P2>
 static void run2(const char* name, const P1& p1, const P2& p2, double flop) {
   const size_t lds = std::max(gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>());
   const double us = time_us([&] {
-    hipLaunchKernelGGL((k_gemm32_pair<P1, P2, NoSide>), dim3(p1.g.blocks() + p2.g.blocks()), dim3(256), lds, 0, p1, p2, NoSide{});
+    hipLaunchKernelGGL((k_gemm32_pair<P1, P2, NoSide, NoSide>), dim3(p1.g.blocks() + p2.g.blocks()), dim3(256), lds, 0, p1, p2, NoSide{},
+                       NoSide{});
   });
   printf("%-34s blocks %6d lds %6zu  %9.2f us  %7.2f TF  %5.1f %%\n", name, p1.g.blocks() + p2.g.blocks(), lds, us,
          flop / us / 1e6, flop / us / 1e6 / 157.3 * 100);
@@ -400,14 +401,15 @@ int main(int argc, char** argv) {
       SideFc2 S{a4, act, dz4, dz4 + 1024, B, gw, gw + 2000, gw + 3000};
       const size_t lds = std::max({gemm_lds_bytes<PFc1WgradS>(), gemm_lds_bytes<PFc1DgradS>(), SideFc2::LDS});
       double us = time_us([&] {
-        hipLaunchKernelGGL((k_gemm32_pair<PFc1WgradS, PFc1DgradS, SideFc2>), dim3(SideFc2::BLOCKS + Pw.g.blocks() + Pd.g.blocks()),
-                           dim3(256), lds, 0, Pw, Pd, S);
+        hipLaunchKernelGGL((k_gemm32_pair<PFc1WgradS, PFc1DgradS, SideFc2, NoSide>), dim3(SideFc2::BLOCKS + Pw.g.blocks() + Pd.g.blocks()),
+                           dim3(256), lds, 0, Pw, Pd, S, NoSide{});
       });
       printf("%-34s %9.2f us\n", "fc1_bwd pair + SideFc2", us);
       PFc1WgradS Pw0{Grid{0, 1, 1}, a3, dz4, gw, gw, B};
       PFc1DgradS Pd0{Grid{0, 1, 1}, dz4, W3, a3, dz3, B};
       us = time_us([&] {
-        hipLaunchKernelGGL((k_gemm32_pair<PFc1WgradS, PFc1DgradS, SideFc2>), dim3(SideFc2::BLOCKS), dim3(256), lds, 0, Pw0, Pd0, S);
+        hipLaunchKernelGGL((k_gemm32_pair<PFc1WgradS, PFc1DgradS, SideFc2, NoSide>), dim3(SideFc2::BLOCKS), dim3(256), lds, 0, Pw0, Pd0, S,
+                           NoSide{});
       });
       printf("%-34s %9.2f us\n", "SideFc2 alone", us);
     }
