@@ -382,37 +382,59 @@ struct AdamDense {
   }
 };
 
-// clip_by_norm + Adam of the six conv variables (W0 .. b2, 78K elements), one 1024-thread block per variable: its
-// segment partials (four 256-thread groups, each one k_norm32 block's arithmetic), the norm, the element update.  No
-// block depends on another, so the update's tail after the weight-gradient reduction is one small launch.
+// clip_by_norm + Adam of the six conv variables (W0 .. b2, 78K elements) in one launch of independent 1024-thread blocks:
+// block = (variable v, chunk c of 4,096 elements).  Each block finishes v's norm itself - every gradient element of v
+// loaded at once (four 256-thread groups, group q taking segments q, q + 4, .., each with one k_norm32 block's
+// arithmetic), then the partials and the final chain in LDS - and updates its chunk (one float4 per thread).  The
+// re-read of v per chunk (<= 147 KB, from L2) buys a launch with one memory round per phase.
+constexpr int kConvAdamChunk = 4096;
+constexpr int kConvSegsPerGroup = 5;   // segments per 256-thread group: W2 has 18 = 4 x 4 + 2
 __global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) {
-  __shared__ float wsum[4][4];
+  __shared__ float wsum[kConvSegsPerGroup][4][4];
   __shared__ float part[64];
-  __shared__ float nrm[kNumVars];
-  const int v = blockIdx.x, grp = threadIdx.x >> 8, tl = threadIdx.x & 255;
-  const int nseg = N.seg_first[v + 1] - N.seg_first[v];
-  for (int j0 = 0; j0 < nseg; j0 += 4) {   // block-uniform trip count
-    const int j = j0 + grp;
-    const float t = norm32_lane(N.g, N.off, N.scale, v, j < nseg ? j : 0, tl);
-    if ((tl & 63) == 0) wsum[grp][tl >> 6] = t;
-    __syncthreads();
-    if (tl == 0 && j < nseg) part[j] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[grp][0], wsum[grp][1]), wsum[grp][2]), wsum[grp][3]);
-    __syncthreads();
+  __shared__ float nrm;
+  // block -> (variable, chunk): chunks of the six variables in order
+  int v = 0, c = blockIdx.x;
+  for (;;) {
+    const int nc = (int)((A.off[v + 1] - A.off[v] + kConvAdamChunk - 1) / kConvAdamChunk);
+    if (c < nc || v == 5) break;
+    c -= nc;
+    ++v;
   }
-  if (threadIdx.x < 64) {   // <= 64 partials: each lane's chain is 0 + its partial
-    const int lane = threadIdx.x;
-    float t = __fadd_rn(0.0f, lane < nseg ? part[lane] : 0.0f);
-    for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
-    if (lane == 0) {
-      nrm[v] = t > 0.0f ? sqrtf(t) : t;
-      A.norms[v] = nrm[v];
+  const int grp = threadIdx.x >> 8, tl = threadIdx.x & 255, lane = threadIdx.x & 63;
+  const int nseg = N.seg_first[v + 1] - N.seg_first[v];
+  float t[kConvSegsPerGroup];
+#pragma unroll
+  for (int r = 0; r < kConvSegsPerGroup; ++r) {
+    const int j = grp + 4 * r;
+    t[r] = j < nseg ? norm32_lane(N.g, N.off, N.scale, v, j, tl) : 0.0f;
+  }
+#pragma unroll
+  for (int r = 0; r < kConvSegsPerGroup; ++r)
+    if ((tl & 63) == 0) wsum[r][grp][tl >> 6] = t[r];
+  __syncthreads();
+  if (tl == 0) {
+#pragma unroll
+    for (int r = 0; r < kConvSegsPerGroup; ++r) {
+      const int j = grp + 4 * r;
+      if (j < nseg) part[j] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[r][grp][0], wsum[r][grp][1]), wsum[r][grp][2]), wsum[r][grp][3]);
     }
   }
   __syncthreads();
-  const float denom = fmaxf(nrm[v], A.clipnorm);
-  const int64_t o = A.off[v], n4 = (A.off[v + 1] - o) / 4;   // conv variables are multiples of 4 long
-  for (int64_t q = threadIdx.x; q < n4; q += blockDim.x) {
-    const int64_t i0 = o + q * 4;
+  if (threadIdx.x < 64) {   // <= 64 partials: each lane's chain is 0 + its partial
+    float s = __fadd_rn(0.0f, lane < nseg ? part[lane] : 0.0f);
+    for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o));
+    if (lane == 0) {
+      nrm = s > 0.0f ? sqrtf(s) : s;
+      if (c == 0) A.norms[v] = nrm;
+    }
+  }
+  __syncthreads();
+  const float denom = fmaxf(nrm, A.clipnorm);
+  const int64_t o = A.off[v], n = A.off[v + 1] - o;   // conv variables are multiples of 4 long
+  const int64_t e = (int64_t)c * kConvAdamChunk + 4 * threadIdx.x;
+  if (e < n) {
+    const int64_t i0 = o + e;
     const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
     f32x4 m = ld4(A.m + i0), vv = ld4(A.v + i0), out;
 #pragma unroll
@@ -428,6 +450,12 @@ __global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) 
   }
 }
 
+static int conv_adam_blocks() {
+  int n = 0;
+  for (int v = 0; v < 6; ++v) n += (kVarSize[v] + kConvAdamChunk - 1) / kConvAdamChunk;
+  return n;
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // host side
 
@@ -439,6 +467,8 @@ using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
 static_assert((1605632 + kNormSeg - 1) / kNormSeg <= kNormSegMax, "norm partials per variable");
+static_assert((36864 + kNormSeg - 1) / kNormSeg <= 4 * kConvSegsPerGroup && (32768 + kNormSeg - 1) / kNormSeg <= 4 * kConvSegsPerGroup,
+              "conv variable segments per k_conv_adam32 block");
 static_assert((512 * 3 + kNormSeg - 1) / kNormSeg <= 64 && (32768 + kNormSeg - 1) / kNormSeg <= 64 &&
               (36864 + kNormSeg - 1) / kNormSeg <= 64 && (8192 + kNormSeg - 1) / kNormSeg <= 64, "<= 64 partials but W3");
 
@@ -724,7 +754,7 @@ void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   if (m->f32_update_fused) {   // dense variables done beside the conv backward; the six conv variables here
     QLX_CHECK(scale == 1.0f, QLX_E_STATE, "fused fp32 update with a gradient scale");
     ProfScope ps(m->prof, "f32_conv_adam", s, 28.0 * kVarOffsetDense);
-    hipLaunchKernelGGL(k_conv_adam32, dim3(6), dim3(1024), 0, s, a, norm_args(m, 1.0f));
+    hipLaunchKernelGGL(k_conv_adam32, dim3(conv_adam_blocks()), dim3(1024), 0, s, a, norm_args(m, 1.0f));
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv_adam32");
     m->f32_update_fused = false;
