@@ -403,6 +403,16 @@ __global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) 
   }
   const int grp = threadIdx.x >> 8, tl = threadIdx.x & 255, lane = threadIdx.x & 63;
   const int nseg = N.seg_first[v + 1] - N.seg_first[v];
+  // this thread's float4 of the chunk, loaded in the same memory round as the norm's gradient reads
+  const int64_t o = A.off[v], n = A.off[v + 1] - o;   // conv variables are multiples of 4 long
+  const int64_t e = (int64_t)c * kConvAdamChunk + 4 * threadIdx.x, i0 = o + e;
+  f32x4 g = zero4(), w = zero4(), m = zero4(), vv = zero4();
+  if (e < n) {
+    g = ld4(A.g + i0);
+    w = ld4(A.w + i0);
+    m = ld4(A.m + i0);
+    vv = ld4(A.v + i0);
+  }
   float t[kConvSegsPerGroup];
 #pragma unroll
   for (int r = 0; r < kConvSegsPerGroup; ++r) {
@@ -431,12 +441,8 @@ __global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) 
   }
   __syncthreads();
   const float denom = fmaxf(nrm, A.clipnorm);
-  const int64_t o = A.off[v], n = A.off[v + 1] - o;   // conv variables are multiples of 4 long
-  const int64_t e = (int64_t)c * kConvAdamChunk + 4 * threadIdx.x;
   if (e < n) {
-    const int64_t i0 = o + e;
-    const f32x4 g = ld4(A.g + i0), w = ld4(A.w + i0);
-    f32x4 m = ld4(A.m + i0), vv = ld4(A.v + i0), out;
+    f32x4 out;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float mk = m[k], vk = vv[k];
