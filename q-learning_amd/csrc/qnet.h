@@ -88,7 +88,7 @@ struct qlx_model {
   // QLX_F32_FUSED_ADAM=0 at create time keeps the separate k_norm32 + k_adam32 launches.  f32_update_fused: set by a
   // backward that scheduled it, consumed by the next model_norms / model_adam
   bool f32_fuse_enabled = true;
-  int f32_adam_pos = 1;   // QLX_F32_ADAM_POS: 0 leading blocks of the conv2 pair, 1 trailing blocks
+  int f32_adam_pos = 0;   // QLX_F32_ADAM_POS: 0 leading blocks of the conv2 pair (measured best), 1 trailing blocks
   bool f32_update_fused = false;
   // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
   // sample's result does not depend on the batch it is evaluated in (the learner's target net)
