@@ -84,10 +84,12 @@ struct qlx_model {
   bool conv1_halves = true;
   // fp32: clip_by_norm + Adam of the dense variables run inside the conv backward launches (their norm partials as
   // trailing blocks of the conv3 pair, the update beside the conv2 pair's tiles) and the conv variables' in one small
-  // launch after the weight-gradient reduction, when the caller allows it (no all-reduce between backward and Adam);
-  // QLX_F32_FUSED_ADAM=0 at create time keeps the separate k_norm32 + k_adam32 launches.  f32_update_fused: set by a
-  // backward that scheduled it, consumed by the next model_norms / model_adam
-  bool f32_fuse_enabled = true;
+  // launch after the weight-gradient reduction, when the caller allows it (no all-reduce between backward and Adam).
+  // Opt-in (QLX_F32_FUSED_ADAM=1 at create time): measured at C3 200.6K vs 199.9K env-steps/s with the separate k_norm32 +
+  // k_adam32 launches (within run-to-run spread), while it puts Adam's HBM work inside the conv2 backward pair - the
+  // roofline kernel (111.7 -> 115.7 us).  f32_update_fused: set by a backward that scheduled it, consumed by the next
+  // model_norms / model_adam
+  bool f32_fuse_enabled = false;
   int f32_adam_pos = 0;   // QLX_F32_ADAM_POS: 0 leading blocks of the conv2 pair (measured best), 1 trailing blocks
   bool f32_update_fused = false;
   // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
