@@ -23,7 +23,7 @@ SCOPES = {
         "f32_conv3_fwd": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2,",
         "f32_conv3_fwd_big": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2,",
         "f32_fc1_fwd": "k_gemm32<qlx::q32::PFc1FwdT<32, 32, 2, 2,",
-        "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<32, 64, 2, 2,",
+        "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<64, 64, 2, 2,",
         "f32_fc1_bwd": "k_gemm32_pair<qlx::q32::PFc1WgradT",
         "f32_conv3_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<9, 9",
         "f32_conv2_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<20, 20",
