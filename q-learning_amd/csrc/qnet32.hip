@@ -40,18 +40,51 @@ static int64_t voff(int v) {
 //   over n of W4[k][n] dq[b][n] is the single rounded product)
 // Block = 16 samples; wave w chains the k quarter [128 w, 128 w + 128) on v_mfma_f32_16x16x4_f32 (A = W4^T rows n < 3,
 // B = a4 columns), q = (((C0 + C1) + C2) + C3) + b4: four 32-step chains side by side instead of one 128-step chain.
+// The block's 16 a4 rows and W4 are staged in LDS with coalesced 16-byte loads (one memory round), the MFMA operands and
+// the dz4 epilogue read them from there.  Row pitch 514 floats: a fragment read's 32-lane group (16 rows x 2 k) hits 32
+// distinct banks (ds_read_b32: 32 banks, (address / 4) mod 32); rows are 8-byte aligned, so stores / epilogue reads are b64.
+constexpr int kHeadPitch = 514;
 template <int MODE>
 __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
   __shared__ f32x4 part[4][16];
   __shared__ float gsh[16];
   __shared__ int ash[16];
+  __shared__ __attribute__((aligned(16))) float xs[16 * kHeadPitch];
+  __shared__ __attribute__((aligned(16))) float w4s[512 * 3];
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s0 = blockIdx.x * 16;
   const int j = lane & 15, g = lane >> 4, n = lane & 15;
   const int b = s0 + j;
   const bool valid = b < A.B;
-  const float* x = A.a4f + (size_t)(valid ? b : s0) * 512 + 128 * wave + g;   // a4[b][128 w + 4 t + g]
-  const float* wp = A.w4 + (128 * wave + g) * 3 + (n < 3 ? n : 0);             // W4[128 w + 4 t + g][n]
+  {   // stage: 16 rows x 128 float4 of a4 (8 per thread; rows past B read row s0) and W4's 384 float4
+    f32x4 xr[8], wr[2];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int f = threadIdx.x + 256 * r, jj = f >> 7, k4 = f & 127;
+      xr[r] = ld4(A.a4f + (size_t)(s0 + jj < A.B ? s0 + jj : s0) * 512 + 4 * k4);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int f = threadIdx.x + 256 * r;
+      if (f < 384) wr[r] = ld4(A.w4 + 4 * f);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int f = threadIdx.x + 256 * r, jj = f >> 7, k4 = f & 127;
+      f32x2* d = reinterpret_cast<f32x2*>(xs + jj * kHeadPitch + 4 * k4);
+      d[0] = f32x2{xr[r][0], xr[r][1]};
+      d[1] = f32x2{xr[r][2], xr[r][3]};
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int f = threadIdx.x + 256 * r;
+      if (f < 384) *reinterpret_cast<f32x4*>(w4s + 4 * f) = wr[r];
+    }
+  }
+  __syncthreads();
+  const float* x = xs + j * kHeadPitch + 128 * wave + g;        // a4[b][128 w + 4 t + g]
+  const float* wp = w4s + (128 * wave + g) * 3 + (n < 3 ? n : 0);   // W4[128 w + 4 t + g][n]
   float wv[32], xv[32];
 #pragma unroll
   for (int t = 0; t < 32; ++t) wv[t] = wp[t * 12];
@@ -105,18 +138,20 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
       ash[j] = a;
     }
   }
-  if (MODE == 3 && A.dz4_out) {   // the block's 16 x 512 dz4 as float4s, 8 per thread (a4 rows are cache-hot)
+  if (MODE == 3 && A.dz4_out) {   // the block's 16 x 512 dz4 as float4s, 8 per thread (a4 and W4 from LDS)
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int f = threadIdx.x + 256 * r, jj = f >> 7, k = 4 * (f & 127), bb = s0 + jj;
       if (bb < A.B) {
-        const f32x4 xa = ld4(A.a4f + (size_t)bb * 512 + k);
+        const f32x2* xp = reinterpret_cast<const f32x2*>(xs + jj * kHeadPitch + k);
+        const f32x2 x01 = xp[0], x23 = xp[1];
+        const float xa[4] = {x01[0], x01[1], x23[0], x23[1]};
         const int a = ash[jj];
         const float gb = gsh[jj];
         f32x4 d;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[e] = xa[e] > 0.0f ? __fmul_rn(A.w4[(k + e) * 3 + a], gb) : 0.0f;
+        for (int e = 0; e < 4; ++e) d[e] = xa[e] > 0.0f ? __fmul_rn(w4s[(k + e) * 3 + a], gb) : 0.0f;
         *reinterpret_cast<f32x4*>(A.dz4_out + (size_t)bb * 512 + k) = d;
       }
     }
