@@ -158,51 +158,6 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
   }
 }
 
-// Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
-// [16 q, 16 q + 16)), S_q = chain over its chunks in order, dW = chain over q of S_q (each chain t = 0; t = t + x).
-// Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order, the last row of each the bias.
-// Block = 64 consecutive outputs x 16 group lanes (one wave per lane, 256-byte rows per load): wave g chains groups
-// g, g + 16, .. (16 partial loads in flight each); the group sums meet in LDS and wave 0 chains them.
-constexpr int kWGroup = 16;
-constexpr int kWGroupsMax = 128;   // chunks <= 2,048 (conv1 at the largest fp32 batch, 8,192)
-struct WRed {
-  const float* slab[3];
-  int nz[3];
-  int count[3];   // (M + 1) * OC; segments 0 and 1 are multiples of 64
-  int oc[3];
-  float* gw[3];   // W gradient
-  float* gb[3];   // b gradient
-};
-__global__ __launch_bounds__(1024) void k_wreduce32(WRed R) {
-  __shared__ float gs[kWGroupsMax * 64];
-  const int o = threadIdx.x & 63, g0 = threadIdx.x >> 6;
-  int e = blockIdx.x * 64;
-  int L = 0;
-  while (L < 3 && e >= R.count[L]) { e -= R.count[L]; ++L; }
-  if (L >= 3) return;   // block-uniform
-  const bool live = e + o < R.count[L];
-  const size_t stride = (size_t)R.count[L];
-  const int nz = R.nz[L], ng = (nz + kWGroup - 1) / kWGroup;
-  const float* p = R.slab[L] + e + (live ? o : 0);
-  for (int q = g0; q < ng; q += 16) {
-    float v[kWGroup];
-#pragma unroll
-    for (int j = 0; j < kWGroup; ++j) v[j] = q * kWGroup + j < nz ? p[(size_t)(q * kWGroup + j) * stride] : 0.0f;
-    float t = 0.0f;
-#pragma unroll
-    for (int j = 0; j < kWGroup; ++j) t = __fadd_rn(t, v[j]);   // + 0 past the last chunk leaves t unchanged
-    gs[q * 64 + o] = t;
-  }
-  __syncthreads();
-  if (g0 != 0 || !live) return;
-  float t = 0.0f;
-  for (int q = 0; q < ng; ++q) t = __fadd_rn(t, gs[q * 64 + o]);
-  const int oc = R.oc[L], m = (e + o) / oc, n = (e + o) - m * oc;
-  const int M = R.count[L] / oc - 1;
-  if (m == M) R.gb[L][n] = t;
-  else R.gw[L][(size_t)m * oc + n] = t;
-}
-
 // clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg = 2048;
 // thread t chains t = fmaf(x, x, t) over its elements j S + 4 t .. + 3, then j S + 1024 + 4 t .. + 3 (x = g * scale);
 // wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  Norm_v from its partials in k_adam32.
@@ -270,6 +225,66 @@ struct NormTail {
   __host__ __device__ int blocks() const { return nblocks; }
   __device__ void run(int t, float* lds) const { norm32_block(A, first_seg + t, lds); }
 };
+
+// Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
+// [16 q, 16 q + 16)), S_q = chain over its chunks in order, dW = chain over q of S_q (each chain t = 0; t = t + x).
+// Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order, the last row of each the bias.
+// Block = 64 consecutive outputs x 16 group lanes (one wave per lane, 256-byte rows per load): wave g chains groups
+// g, g + 16, .. (16 partial loads in flight each); the group sums meet in LDS and wave 0 chains them.
+constexpr int kWGroup = 16;
+constexpr int kWGroupsMax = 128;   // chunks <= 2,048 (conv1 at the largest fp32 batch, 8,192)
+struct WRed {
+  const float* slab[3];
+  int nz[3];
+  int count[3];   // (M + 1) * OC; segments 0 and 1 are multiples of 64
+  int oc[3];
+  float* gw[3];   // W gradient
+  float* gb[3];   // b gradient
+};
+// Blocks [nred, ..) of the launch (update schedule 2, qnet.h): clip-norm segment partials of segments seg0 .. seg0 + nseg
+// - the dense variables', final since the fc1 backward - four 256-thread groups per block, one k_norm32 block's
+// arithmetic each.
+__global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred, int seg0, int nseg) {
+  __shared__ float gs[kWGroupsMax * 64];
+  if ((int)blockIdx.x >= nred) {
+    const int grp = threadIdx.x >> 8, tl = threadIdx.x & 255;
+    const int sg = seg0 + 4 * ((int)blockIdx.x - nred) + grp;
+    const bool live = sg < seg0 + nseg;
+    int v = 0;
+    while (v < kNumVars - 1 && sg >= N.seg_first[v + 1]) ++v;
+    const float t = live ? norm32_lane(N.g, N.off, N.scale, v, sg - N.seg_first[v], tl) : 0.0f;
+    if ((tl & 63) == 0) gs[grp * 4 + (tl >> 6)] = t;
+    __syncthreads();
+    if (tl == 0 && live) N.partial[sg] = __fadd_rn(__fadd_rn(__fadd_rn(gs[grp * 4], gs[grp * 4 + 1]), gs[grp * 4 + 2]), gs[grp * 4 + 3]);
+    return;
+  }
+  const int o = threadIdx.x & 63, g0 = threadIdx.x >> 6;
+  int e = blockIdx.x * 64;
+  int L = 0;
+  while (L < 3 && e >= R.count[L]) { e -= R.count[L]; ++L; }
+  if (L >= 3) return;   // block-uniform
+  const bool live = e + o < R.count[L];
+  const size_t stride = (size_t)R.count[L];
+  const int nz = R.nz[L], ng = (nz + kWGroup - 1) / kWGroup;
+  const float* p = R.slab[L] + e + (live ? o : 0);
+  for (int q = g0; q < ng; q += 16) {
+    float v[kWGroup];
+#pragma unroll
+    for (int j = 0; j < kWGroup; ++j) v[j] = q * kWGroup + j < nz ? p[(size_t)(q * kWGroup + j) * stride] : 0.0f;
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kWGroup; ++j) t = __fadd_rn(t, v[j]);   // + 0 past the last chunk leaves t unchanged
+    gs[q * 64 + o] = t;
+  }
+  __syncthreads();
+  if (g0 != 0 || !live) return;
+  float t = 0.0f;
+  for (int q = 0; q < ng; ++q) t = __fadd_rn(t, gs[q * 64 + o]);
+  const int oc = R.oc[L], m = (e + o) / oc, n = (e + o) - m * oc;
+  const int M = R.count[L] / oc - 1;
+  if (m == M) R.gb[L][n] = t;
+  else R.gw[L][(size_t)m * oc + n] = t;
+}
 
 struct Adam32Args {
   float* w;
@@ -424,12 +439,12 @@ struct AdamDense {
 // re-read of v per chunk (<= 147 KB, from L2) buys a launch with one memory round per phase.
 constexpr int kConvAdamChunk = 4096;
 constexpr int kConvSegsPerGroup = 5;   // segments per 256-thread group: W2 has 18 = 4 x 4 + 2
-__global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) {
+__device__ __forceinline__ void conv_adam_block(const Adam32Args& A, const NormArgs& N, int blk) {
   __shared__ float wsum[kConvSegsPerGroup][4][4];
   __shared__ float part[64];
   __shared__ float nrm;
   // block -> (variable, chunk): chunks of the six variables in order
-  int v = 0, c = blockIdx.x;
+  int v = 0, c = blk;
   for (;;) {
     const int nc = (int)((A.off[v + 1] - A.off[v] + kConvAdamChunk - 1) / kConvAdamChunk);
     if (c < nc || v == 5) break;
@@ -489,6 +504,17 @@ __global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) 
     *reinterpret_cast<f32x4*>(A.m + i0) = m;
     *reinterpret_cast<f32x4*>(A.v + i0) = vv;
   }
+}
+
+__global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) { conv_adam_block(A, N, blockIdx.x); }
+
+// Update schedule 2 (qnet.h): clip_by_norm + Adam of every variable in one launch after the weight-gradient reduction -
+// blocks [0, nconv) the conv variables (conv_adam_block: norm from the gradient itself), the rest the dense variables
+// (their segment partials came from the reduction launch; AdamDense arithmetic).  No block depends on another.
+__global__ __launch_bounds__(1024) void k_update32(Adam32Args A, NormArgs N, int nconv, int ndense) {
+  __shared__ float nrm[kNumVars];
+  if ((int)blockIdx.x < nconv) conv_adam_block(A, N, blockIdx.x);
+  else AdamDense{A, ndense}.run((int)blockIdx.x - nconv, nrm);
 }
 
 static int conv_adam_blocks() {
@@ -728,7 +754,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   ModelWs& w = m->w;
   // the dense variables' clip norms and Adam beside the conv backward (qnet.h f32_fuse_enabled)
   const bool fuse = fuse_update && m->f32_fuse_enabled;
-  m->f32_update_fused = fuse;
+  m->f32_update_mode = fuse ? 1 : (fuse_update && m->f32_tail_enabled ? 2 : 0);
   const NormArgs N = norm_args(m, 1.0f);
   const NormTail ntail{N, N.seg_first[6], fuse ? N.seg_first[kNumVars] - N.seg_first[6] : 0};
   const AdamDense adense{adam_args(m, 1.0f), fuse ? kAdamDenseBlocks : 0};
@@ -774,14 +800,17 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
     const int total = R.count[0] + R.count[1] + R.count[2];
     QLX_CHECK(std::max({z1, z2, z3}) <= kWGroup * kWGroupsMax, QLX_E_INVALID, "too many weight-gradient chunks");
-    hipLaunchKernelGGL(k_wreduce32, dim3((total + 63) / 64), dim3(1024), 0, s, R);
+    // update schedule 2: + the dense variables' clip-norm segment partials (4 per block)
+    const int nred = (total + 63) / 64;
+    const int dseg = m->f32_update_mode == 2 ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
+    hipLaunchKernelGGL(k_wreduce32, dim3(nred + (dseg + 3) / 4), dim3(1024), 0, s, R, N, nred, N.seg_first[6], dseg);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_wreduce32");
   }
 }
 
 void f32_norms(qlx_model* m, hipStream_t s, float scale) {
-  if (m->f32_update_fused) return;   // the backward scheduled them (f32_backward_conv)
+  if (m->f32_update_mode != 0) return;   // the backward scheduled them (f32_backward_conv)
   ProfScope ps(m->prof, "f32_norms", s, 4.0 * kNumParams);
   const NormArgs A = norm_args(m, scale);
   hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
@@ -792,13 +821,24 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
 void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const int64_t t = m->iterations + 1;
   const Adam32Args a = adam_args(m, scale);
-  if (m->f32_update_fused) {   // dense variables done beside the conv backward; the six conv variables here
+  if (m->f32_update_mode == 1) {   // dense variables done beside the conv backward; the six conv variables here
     QLX_CHECK(scale == 1.0f, QLX_E_STATE, "fused fp32 update with a gradient scale");
     ProfScope ps(m->prof, "f32_conv_adam", s, 28.0 * kVarOffsetDense);
     hipLaunchKernelGGL(k_conv_adam32, dim3(conv_adam_blocks()), dim3(1024), 0, s, a, norm_args(m, 1.0f));
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv_adam32");
-    m->f32_update_fused = false;
+    m->f32_update_mode = 0;
+    m->iterations = t;
+    return;
+  }
+  if (m->f32_update_mode == 2) {   // every variable in one launch; the dense norm partials came with the reduction
+    QLX_CHECK(scale == 1.0f, QLX_E_STATE, "fp32 update schedule 2 with a gradient scale");
+    ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
+    const int nconv = conv_adam_blocks(), ndense = (int)((kNumParams - kVarOffsetDense) / 4 / 1024 + 1);
+    hipLaunchKernelGGL(k_update32, dim3(nconv + ndense), dim3(1024), 0, s, a, norm_args(m, 1.0f), nconv, ndense);
+    QLX_HIP(hipGetLastError());
+    debug_sync(s, "k_update32");
+    m->f32_update_mode = 0;
     m->iterations = t;
     return;
   }
