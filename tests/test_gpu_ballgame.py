@@ -241,3 +241,27 @@ def test_double_dqn_prioritized_learner_learns_ballgame():
     print(f"\nballgame ddqn+per learning: running_reward {st['running_reward']:.3f} after {st['step_count']} env-steps, "
           f"{st['update_count']} updates, {st['episode_count']} episodes")
     assert best >= 9.0, (best, st)
+
+
+def test_reference_learner_single_episode():
+    """The reference's own learner test (self_driving_tf_q_learner.rs:325-344 test_learner_single_episode): one
+    BallGame env, Parameter::default(), both nets loaded from the reference's exported model
+    (QL_MODEL_BALLGAME_3x3x4_5_512_PATH; tests/golden/ballgame_saved_variables); not solved, then learn_episode (vector
+    steps of one env until its first episode ends), then still not solved, step_count > 1, episode_count == 1."""
+    import os
+    qlx = _qlx()
+    prefix = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ballgame_saved_variables", "variables")
+    L = qlx.BallGameLearner(qlx.Parameter(n_envs=1))   # Parameter::default() (B = 32, 50k pure-random steps, ...)
+    L.model.load_tf(prefix)
+    L.stabilized_model.load_tf(prefix)   # SelfDrivingQLearner::new loads the stabilized model the same way (:94-116)
+    assert not L.solved()
+    steps = 0
+    while L.stats()["episode_count"] == 0:   # learn_episode: until the episode ends (done or max_steps_per_episode)
+        L.vector_step()
+        steps += 1
+        assert steps <= 10_000
+    st = L.stats()
+    assert not L.solved()
+    assert st["step_count"] > 1
+    assert st["episode_count"] == 1
+    L.close()
