@@ -157,6 +157,16 @@ struct ACtxOf { using type = NoCtx; };
 template <class P>
 struct ACtxOf<P, true> { using type = typename P::ACtx; };
 
+// Optional early epilogue operands (MF 16 policies): a policy with epi_pre(z, row, col) -> f32x4 (e.g. the ReLU mask
+// values of its four rows) and epi_post(z, row, col, acc, pre) has epi_pre's loads issued before the slab loop, so the
+// epilogue waits on nothing (a load issued after the loop would wait behind every slab load still in flight).
+template <class P, class = void>
+struct HasEpiPre : std::false_type {};
+#ifndef QLX_Q32_NO_EPIPRE   // (A/B builds: epilogue loads after the loop)
+template <class P>
+struct HasEpiPre<P, std::void_t<decltype(std::declval<const P&>().epi_pre(0, 0, 0))>> : std::true_type {};
+#endif
+
 // One output tile of a policy P (see the policies below for the members it provides):
 //   acc[row][col] = sum over the slabs s = 0 .. nslabs(z) - 1 and k = 0 .. 31 of A(z, s, row, k) * B(z, s, col, k),
 // one fmaf chain per output in (s, k) order; then P::epi stores it.  With P::BIAS the tiles of row-tile 0 also
@@ -285,6 +295,15 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     if (s + 1 < ns) store(s + 1, xa, xb);
     lds_barrier();
   };
+  constexpr bool PRE = HasEpiPre<P>::value && MF == 16 && G == 1;
+  f32x4 pre[TM][TN];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+  }
   if (ns > 0) {
     load(0, ra1, rb1);
     store(0, ra1, rb1);
@@ -322,7 +341,9 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      if constexpr (MF == 16) {
+      if constexpr (PRE) {
+        p.epi_post(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j], pre[i][j]);
+      } else if constexpr (MF == 16) {
         p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
       } else {
 #pragma unroll
@@ -460,7 +481,18 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   };
-  // after slab s: the epilogue of a sub-tile ending there, fresh accumulators
+  constexpr bool PRE = HasEpiPre<P>::value;
+  f32x4 pre[TM][TN];
+  auto fetch_pre = [&](int z) {
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+    }
+  };
+  // after slab s: the epilogue of a sub-tile ending there, fresh accumulators (and the next sub-tile's early operands)
   auto flush = [&](int s) {
     if (s + 1 != fq.e0) return;
     const int z = fq.z0;
@@ -468,10 +500,13 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), acc[i][j]);
+        const int row = row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col = col0 + (wn * TN + j) * 16 + (lane & 15);
+        if constexpr (PRE) p.epi_post(z, row, col, acc[i][j], pre[i][j]);
+        else p.epi(z, row, col, acc[i][j]);
         acc[i][j] = zero4();
       }
     fq.pop();
+    if (s + 1 < ns) fetch_pre(fq.z0);
   };
   auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
     load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
@@ -481,6 +516,7 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
     if (s + 1 < ns) store(s + 1, xa, xb);
     lds_barrier();
   };
+  fetch_pre(q.z0);
   if (ns > 0) {
     load(0, ra1, rb1);
     store(0, ra1, rb1);
@@ -655,6 +691,18 @@ struct PFc1DgradT {
         dz3[o] = a3[o] > 0.0f ? v[r] : 0.0f;
       }
   }
+  // the ReLU mask of the four rows, loaded before the slab loop (HasEpiPre; rows past M read row 0)
+  __device__ f32x4 epi_pre(int, int row, int col) const {
+    f32x4 m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m[r] = a3[(size_t)(row + r < M ? row + r : 0) * 3136 + col];
+    return m;
+  }
+  __device__ void epi_post(int, int row, int col, f32x4 v, f32x4 m) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) dz3[(size_t)(row + r) * 3136 + col] = m[r] > 0.0f ? v[r] : 0.0f;
+  }
 };
 using PFc1Dgrad = PFc1DgradT<>;
 using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
@@ -783,6 +831,19 @@ struct PConv3DgradPx {
         dz2[o] = a2[o] > 0.0f ? v[r] : 0.0f;
       }
   }
+  __device__ f32x4 epi_pre(int z, int row, int col) const {
+    const Px q = px(z);
+    f32x4 m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m[r] = a2[((size_t)((row + r < B ? row + r : 0) * 9 + q.ih) * 9 + q.iw) * 64 + col];
+    return m;
+  }
+  __device__ void epi_post(int z, int row, int col, f32x4 v, f32x4 m) const {
+    const Px q = px(z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < B) dz2[((size_t)((row + r) * 9 + q.ih) * 9 + q.iw) * 64 + col] = m[r] > 0.0f ? v[r] : 0.0f;
+  }
 };
 
 // conv2 backward-data, pixel-major over the class grid: z = (i, j) of 10 x 10; rows b; cols (py, px, c) = 128 (the four
@@ -834,6 +895,21 @@ struct PConv2DgradPx {
         const size_t o = ((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31);
         dz1[o] = a1[o] > 0.0f ? v[r] : 0.0f;
       }
+  }
+  __device__ f32x4 epi_pre(int z, int row, int col) const {
+    const Px q = px(z);
+    const int cls = col >> 5, ih = 2 * q.i + (cls >> 1), iw = 2 * q.j + (cls & 1);
+    f32x4 m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m[r] = a1[((size_t)((row + r < B ? row + r : 0) * 20 + ih) * 20 + iw) * 32 + (col & 31)];
+    return m;
+  }
+  __device__ void epi_post(int z, int row, int col, f32x4 v, f32x4 m) const {
+    const Px q = px(z);
+    const int cls = col >> 5, ih = 2 * q.i + (cls >> 1), iw = 2 * q.j + (cls & 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < B) dz1[((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31)] = m[r] > 0.0f ? v[r] : 0.0f;
   }
 };
 

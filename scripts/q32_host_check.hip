@@ -65,7 +65,13 @@ static void replay(const P& p, const char* name) {
       for (int i = 0; i < TM; ++i)
         for (int j = 0; j < TN; ++j)
           for (int lane = 0; lane < 64; ++lane) {
-            if (MF == 16) p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), zero4());
+            if constexpr (HasEpiPre<P>::value && MF == 16) {
+              const int row = row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col = col0 + (wn * TN + j) * 16 + (lane & 15);
+              const f32x4 m = p.epi_pre(z, row, col);
+              p.epi_post(z, row, col, zero4(), m);
+            } else if (MF == 16) {
+              p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), zero4());
+            }
             else
               for (int q = 0; q < 4; ++q)
                 p.epi(z, row0 + (wm * TM + i) * 32 + 8 * q + 4 * (lane >> 5), col0 + (wn * TN + j) * 32 + (lane & 31), zero4());
