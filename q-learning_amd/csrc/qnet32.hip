@@ -779,9 +779,16 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
-    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
-    if (m->f32_adam_pos == 0) launch_pair(m, Pw, Pd, adense, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);   // + dense Adam
-    else launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s, adense);
+    static const bool pxg2 = [] { const char* e = std::getenv("QLX_F32_PXG2"); return e && e[0] == '1'; }();
+    if (pxg2) {   // (A/B: conv2 pixel groups too)
+      PConv2DgradPxG<64, 64, 2, 2> Pd{{Grid{(B + 63) / 64, 2, PConv2DgradPxG<>::GROUPS}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B}};
+      if (m->f32_adam_pos == 0) launch_pair(m, Pw, Pd, adense, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+      else launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s, adense);
+    } else {
+      PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
+      if (m->f32_adam_pos == 0) launch_pair(m, Pw, Pd, adense, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);   // + dense Adam
+      else launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s, adense);
+    }
   }
   {
     constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
