@@ -629,6 +629,16 @@ struct PConvFwd {
     for (int r = 0; r < 4; ++r)
       if (row + r < M) out[(size_t)(row + r) * OC + col] = relu(v[r] + bias[col]);
   }
+  // the bias, loaded before the slab loop (HasEpiPre: a load after the loop waits behind the pipeline's last loads)
+  __device__ f32x4 epi_pre(int, int, int col) const {
+    const float b = bias[col];
+    return f32x4{b, b, b, b};
+  }
+  __device__ void epi_post(int, int row, int col, f32x4 v, f32x4 b) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) out[(size_t)(row + r) * OC + col] = relu(v[r] + b[r]);
+  }
 };
 using PConv2Fwd = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>;
 using PConv3Fwd = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>;
@@ -659,6 +669,15 @@ struct PFc1FwdT {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (row + r < M) a4[(size_t)(row + r) * 512 + col] = relu(v[r] + b3[col]);
+  }
+  __device__ f32x4 epi_pre(int, int, int col) const {
+    const float b = b3[col];
+    return f32x4{b, b, b, b};
+  }
+  __device__ void epi_post(int, int row, int col, f32x4 v, f32x4 b) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (row + r < M) a4[(size_t)(row + r) * 512 + col] = relu(v[r] + b[r]);
   }
 };
 using PFc1Fwd = PFc1FwdT<>;
