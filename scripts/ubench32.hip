@@ -345,6 +345,27 @@ int main(int argc, char** argv) {
   const float* W1 = w + 8192 + 32;
   const float* W2 = W1 + 32768 + 64;
   const float* W3 = W2 + 36864 + 64;
+  if (argc > 1 && std::string(argv[1]) == "tail") {   // grid-tail check: the B = 1024 layer launches at batches around 1024
+    for (int B : {896, 960, 992, 1002, 1008, 1016, 1024, 1040, 1088, 1152}) {
+      char n[64];
+      printf("--- B = %d\n", B);
+      snprintf(n, sizeof n, "conv2_fwd t64x32 B%d", B);
+      run1(n, PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32>{grid(B * 81, 64, 64, 32, 1), a1, W1, W1, a2, B * 81}, 2.0 * B * 81 * 64 * 512);
+      snprintf(n, sizeof n, "conv3_fwd t64x32 B%d", B);
+      run1(n, PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32>{grid(B * 49, 64, 64, 32, 1), a2, W2, W2, a3, B * 49}, 2.0 * B * 49 * 64 * 576);
+      snprintf(n, sizeof n, "conv3_fwd t64x64 B%d", B);
+      run1(n, PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>{grid(B * 49, 64, 64, 64, 1), a2, W2, W2, a3, B * 49}, 2.0 * B * 49 * 64 * 576);
+      snprintf(n, sizeof n, "fc1_fwd t32x32 B%d", B);
+      run1(n, PFc1FwdT<32, 32, 2, 2>{grid(B, 32, 512, 32, 1), a3, W3, W3, a4, B}, 2.0 * B * 3136 * 512);
+      snprintf(n, sizeof n, "conv3 pair pxg B%d", B);
+      run2(n, PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>{grid(576, 64, 64, 64, (B + 15) / 16), a2, dz3, slab, B},
+           PConv3DgradPxG<32, 64, 2, 2>{{Grid{(B + 31) / 32, 1, 49}, dz3, W2, a2, dz2, B}}, 4.0 * B * 49 * 64 * 576);
+      snprintf(n, sizeof n, "conv2 pair px B%d", B);
+      run2(n, PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>{grid(512, 64, 64, 64, (B + 15) / 16), a1, dz2, slab, B},
+           PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, W1, a1, dz1, B}, 4.0 * B * 81 * 64 * 512);
+    }
+    return 0;
+  }
   if (argc > 1 && std::string(argv[1]) == "bwd") {   // pixel-major backward data: one pixel per tile vs pixel groups
     for (int B : {1024, 8192}) {
       const double f3 = 2.0 * B * 49 * 64 * 576, f2 = 2.0 * B * 81 * 64 * 512;
