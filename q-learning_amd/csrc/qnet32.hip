@@ -632,6 +632,31 @@ static int num_cus() {
 
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
+// training-batch conv2 / conv3 forward over M rows on a balanced grid (PConv2FwdR / PConv3FwdR): `whole` 64 x 64 tiles,
+// a multiple of the CU count, plus the remaining rows as 16 x 64 tiles; 0 when the shape has no such split (fewer whole
+// tiles than CUs, or more than half a tile per CU left over) and the plain grid runs.  At B = 1024 (784 / 1296 whole
+// tiles: 16 left over after 3 / 5 per CU) in place at C3: conv3 forward 42.4 -> 38.4 us, conv2 forward 56.2 -> 53.3 us
+// (`QLX_F32_FWD_BALANCED=0`: the plain 64 x 32 grid).
+static int balanced_whole_tiles(int M) {
+  if (std::getenv("QLX_F32_FWD_BALANCED") && std::getenv("QLX_F32_FWD_BALANCED")[0] == '0') return 0;
+  const int ncu = num_cus(), t = M / 64, whole = t - t % ncu;
+  if (whole < ncu || M - whole * 64 > 32 * ncu) return 0;
+  return whole;
+}
+
+template <class PW, class PR, class PF>
+static void conv_fwd(qlx_model* m, int M, const float* in, const float* wt, const float* bias, float* out, const char* scope,
+                     double work, hipStream_t s, const PF& plain) {
+  const int whole = balanced_whole_tiles(M);
+  if (!whole) {
+    launch(m, plain, scope, work, s);
+    return;
+  }
+  const PW pw{Grid{whole, 1, 1}, in, wt, bias, out, M};
+  const PR pr{{Grid{(M - whole * 64 + 15) / 16, 1, 1}, in, wt, bias, out, M}, whole * 4};
+  launch_pair(m, pw, pr, NoSide{}, scope, work, s);
+}
+
 // forward over B samples in chunks of the workspace's forward chunk: a1..a3 hold the last chunk (the whole batch when
 // B <= chunk, as training needs), a4 all B samples
 void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s) {
@@ -657,6 +682,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       debug_sync(s, sc);
     }
     if (big) {
+      // (plain grids: 40.5 / 24.5 whole tiles per CU at 8,192 samples; the balanced split measured 373 -> 385 us on conv2)
       launch(m, PConv2Fwd{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, "f32_conv2_fwd_big",
              2.0 * n * 81 * 64 * 512, s);
       launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd_big",
@@ -664,10 +690,10 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
              2.0 * n * 3136 * 512, s);
     } else {
-      launch(m, PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, "f32_conv2_fwd",
-             2.0 * n * 81 * 64 * 512, s);
-      launch(m, PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd",
-             2.0 * n * 49 * 64 * 576, s);
+      conv_fwd<PConv2Fwd, PConv2FwdR>(m, n * 81, w.fa1, p + voff(2), p + voff(3), w.fa2, "f32_conv2_fwd", 2.0 * n * 81 * 64 * 512, s,
+                                      PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81});
+      conv_fwd<PConv3Fwd, PConv3FwdR>(m, n * 49, w.fa2, p + voff(4), p + voff(5), w.fa3, "f32_conv3_fwd", 2.0 * n * 49 * 64 * 576, s,
+                                      PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49});
       launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
              2.0 * n * 3136 * 512, s);
     }

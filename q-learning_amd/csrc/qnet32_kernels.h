@@ -645,6 +645,19 @@ using PConv3Fwd = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>;
 // training-batch (B <= 2048) tile shapes: more, narrower blocks (scripts/ubench32.hip sweep at B = 1024)
 using PConv2FwdS = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>;
 using PConv3FwdS = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
+// Balanced grids (f32_forward): whole 64 x 64 tiles in a multiple of the CU count, then the rows left over as 16 x 64
+// tiles (RowShift: row tiles counted past the whole ones) in the same launch, so every CU gets the same work instead of
+// a few CUs running one more whole tile at the end.  A 16 x 64 tile is four waves with one chain each (the same k order).
+template <class Base>
+struct RowShift : Base {
+  int tm0;
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const {
+    Base::decode(lb, tm, tn, z);
+    tm += tm0;
+  }
+};
+using PConv2FwdR = RowShift<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 1, 4>>;
+using PConv3FwdR = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 1, 4>>;
 
 // fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3)
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>

@@ -345,6 +345,43 @@ int main(int argc, char** argv) {
   const float* W1 = w + 8192 + 32;
   const float* W2 = W1 + 32768 + 64;
   const float* W3 = W2 + 36864 + 64;
+  if (argc > 1 && std::string(argv[1]) == "split") {   // balanced grids: whole tiles per CU + the remainder as 16-row tiles
+    const int B = 1024;
+    const double f3 = 2.0 * B * 49 * 64 * 576, f2 = 2.0 * B * 81 * 64 * 512;
+    using C3W = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64>;
+    using C3N = PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2>;
+    using C3M = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 1, 4>>;
+    using C3H = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 32, 64, 2, 2>>;
+    using C2W = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64>;
+    using C2N = PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2>;
+    using C2M = RowShift<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 1, 4>>;
+    const int M3 = B * 49, M2 = B * 81;
+    for (int rep = 0; rep < 2; ++rep) {
+      run1("conv3_fwd t64x32 (now)", C3N{grid(M3, 64, 64, 32, 1), a2, W2, W2, a3, M3}, f3);
+      run1("conv3_fwd t64x64", C3W{grid(M3, 64, 64, 64, 1), a2, W2, W2, a3, M3}, f3);
+      run2("conv3_fwd 768 t64x64 + 64 t16x64", C3W{Grid{768, 1, 1}, a2, W2, W2, a3, M3},
+           C3M{{Grid{64, 1, 1}, a2, W2, W2, a3, M3}, 3072}, f3);
+      run2("conv3_fwd 64 t16x64 + 768 t64x64", C3M{{Grid{64, 1, 1}, a2, W2, W2, a3, M3}, 3072},
+           C3W{Grid{768, 1, 1}, a2, W2, W2, a3, M3}, f3);
+      run2("conv3_fwd 768 t64x64 + 32 t32x64", C3W{Grid{768, 1, 1}, a2, W2, W2, a3, M3},
+           C3H{{Grid{32, 1, 1}, a2, W2, W2, a3, M3}, 1536}, f3);
+      run2("conv3_fwd 1536 t64x32 + 64 t16x64", C3N{Grid{768, 2, 1}, a2, W2, W2, a3, M3},
+           C3M{{Grid{64, 1, 1}, a2, W2, W2, a3, M3}, 3072}, f3);
+      run2("conv3_fwd 64 t16x64 + 1536 t64x32", C3M{{Grid{64, 1, 1}, a2, W2, W2, a3, M3}, 3072},
+           C3N{Grid{768, 2, 1}, a2, W2, W2, a3, M3}, f3);
+      run1("conv2_fwd t64x32 (now)", C2N{grid(M2, 64, 64, 32, 1), a1, W1, W1, a2, M2}, f2);
+      run1("conv2_fwd t64x64", C2W{grid(M2, 64, 64, 64, 1), a1, W1, W1, a2, M2}, f2);
+      run2("conv2_fwd 1280 t64x64 + 64 t16x64", C2W{Grid{1280, 1, 1}, a1, W1, W1, a2, M2},
+           C2M{{Grid{64, 1, 1}, a1, W1, W1, a2, M2}, 5120}, f2);
+      run2("conv2_fwd 64 t16x64 + 1280 t64x64", C2M{{Grid{64, 1, 1}, a1, W1, W1, a2, M2}, 5120},
+           C2W{Grid{1280, 1, 1}, a1, W1, W1, a2, M2}, f2);
+      run2("conv2_fwd 2560 t64x32 + 64 t16x64", C2N{Grid{1280, 2, 1}, a1, W1, W1, a2, M2},
+           C2M{{Grid{64, 1, 1}, a1, W1, W1, a2, M2}, 5120}, f2);
+      run2("conv2_fwd 64 t16x64 + 2560 t64x32", C2M{{Grid{64, 1, 1}, a1, W1, W1, a2, M2}, 5120},
+           C2N{Grid{1280, 2, 1}, a1, W1, W1, a2, M2}, f2);
+    }
+    return 0;
+  }
   if (argc > 1 && std::string(argv[1]) == "tail") {   // grid-tail check: the B = 1024 layer launches at batches around 1024
     for (int B : {896, 960, 992, 1002, 1008, 1016, 1024, 1040, 1088, 1152}) {
       char n[64];
