@@ -632,6 +632,16 @@ static int num_cus() {
 
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
+// conv1 forward / weight gradient: MFMA steps whose frame operands are all 0 are not issued (exact, see k_conv1_fwd32);
+// QLX_F32_C1_SKIP=0 issues every step (A/B measurement)
+static int c1_skip() {
+  static const int v = [] {
+    const char* e = std::getenv("QLX_F32_C1_SKIP");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
 // training-batch conv2 / conv3 forward over M rows on a balanced grid (PConv2FwdR / PConv3FwdR): `whole` 64 x 64 tiles,
 // a multiple of the CU count, plus the remaining rows as 16 x 64 tiles; 0 when the shape has no such split (fewer whole
 // tiles than CUs, or more than half a tile per CU left over) and the plain grid runs.  At B = 1024 (784 / 1296 whole
@@ -677,7 +687,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       auto kern = big ? k_conv1_fwd32<1> : k_conv1_fwd32<0>;
       set_lds_limit((const void*)kern, 2 * kC1Frames);
       hipExtLaunchKernelGGL(kern, dim3(std::min(n, 2 * num_cus())), dim3(256), 2 * kC1Frames, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
-                            p + voff(0), p + voff(1), w.fa1);
+                            p + voff(0), p + voff(1), w.fa1, c1_skip());
       QLX_HIP(hipGetLastError());
       debug_sync(s, sc);
     }
@@ -821,7 +831,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     hipEvent_t ea = nullptr, eb = nullptr;
     if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);
-    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1);
+    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1, c1_skip());
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv1_wgrad32");
   }

@@ -1257,13 +1257,18 @@ __device__ __forceinline__ void c1_stage(uint32_t* dst, const uint4 (&pf)[7]) {
 __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >> (8 * i)) & 0xFFu); }
 
 // forward: a1[b][r][oc] = relu(chain over k = (kh, kw, c) of x * W0[kh][kw][c][oc] + b0[oc]), r = (oh, ow).
-// Wave w owns output channels (w & 1) * 16 .. + 15 and the 16-row tiles rt = (w >> 1) + 2 j (13 / 12 of the 25); one
+// Wave w owns output channels (w & 1) * 16 .. + 15 and the tiles t = (w >> 1) + 2 j (13 / 12 of the 25); tile t is the
+// 4 x 4 patch of output positions oh = 4 (t / 5) + 0..3, ow = 4 (t % 5) + 0..3 (tile row l = (oh % 4, ow % 4)); one
 // v_mfma_f32_16x16x4_f32 per (tile, kh, kw) with c on the lane groups, W0 fragments resident in VGPRs.
+// Zero steps (skip != 0): an MFMA whose 64 frame values are all 0 adds +-0 to each of its 16 x 16 chains, which leaves
+// every chain as it is (a chain from +0 never holds -0: x + (-x) and +0 + -0 round to +0), so it is not issued.  The
+// frames are mostly background (0), and a patch tile's receptive field (20 x 20 pixels per frame) is often all of it
+// (~70 % of the steps at C3), where a tile of 16 consecutive positions crosses the side walls.  Exact for finite W0.
 // ROLE only names the instantiation (0: training batches, 1: chunk-size target / acting passes), so a kernel trace
 // tells the two launch shapes apart
 template <int ROLE>
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0, const float* b0,
-                                                        float* a1) {
+                                                        float* a1, int skip) {
   extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // [2][4 slots][1776 dwords]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1279,8 +1284,8 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
   for (int j = 0; j < 7; ++j) ob2[j] = 0;
 #pragma unroll
   for (int j = 0; j < 13; ++j) {
-    const int r = (rp + 2 * j) * 16 + (lane & 15);
-    const int oh = r / 20, ow = r - oh * 20;
+    const int t = rp + 2 * j < 25 ? rp + 2 * j : 0, l = lane & 15;
+    const int oh = 4 * (t / 5) + (l >> 2), ow = 4 * (t % 5) + (l & 3);
     ob2[j >> 1] |= (uint32_t)(g * kC1SlotDw + 4 * oh * 21 + ow) << (16 * (j & 1));
   }
   const int nt = rp == 0 ? 13 : 12;
@@ -1307,19 +1312,31 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
       const int kh = kq >> 1, hw = kq & 1;
       const int off = kh * 21 + hw;
       uint32_t d[13];
+      bool on[13];
 #pragma unroll
-      for (int j = 0; j < 13; ++j)
-        if (j < nt) d[j] = fr[((ob2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + off];
+      for (int j = 0; j < 13; ++j) {
+        d[j] = j < nt ? fr[((ob2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + off] : 0u;
+        on[j] = j < nt && (!skip || __builtin_amdgcn_ballot_w64(d[j] != 0u) != 0);   // wave-uniform
+      }
+#ifdef QLX_C1_KW_OUTER
 #pragma unroll
       for (int kw = 0; kw < 4; ++kw)
 #pragma unroll
         for (int j = 0; j < 13; ++j)
-          if (j < nt) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[j], kw), wf[kq * 4 + kw], acc[j], 0, 0, 0);
+          if (on[j]) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[j], kw), wf[kq * 4 + kw], acc[j], 0, 0, 0);
+#else
+      // one branch per (kq, tile): its four kw steps chain on one accumulator back to back
+#pragma unroll
+      for (int j = 0; j < 13; ++j)
+        if (on[j])
+#pragma unroll
+          for (int kw = 0; kw < 4; ++kw) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[j], kw), wf[kq * 4 + kw], acc[j], 0, 0, 0);
+#endif
     }
 #pragma unroll
     for (int j = 0; j < 13; ++j)
       if (j < nt) {
-        const int r0 = (rp + 2 * j) * 16 + 4 * g;
+        const int t = rp + 2 * j, r0 = (4 * (t / 5) + g) * 20 + 4 * (t % 5);   // rows (oh, ow .. ow + 3) of the patch
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[j][i] + bias);
       }
@@ -1329,7 +1346,8 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
-// x[r][m] dz1[r][oc], m = (kh, kw, c) HWIO; bias slab[z][256][oc] = ((C0 + C1) + C2) + C3 with Cq the chain over (b, rs)
+// x[r][m] dz1[r][oc] (steps whose frame values are all 0 skipped when skip != 0, exactly as in the forward; exact for
+// finite dz1), m = (kh, kw, c) HWIO; bias slab[z][256][oc] = ((C0 + C1) + C2) + C3 with Cq the chain over (b, rs)
 // ascending of dz1[b][4 rs + q][oc] (the four lane groups' chains of the MFMA B operand).  Block (z, hh)
 // covers output channels hh * 16 .. + 15.  Wave w owns kh = 2 w, 2 w + 1: lane row rho = (kh low bit, h, c), tile
 // t = kw - 4 h, so one LDS dword (pixels 4 ow + 4 h .. + 3 of image row 4 oh + kh) feeds the lane's four MFMAs of a
@@ -1338,7 +1356,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
 constexpr int kC1WgradThreads = 256;
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
-                                                                       float* slab) {
+                                                                       float* slab, int skip) {
   extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1776] dwords, then dz [400][16] f32
   float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1SlotDw);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1390,8 +1408,9 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
       const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
       const float bv = dzs[r * 16 + l15];
       const uint32_t px = c1w[ao + 84 * oh + ow];
+      if (!skip || __builtin_amdgcn_ballot_w64(px != 0u) != 0)   // all 64 x 4 frame values 0: the step adds +-0 (see the forward)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px, t), bv, acc[t], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px, t), bv, acc[t], 0, 0, 0);
       if (wave == 0) bsum = __fadd_rn(bsum, bv);
     }
   }

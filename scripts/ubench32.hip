@@ -434,7 +434,7 @@ int main(int argc, char** argv) {
     {
       const int G = std::min(B, 512);
       CK(hipFuncSetAttribute((const void*)k_conv1_fwd32<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kC1Frames));
-      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32<0>, dim3(G), dim3(256), 2 * kC1Frames, 0, table, B, W0, W0 + 8192, a1); });
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32<0>, dim3(G), dim3(256), 2 * kC1Frames, 0, table, B, W0, W0 + 8192, a1, 1); });
       const double f = 2.0 * B * 400 * 32 * 256;
       printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_fwd (k_conv1_fwd32)", G, 2 * kC1Frames, us, f / us / 1e6,
              f / us / 1e6 / 157.3 * 100);
@@ -481,7 +481,7 @@ int main(int argc, char** argv) {
     {
       const int nz = B / 4, lds = kC1Frames + 400 * 16 * 4;
       CK(hipFuncSetAttribute((const void*)k_conv1_wgrad32, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(kC1WgradThreads), lds, 0, table, dz1, B, nz, slab); });
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(kC1WgradThreads), lds, 0, table, dz1, B, nz, slab, 1); });
       const double f = 2.0 * B * 400 * 256 * 32;
       printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_wgrad (k_conv1_wgrad32)", 2 * nz, lds, us,
              f / us / 1e6, f / us / 1e6 / 157.3 * 100);
