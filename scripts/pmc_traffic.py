@@ -18,10 +18,10 @@ SCOPES = {
     "fp32": {
         "f32_conv1_fwd": "k_conv1_fwd32<0>",
         "f32_conv1_fwd_big": "k_conv1_fwd32<1>",
-        "f32_conv2_fwd": "PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 32, 2, 2,",
-        "f32_conv2_fwd_big": "PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2,",
-        "f32_conv3_fwd": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 32, 2, 2,",
-        "f32_conv3_fwd_big": "PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2,",
+        "f32_conv2_fwd": "k_gemm32_pair<qlx::q32::PConvFwd<20, 20,",   # the balanced grid (whole + 16-row tiles)
+        "f32_conv2_fwd_big": "k_gemm32<qlx::q32::PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2,",
+        "f32_conv3_fwd": "k_gemm32_pair<qlx::q32::PConvFwd<9, 9,",
+        "f32_conv3_fwd_big": "k_gemm32<qlx::q32::PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2,",
         "f32_fc1_fwd": "k_gemm32<qlx::q32::PFc1FwdT<32, 32, 2, 2,",
         "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<64, 64, 2, 2,",
         "f32_fc1_bwd": "k_gemm32_pair<qlx::q32::PFc1WgradT",
