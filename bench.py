@@ -360,7 +360,12 @@ class Run:
         for k in GEMM_SCOPES[self.precision]:
             if k in c and c[k]["total_us_per_step"] > 0:
                 t = rate(c[k]["work"], c[k]["total_us_per_step"], 1e6)
-                layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
+                if k in ZERO_STEP_SCOPES:   # not an MFMA utilisation: the all-zero frame steps are not issued
+                    layers[k] = {"tflops_dense_equivalent": round(t, 2), "mfma_frac": None, "avg_us": round(c[k]["avg_us"], 2),
+                                 "note": "dense FLOP / time; MFMA steps whose frame operands are all 0 are not issued "
+                                         "(exact, DESIGN.md 4.1)"}
+                else:
+                    layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
         upd = self.updates / max(self.steps, 1) / max(self.ctl.world, 1)   # updates per vector step on one GPU
         B = self.args.batch
         t_samp = sum(c[k]["total_us_per_step"] for k in SAMPLE_SCOPES[self.precision][:3] if k in c)
@@ -388,6 +393,10 @@ class Run:
 
     def value(self):
         return self.env_steps / self.dt
+
+
+# conv1 launches skip the MFMA steps whose u8 frame operands are all 0 (k_conv1_fwd32 / k_conv1_wgrad32)
+ZERO_STEP_SCOPES = ("f32_conv1_fwd", "f32_conv1_fwd_big", "f32_conv1_wgrad")
 
 
 def pmc_traffic(precision, scope):
