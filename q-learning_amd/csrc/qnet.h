@@ -38,6 +38,12 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float *fdz1 = nullptr, *fdz2 = nullptr, *fdz3 = nullptr, *fdz4 = nullptr;
   float *fslab1 = nullptr, *fslab2 = nullptr, *fslab3 = nullptr;
   float* fpart = nullptr;   // clip_by_norm segment partials
+  // background rows of the conv2 / conv3 forward (qnet32_kernels.h C1Lists): row lists of the forward chunk, the list
+  // counters of two forwards (double-buffered by forward parity), the constant rows relu(b0) / c2 / c3
+  int *frl2 = nullptr, *frl3 = nullptr;
+  unsigned long long* frcnt = nullptr;
+  float* fbgc = nullptr;
+  int fparity = 0;
   int fchunk = 0;
   void* fgrad = nullptr;
   int fgrad_batch = 0;

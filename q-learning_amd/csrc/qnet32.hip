@@ -558,6 +558,7 @@ void f32_workspace(qlx_model* m, int B) {
   for (int v = 0; v < kNumVars; ++v) nseg += segs_of(v);
   const size_t o_part = take((size_t)nseg * 4);
   const size_t o_loss = take(64);
+  const size_t o_rl2 = take((size_t)C * 81 * 4), o_rl3 = take((size_t)C * 49 * 4), o_rcnt = take(4 * 8), o_bgc = take(160 * 4);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -569,6 +570,11 @@ void f32_workspace(qlx_model* m, int B) {
   w.done = (uint8_t*)(base + o_done);
   w.fpart = (float*)(base + o_part);
   w.loss = (float*)(base + o_loss);
+  w.frl2 = (int*)(base + o_rl2); w.frl3 = (int*)(base + o_rl3);
+  w.frcnt = (unsigned long long*)(base + o_rcnt);
+  w.fbgc = (float*)(base + o_bgc);
+  QLX_HIP(hipMemset(w.frcnt, 0, 4 * 8));
+  w.fparity = 0;
   w.fchunk = C;
   m->ws_batch = B;
 }
@@ -654,6 +660,26 @@ static int balanced_whole_tiles(int M) {
   return whole;
 }
 
+// conv2 / conv3 forward over the non-background rows (PConvFwdL) with the background rows written by the side blocks
+template <class P, class S>
+static void launch_list(qlx_model* m, const P& p, const S& side, const char* scope, double work, hipStream_t s) {
+  hipEvent_t ea = nullptr, eb = nullptr;
+  if (m->prof) m->prof->ext(scope, work, &ea, &eb);
+  const size_t lds = std::max(gemm_lds_bytes<P>(), S::LDS);
+  hipExtLaunchKernelGGL((k_gemm32_side<P, S>), dim3(side.blocks() + p.g.blocks()), dim3(threads_of<P>()), lds, s, ea, eb, 0u, p, side);
+  QLX_HIP(hipGetLastError());
+  debug_sync(s, scope);
+}
+
+// background rows (see C1Lists in qnet32_kernels.h): on by default; QLX_F32_BG=0 computes every conv2 / conv3 row (A/B)
+static bool bg_rows() {
+  static const bool v = [] {
+    const char* e = std::getenv("QLX_F32_BG");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <class PW, class PR, class PF>
 static void conv_fwd(qlx_model* m, int M, const float* in, const float* wt, const float* bias, float* out, const char* scope,
                      double work, hipStream_t s, const PF& plain) {
@@ -680,18 +706,46 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     // training-size batches the narrower tiles that put more blocks on the chip (scripts/ubench32.hip sweep); the two
     // shapes are separate kernels and separate profiler scopes (suffix _big)
     const bool big = n > 2048;
+    // background rows: conv1 lists them, conv2 / conv3 run the rest (the list counters alternate between forwards)
+    const bool lists = bg_rows();
+    unsigned long long* cnt = w.frcnt + 2 * w.fparity;
+    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cnt, w.frcnt + 2 * (w.fparity ^ 1)};
+    if (lists) w.fparity ^= 1;
     {
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
       hipEvent_t ea = nullptr, eb = nullptr;
       if (m->prof) m->prof->ext(sc, 2.0 * n * 400 * 32 * 256, &ea, &eb);
       auto kern = big ? k_conv1_fwd32<1> : k_conv1_fwd32<0>;
-      set_lds_limit((const void*)kern, 2 * kC1Frames);
-      hipExtLaunchKernelGGL(kern, dim3(std::min(n, 2 * num_cus())), dim3(256), 2 * kC1Frames, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
-                            p + voff(0), p + voff(1), w.fa1, c1_skip());
+      const int G = std::min(n, 2 * num_cus());
+      constexpr int kMaxIt = 64;   // samples per block (flags kept in LDS until the block's lists are written)
+      QLX_CHECK((n + G - 1) / G <= kMaxIt, QLX_E_STATE, "conv1 forward: too many samples per block");
+      const size_t lds = 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
+      set_lds_limit((const void*)kern, 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)kMaxIt * 6 * 8);
+      hipExtLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
+                            p + voff(0), p + voff(1), w.fa1, c1_skip(), L);
       QLX_HIP(hipGetLastError());
       debug_sync(s, sc);
     }
-    if (big) {
+    if (lists) {
+      const int nw = std::min(256, std::max(16, n / 16));   // background-row blocks
+      const BgRows<4, 32> s2{nw, w.frl2, cnt, n * 81, p + voff(1), nullptr, p + voff(2), p + voff(3), w.fa2, w.fbgc + 32};
+      const BgRows<3, 64> s3{nw, w.frl3, cnt + 1, n * 49, nullptr, w.fbgc + 32, p + voff(4), p + voff(5), w.fa3, nullptr};
+      if (big) {
+        launch_list(m, PConv2FwdL<64, 64, 2, 2>{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cnt}, s2,
+                    "f32_conv2_fwd_big", 2.0 * n * 81 * 64 * 512, s);
+        launch_list(m, PConv3FwdL<64, 64, 2, 2>{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cnt + 1},
+                    s3, "f32_conv3_fwd_big", 2.0 * n * 49 * 64 * 576, s);
+        launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
+               2.0 * n * 3136 * 512, s);
+      } else {
+        launch_list(m, PConv2FwdL<64, 32, 2, 2>{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cnt}, s2,
+                    "f32_conv2_fwd", 2.0 * n * 81 * 64 * 512, s);
+        launch_list(m, PConv3FwdL<64, 32, 2, 2>{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cnt + 1},
+                    s3, "f32_conv3_fwd", 2.0 * n * 49 * 64 * 576, s);
+        launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
+               2.0 * n * 3136 * 512, s);
+      }
+    } else if (big) {
       // (plain grids: 40.5 / 24.5 whole tiles per CU at 8,192 samples; the balanced split measured 373 -> 385 us on conv2)
       launch(m, PConv2Fwd{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81}, "f32_conv2_fwd_big",
              2.0 * n * 81 * 64 * 512, s);

@@ -166,6 +166,17 @@ struct HasEpiPre : std::false_type {};
 template <class P>
 struct HasEpiPre<P, std::void_t<decltype(std::declval<const P&>().epi_pre(0, 0, 0))>> : std::true_type {};
 #endif
+// the type epi_pre returns (f32x4 unless the policy says otherwise)
+template <class P, bool = HasEpiPre<P>::value>
+struct PreOf { using type = f32x4; };
+template <class P>
+struct PreOf<P, true> { using type = decltype(std::declval<const P&>().epi_pre(0, 0, 0)); };
+
+// Optional tile filter: a policy with active(z, row0) skips the tiles it returns false for (rows counted on the device)
+template <class P, class = void>
+struct HasActive : std::false_type {};
+template <class P>
+struct HasActive<P, std::void_t<decltype(std::declval<const P&>().active(0, 0))>> : std::true_type {};
 
 // One output tile of a policy P (see the policies below for the members it provides):
 //   acc[row][col] = sum over the slabs s = 0 .. nslabs(z) - 1 and k = 0 .. 31 of A(z, s, row, k) * B(z, s, col, k),
@@ -195,6 +206,9 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   int tm, tn, z;
   p.decode(lb, tm, tn, z);
   const int row0 = tm * P::BM, col0 = tn * P::BN;
+  if constexpr (HasActive<P>::value) {
+    if (!p.active(z, row0)) return;
+  }
   const int ns = p.nslabs(z) / G, s_base = kg * ns;   // this group's slabs: s_base + [0, ns)
   typename ACtxOf<P>::type actx{};
   if constexpr (HasACtx<P>::value) actx = p.a_ctx(z, row0, tid);
@@ -296,7 +310,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     lds_barrier();
   };
   constexpr bool PRE = HasEpiPre<P>::value && MF == 16 && G == 1;
-  f32x4 pre[TM][TN];
+  typename PreOf<P>::type pre[TM][TN];
   if constexpr (PRE) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -589,6 +603,15 @@ __global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, c
   else tail.run(h - g1 - g2, lds);
 }
 
+// one GEMM plus `side` leading blocks running S (the background rows of a list forward)
+template <class P, class S>
+__global__ __launch_bounds__(threads_of<P>()) void k_gemm32_side(const P p, const S side) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x, ns = side.blocks();
+  if (b < ns) { side.run(b, lds); return; }
+  body(p, block_order<P>(b - ns, (int)gridDim.x - ns), lds);
+}
+
 struct NoSide {
   static constexpr size_t LDS = 0;
   __host__ __device__ int blocks() const { return 0; }
@@ -658,6 +681,133 @@ struct RowShift : Base {
 };
 using PConv2FwdR = RowShift<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 1, 4>>;
 using PConv3FwdR = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 1, 4>>;
+
+// conv2 / conv3 forward over the non-background rows (see C1Lists): GEMM row r is output row list[r] (chunk-local
+// b * OH * OW + p) for r < the list's count (device memory); tiles past the count return at once.  Tiles are taken in
+// hardware block order, so the live ones (the first) spread over all XCDs.  Every output is the chain PConvFwd computes.
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+struct PConvFwdL {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false, RAW_ORDER = true;
+  static constexpr bool LOAD_FENCE = !(H == 20 && BN_ == 64);
+  static constexpr int R = OH * OW;
+  using OA = Opnd<BM, false, 16>;
+  static constexpr int T = WM * WN * 64, NA = (OA::F4 + T - 1) / T;
+  Grid g;
+  const float* in;
+  const float* w;    // [KS][KS][C][OC]
+  const float* bias;
+  float* out;        // [rows][OC]
+  const int* list;
+  const unsigned long long* cnt;   // non-background rows << 32 | background rows
+  struct ACtx { int off[NA]; };
+  struct Pre { float b; int o[4]; };
+  __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
+  __host__ __device__ int nslabs(int) const { return KS * KS * C / BK; }
+  __device__ int rows() const { return (int)(*cnt >> 32); }
+  __device__ bool active(int, int row0) const { return row0 < rows(); }
+  // input offsets of the thread's NA operand rows (-1: past the count)
+  __device__ ACtx a_ctx(int, int row0, int tid) const {
+    ACtx c;
+    const int n = rows();
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      int r, k;
+      OA::coord(tid + i * T, r, k);
+      const int row = row0 + r;
+      const int e = row < n ? list[row] : -1;
+      const int b = e / R, p = e - b * R, oh = p / OW, ow = p - oh * OW;
+      c.off[i] = e >= 0 ? ((b * H + oh * S) * W + ow * S) * C : -1;
+    }
+    return c;
+  }
+  __device__ f32x4 ldA_c(const ACtx& c, int i, int, int s, int, int k) const {
+    const int tap = (s * BK) / C, c0 = (s * BK) % C, kh = tap / KS, kw = tap % KS;
+    const int o = c.off[i];
+    return ld4m(in + (size_t)(o < 0 ? 0 : o) + (kh * W + kw) * C + c0 + k, o >= 0);
+  }
+  __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w + (size_t)(s * BK + k) * OC + col); }
+  __device__ Pre epi_pre(int, int row, int col) const {
+    const int n = rows();
+    Pre q;
+    q.b = bias[col];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q.o[r] = row + r < n ? list[row + r] * OC : -1;
+    return q;
+  }
+  __device__ void epi_post(int, int, int col, f32x4 v, const Pre& q) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (q.o[r] >= 0) out[(size_t)q.o[r] + col] = relu(v[r] + q.b);
+  }
+};
+template <int BM, int BN, int WM, int WN>
+using PConv2FwdL = PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, BM, BN, WM, WN>;
+template <int BM, int BN, int WM, int WN>
+using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN>;
+
+// Leading blocks of a list launch: the background rows.  Wave 0 of every block computes the constant output row
+// c[oc] = relu(chain over k = (kh, kw, ch) of x[ch] W[kh][kw][ch][oc] + bias[oc]) - the GEMM's chain on the constant
+// input row x: conv2: x = relu(0 + b0) (every conv1 output over background pixels), conv3: x = c2 - then the block
+// writes c to its share of the background rows (the list's back end).  Block 0 also stores c (the next layer's x).
+template <int KS, int C>
+struct BgRows {
+  static constexpr int K = KS * KS * C, KC = 32, NCH = K / KC;   // W staged in LDS KC k-rows at a time (double-buffered)
+  static_assert(K % KC == 0 && C % KC == 0, "chunks of KC k-rows within one tap");
+  static constexpr size_t LDS = (128 + 2 * KC * 64) * sizeof(float);   // below the GEMM tiles' LDS
+  int nblk;
+  const int* list;
+  const unsigned long long* cnt;
+  int total;               // list length (n * rows per sample)
+  const float* x_bias;     // conv2: b0 (x = relu(0 + b0)); null: x = x_row
+  const float* x_row;      // conv3: c2
+  const float* w;          // [KS][KS][C][64]
+  const float* bias;
+  float* out;              // [rows][64]
+  float* c_out;            // block 0 stores c here (null: not needed)
+  __host__ __device__ int blocks() const { return nblk; }
+  __device__ void run(int blk, float* lds) const {
+    const int tid = threadIdx.x;
+    float* xs = lds;         // x [C]
+    float* cs = lds + 64;    // c [64]
+    float* wb = lds + 128;   // [2][KC k][64 oc]
+    if (tid < C) xs[tid] = x_bias ? relu(0.0f + x_bias[tid]) : x_row[tid];
+    f32x4 r[KC / 16];
+    auto ldw = [&](int q) {
+#pragma unroll
+      for (int i = 0; i < KC / 16; ++i) r[i] = ld4(w + (size_t)q * KC * 64 + 4 * (tid + 256 * i));
+    };
+    auto stw = [&](int q) {
+#pragma unroll
+      for (int i = 0; i < KC / 16; ++i) *reinterpret_cast<f32x4*>(wb + (q & 1) * KC * 64 + 4 * (tid + 256 * i)) = r[i];
+    };
+    ldw(0);
+    stw(0);
+    __syncthreads();
+    float acc = 0.0f;
+    for (int q = 0; q < NCH; ++q) {
+      if (q + 1 < NCH) ldw(q + 1);
+      if (tid < 64) {   // wave 0: the chain, k = KC q + kk in order (channel (KC q + kk) % C)
+        const float* wq = wb + (q & 1) * KC * 64;
+        const float* xq = xs + (q * KC) % C;
+#pragma unroll
+        for (int kk = 0; kk < KC; ++kk) acc = __builtin_fmaf(xq[kk], wq[kk * 64 + tid], acc);
+      }
+      if (q + 1 < NCH) stw(q + 1);
+      __syncthreads();
+    }
+    if (tid < 64) {
+      const float c = relu(acc + bias[tid]);
+      cs[tid] = c;
+      if (blk == 0 && c_out) c_out[tid] = c;
+    }
+    __syncthreads();
+    const int nbg = (int)(uint32_t)*cnt, q = tid & 15;
+    const f32x4 v = ld4(cs + 4 * q);
+    for (int i = blk * 16 + (tid >> 4); i < nbg; i += nblk * 16)
+      *reinterpret_cast<f32x4*>(out + (size_t)list[total - 1 - i] * 64 + 4 * q) = v;
+  }
+};
 
 // fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3)
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
@@ -1256,6 +1406,99 @@ __device__ __forceinline__ void c1_stage(uint32_t* dst, const uint4 (&pf)[7]) {
 }
 __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >> (8 * i)) & 0xFFu); }
 
+// Background rows.  A conv2 output position (i, j) sees the pixels x in [8 i, 8 i + 20), y in [8 j, 8 j + 20) of the four
+// frames (conv1 positions 2 i .. 2 i + 3 of 8 x 8 pixels at stride 4); when they are all 0 (the black background), every
+// conv1 output it reads is relu(0 + b0), so its input row is the same vector for every such position of every sample and
+// its output is the same chain: one constant row c2.  A conv3 position (i, j) whose nine conv2 positions are all
+// background (pixels [8 i, 8 i + 36)) likewise has the constant output c3.  So the conv2 / conv3 forward GEMMs run over
+// the non-background rows only (PConvFwdL), and the background rows are written with c2 / c3 (BgRows).  Exact: the same
+// chains on the same operands, whatever row a GEMM tile holds them in.
+// The forward's conv1 kernel classifies each sample while its frames are staged: a 4 x 4 pixel block (one s2d chunk per
+// frame) marks bit by of the row mask rm[bx] (21 x 21 blocks) when any of its bytes is non-zero, and a conv2 (conv3) row is
+// background when the 5 x 5 (9 x 9) blocks from (2 i, 2 j) are unmarked.  Row lists: rl[n * R] per layer (R = 81 / 49
+// rows per sample), entries b * R + p; the non-background rows from the front, the background rows from the back, their
+// counts in cnt (non-background << 32 | background), claimed per wave with one atomic (so the order of a list's entries
+// varies between runs; the values do not).
+struct C1Lists {
+  int* rl2;                       // null: no lists (every row computed)
+  int* rl3;
+  unsigned long long* cnt;        // this forward's counters: [0] conv2, [1] conv3
+  unsigned long long* cnt_next;   // the next forward's (double-buffered by forward parity), zeroed here
+};
+constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
+
+// (the thread index is laundered through an empty asm per call, so the address arithmetic is redone per sample instead
+// of being hoisted out of the sample loop into registers the MFMA loop needs: conv1 runs at the 256-VGPR limit)
+__device__ __forceinline__ int c1_opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+__device__ __forceinline__ void c1_mark(uint32_t* rm, const uint4 (&pf)[7]) {
+  const int t = c1_opaque_tid();
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int q = t + 256 * j;
+    if (q < kC1Chunks && (pf[j].x | pf[j].y | pf[j].z | pf[j].w) != 0u) {
+      const int pos = q % 441, bx = pos / 21, by = pos - bx * 21;
+      atomicOr(&rm[bx], 1u << by);
+    }
+  }
+}
+
+// a sample's row flags, one wave's share (waves 0, 1: conv2 rows p = tid; wave 2: conv3 rows p = tid - 128), as two
+// ballots (non-background / background rows) stored in LDS at the end of the sample's iteration; the list entries are
+// claimed and written once per wave after the block's last sample (c1_lists_flush), so no atomic's round trip is waited
+// for inside the sample loop
+__device__ __forceinline__ void c1_flags(const uint32_t* rm, unsigned long long* cl, int wave, int) {
+  const int tid = c1_opaque_tid();
+  const int R = wave < 2 ? 81 : 49, p = wave < 2 ? tid : tid - 128;
+  const bool valid = p < R;
+  const int pp = valid ? p : 0;
+  bool nonbg;
+  if (wave < 2) {
+    const int i = pp / 9, j = pp - 9 * i;
+    uint32_t mm = 0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) mm |= rm[2 * i + r];
+    nonbg = ((mm >> (2 * j)) & 0x1Fu) != 0u;
+  } else {
+    const int i = pp / 7, j = pp - 7 * i;
+    uint32_t mm = 0;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) mm |= rm[2 * i + r];
+    nonbg = ((mm >> (2 * j)) & 0x1FFu) != 0u;
+  }
+  const unsigned long long bn = __builtin_amdgcn_ballot_w64(valid && nonbg), bb = __builtin_amdgcn_ballot_w64(valid && !nonbg);
+  if ((tid & 63) == 0) {
+    cl[0] = bn;
+    cl[1] = bb;
+  }
+}
+// cl: [iteration][3 waves][2]; the block's samples b0, b0 + G, .. (nit of them)
+__device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int nit, int b0, int G, const C1Lists& L, int wave,
+                                               int tid, int B) {
+  const int lane = tid & 63, R = wave < 2 ? 81 : 49, p = wave < 2 ? tid : tid - 128;
+  int* rl = wave < 2 ? L.rl2 : L.rl3;
+  unsigned long long tot = 0;
+  for (int it = 0; it < nit; ++it)
+    tot += ((unsigned long long)__builtin_popcountll(cl[(it * 3 + wave) * 2]) << 32) |
+           (unsigned long long)__builtin_popcountll(cl[(it * 3 + wave) * 2 + 1]);
+  unsigned long long old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(L.cnt + (wave < 2 ? 0 : 1), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0);
+  int on = (int)(old >> 32), og = (int)(uint32_t)old;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int it = 0; it < nit; ++it) {
+    const unsigned long long bn = cl[(it * 3 + wave) * 2], bb = cl[(it * 3 + wave) * 2 + 1];
+    const int e = (b0 + it * G) * R + p;
+    if ((bn >> lane) & 1ull) rl[on + __builtin_popcountll(bn & below)] = e;
+    else if ((bb >> lane) & 1ull) rl[B * R - 1 - (og + __builtin_popcountll(bb & below))] = e;
+    on += __builtin_popcountll(bn);
+    og += __builtin_popcountll(bb);
+  }
+}
+
 // forward: a1[b][r][oc] = relu(chain over k = (kh, kw, c) of x * W0[kh][kw][c][oc] + b0[oc]), r = (oh, ow).
 // Wave w owns output channels (w & 1) * 16 .. + 15 and the tiles t = (w >> 1) + 2 j (13 / 12 of the 25); tile t is the
 // 4 x 4 patch of output positions oh = 4 (t / 5) + 0..3, ow = 4 (t % 5) + 0..3 (tile row l = (oh % 4, ow % 4)); one
@@ -1268,10 +1511,18 @@ __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >>
 // tells the two launch shapes apart
 template <int ROLE>
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0, const float* b0,
-                                                        float* a1, int skip) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // [2][4 slots][1776 dwords]
+                                                        float* a1, int skip, const C1Lists L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // [2][4 slots][1776 dwords], rm [3][24], flags
+  uint32_t* rm = c1w + 2 * 4 * kC1SlotDw;
+  unsigned long long* cl = reinterpret_cast<unsigned long long*>(rm + 3 * kC1RmDw);   // [iteration][3][2] (c1_flags)
+  const bool lists = L.rl2 != nullptr;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (lists) {
+    if (blockIdx.x == 0 && tid < 2) L.cnt_next[tid] = 0ull;
+    if (tid < 3 * kC1RmDw) rm[tid] = 0u;
+    __syncthreads();
+  }
   const int ct = wave & 1, rp = wave >> 1;
   const int col = ct * 16 + (lane & 15), g = lane >> 4;
   float wf[64];
@@ -1296,6 +1547,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
   // frame pointers one sample ahead of the frames (scalar registers)
   C1Ptrs nxt = c1_ptrs(table, b + (int)gridDim.x < B ? b + (int)gridDim.x : b);
   c1_stage(c1w, pf);
+  if (lists) c1_mark(rm, pf);
   __syncthreads();
   for (int it = 0; b < B; b += gridDim.x, ++it) {
     const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
@@ -1304,6 +1556,10 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
       c1_prefetch(nxt, pf);
       nxt = c1_ptrs(table, nb + (int)gridDim.x < B ? nb + (int)gridDim.x : nb);
     }
+    // row masks: buffer it % 3 holds sample b's (complete since the last barrier, read by c1_flags at the end of this
+    // iteration); (it + 1) % 3 gets the next sample's at the end of this iteration; (it + 2) % 3, read at the end of
+    // it - 1, is cleared for it + 1
+    if (lists && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
     f32x4 acc[13];
 #pragma unroll
     for (int j = 0; j < 13; ++j) acc[j] = zero4();
@@ -1333,9 +1589,14 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[j][i] + bias);
       }
-    if (nb < B) c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);
+    if (lists && wave < 3) c1_flags(rm + (it % 3) * kC1RmDw, cl + it * 6 + wave * 2, wave, tid);
+    if (nb < B) {
+      c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);
+      if (lists) c1_mark(rm + ((it + 1) % 3) * kC1RmDw, pf);
+    }
     __syncthreads();
   }
+  if (lists && wave < 3) c1_lists_flush(cl, (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x, blockIdx.x, gridDim.x, L, wave, tid, B);
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of

@@ -41,6 +41,9 @@ static void replay(const P& p, const char* name) {
     int z = zg;
     if constexpr (HasChain<P>::value) z = p.sub_z(zg, si);
     const int row0 = tm * P::BM, col0 = tn * P::BN;
+    if constexpr (HasActive<P>::value) {
+      if (!p.active(z, row0)) continue;
+    }
     const int ns = p.nslabs(z);
     for (int s = 0; s < ns; ++s) {
       for (int idx = 0; idx < OA::F4; ++idx) {
@@ -67,7 +70,7 @@ static void replay(const P& p, const char* name) {
           for (int lane = 0; lane < 64; ++lane) {
             if constexpr (HasEpiPre<P>::value && MF == 16) {
               const int row = row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col = col0 + (wn * TN + j) * 16 + (lane & 15);
-              const f32x4 m = p.epi_pre(z, row, col);
+              const auto m = p.epi_pre(z, row, col);
               p.epi_post(z, row, col, zero4(), m);
             } else if (MF == 16) {
               p.epi(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15), zero4());
@@ -128,6 +131,22 @@ int main(int argc, char** argv) {
   // forward over n
   replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
   replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
+  {  // row-list forwards (background rows): the lists hold a permutation of the rows, 2 / 3 of them non-background
+    int* rl2 = buf<int>((size_t)n * 81);
+    int* rl3 = buf<int>((size_t)n * 49);
+    for (int i = 0; i < n * 81; ++i) rl2[i] = (int)(((long)i * 7919) % (n * 81));
+    for (int i = 0; i < n * 49; ++i) rl3[i] = (int)(((long)i * 7919) % (n * 49));
+    unsigned long long* cnt = buf<unsigned long long>(2);
+    for (int full = 0; full < 2; ++full) {
+      const unsigned long long k2 = full ? n * 81 : n * 81 * 2 / 3, k3 = full ? n * 49 : n * 49 * 2 / 3;
+      cnt[0] = k2 << 32 | (n * 81 - k2);
+      cnt[1] = k3 << 32 | (n * 49 - k3);
+      replay(PConv2FwdL<64, 64, 2, 2>{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, rl2, cnt}, "conv2_fwd L");
+      replay(PConv3FwdL<64, 64, 2, 2>{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, rl3, cnt + 1}, "conv3_fwd L");
+      replay(PConv2FwdL<64, 32, 2, 2>{grid(n * 81, 64, 64, 32, 1), a1, w1, b1, a2, rl2, cnt}, "conv2_fwd LS");
+      replay(PConv3FwdL<64, 32, 2, 2>{grid(n * 49, 64, 64, 32, 1), a2, w2, b2, a3, rl3, cnt + 1}, "conv3_fwd LS");
+    }
+  }
   replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
   replay(PFc1FwdB{grid(n, 64, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd B");
   replay(PConv2FwdS{grid(n * 81, 64, 64, 32, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd S");

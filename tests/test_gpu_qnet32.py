@@ -77,14 +77,18 @@ def test_init_weights_bit_identical():
         assert same(m.get(v), ref.get(v)), f"var {v}"
 
 
-@pytest.mark.parametrize("B,kind", [(1, "env"), (31, "rand"), (129, "sparse"), (256, "env"), (1024, "mixed")])
+@pytest.mark.parametrize("B,kind", [(1, "env"), (31, "rand"), (129, "sparse"), (256, "env"), (1024, "mixed"), (64, "zero"),
+                                    (3000, "env")])
 def test_forward_bit_exact(B, kind):
+    """Every layer bit for bit.  The conv2 / conv3 forward computes the non-background rows as a GEMM and writes the
+    constant rows of the background ones (qnet32_kernels.h C1Lists): env frames are mostly background, random frames
+    have none, zero frames are nothing else; B = 3,000 runs the chunk-size kernels."""
     qlx = _qlx()
     m = qlx.DeepQLearningModel(seed=2)
     ref = O.QNet(seed=2, f32=True)
     randomize(m, ref, B)
     x = {"env": lambda: env_states(B), "rand": lambda: rand_states(B, B), "sparse": lambda: rand_states(B, B, True),
-         "mixed": lambda: mixed_states(B, B)}[kind]()
+         "mixed": lambda: mixed_states(B, B), "zero": lambda: np.zeros((B, 84, 84, 4), np.uint8)}[kind]()
     q, a = m.q_values(x)
     qr, acts = ref.forward(x, acts=True)
     for layer in range(1, 5):
