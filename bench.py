@@ -360,10 +360,9 @@ class Run:
         for k in GEMM_SCOPES[self.precision]:
             if k in c and c[k]["total_us_per_step"] > 0:
                 t = rate(c[k]["work"], c[k]["total_us_per_step"], 1e6)
-                if k in ZERO_STEP_SCOPES:   # not an MFMA utilisation: the all-zero frame steps are not issued
+                if k in ZERO_STEP_SCOPES:   # not an MFMA utilisation: part of the dense work is not issued
                     layers[k] = {"tflops_dense_equivalent": round(t, 2), "mfma_frac": None, "avg_us": round(c[k]["avg_us"], 2),
-                                 "note": "dense FLOP / time; MFMA steps whose frame operands are all 0 are not issued "
-                                         "(exact, DESIGN.md 4.1)"}
+                                 "note": ZERO_STEP_SCOPES[k]}
                 else:
                     layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
         upd = self.updates / max(self.steps, 1) / max(self.ctl.world, 1)   # updates per vector step on one GPU
@@ -395,8 +394,13 @@ class Run:
         return self.env_steps / self.dt
 
 
-# conv1 launches skip the MFMA steps whose u8 frame operands are all 0 (k_conv1_fwd32 / k_conv1_wgrad32)
-ZERO_STEP_SCOPES = ("f32_conv1_fwd", "f32_conv1_fwd_big", "f32_conv1_wgrad")
+# launches that do not issue part of their layer's dense work (exact): their rates are dense FLOP / time
+_C1_NOTE = "dense FLOP / time; MFMA steps whose frame operands are all 0 are not issued (exact, DESIGN.md 4.1)"
+_BG_NOTE = ("dense FLOP / time; the background rows (receptive field all-zero frame pixels) are one constant row, computed "
+            "once and written, the GEMM runs the other rows (exact, DESIGN.md 4.1)")
+ZERO_STEP_SCOPES = {"f32_conv1_fwd": _C1_NOTE, "f32_conv1_fwd_big": _C1_NOTE, "f32_conv1_wgrad": _C1_NOTE,
+                    "f32_conv2_fwd": _BG_NOTE, "f32_conv2_fwd_big": _BG_NOTE, "f32_conv3_fwd": _BG_NOTE,
+                    "f32_conv3_fwd_big": _BG_NOTE}
 
 
 def pmc_traffic(precision, scope):

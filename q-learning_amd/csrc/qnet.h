@@ -44,6 +44,7 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   unsigned long long* frcnt = nullptr;
   float* fbgc = nullptr;
   int fparity = 0;
+  int frl_cap = 0;   // samples the row lists hold
   int fchunk = 0;
   void* fgrad = nullptr;
   int fgrad_batch = 0;

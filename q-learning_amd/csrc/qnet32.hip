@@ -539,6 +539,8 @@ static_assert((36864 + kNormSeg - 1) / kNormSeg <= 4 * kConvSegsPerGroup && (327
 static_assert((512 * 3 + kNormSeg - 1) / kNormSeg <= 64 && (32768 + kNormSeg - 1) / kNormSeg <= 64 &&
               (36864 + kNormSeg - 1) / kNormSeg <= 64 && (8192 + kNormSeg - 1) / kNormSeg <= 64, "<= 64 partials but W3");
 
+static int num_cus();
+
 void f32_workspace(qlx_model* m, int B) {
   if (B <= m->ws_batch) return;
   QLX_HIP(hipStreamSynchronize(m->stream));
@@ -558,7 +560,10 @@ void f32_workspace(qlx_model* m, int B) {
   for (int v = 0; v < kNumVars; ++v) nseg += segs_of(v);
   const size_t o_part = take((size_t)nseg * 4);
   const size_t o_loss = take(64);
-  const size_t o_rl2 = take((size_t)C * 81 * 4), o_rl3 = take((size_t)C * 49 * 4), o_rcnt = take(4 * 8), o_bgc = take(160 * 4);
+  // row lists: kListSlots regions of ceil(G / kListSlots) blocks x ceil(n / G) samples each (G = conv1 blocks), at most frl_cap samples
+  const int frl_cap = C + kListSlots * (C / std::max(1, std::min(C, 2 * num_cus())) + 1) + 2 * num_cus() + kListSlots;
+  const size_t o_rl2 = take((size_t)frl_cap * 81 * 4), o_rl3 = take((size_t)frl_cap * 49 * 4);
+  const size_t o_rcnt = take(2 * 2 * kListSlots * kCntStride * 8), o_bgc = take(160 * 4);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -573,7 +578,8 @@ void f32_workspace(qlx_model* m, int B) {
   w.frl2 = (int*)(base + o_rl2); w.frl3 = (int*)(base + o_rl3);
   w.frcnt = (unsigned long long*)(base + o_rcnt);
   w.fbgc = (float*)(base + o_bgc);
-  QLX_HIP(hipMemset(w.frcnt, 0, 4 * 8));
+  QLX_HIP(hipMemset(w.frcnt, 0, 2 * 2 * kListSlots * kCntStride * 8));
+  w.frl_cap = frl_cap;
   w.fparity = 0;
   w.fchunk = C;
   m->ws_batch = B;
@@ -708,15 +714,19 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     const bool big = n > 2048;
     // background rows: conv1 lists them, conv2 / conv3 run the rest (the list counters alternate between forwards)
     const bool lists = bg_rows();
-    unsigned long long* cnt = w.frcnt + 2 * w.fparity;
-    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cnt, w.frcnt + 2 * (w.fparity ^ 1)};
+    unsigned long long* cnt = w.frcnt + 2 * kListSlots * kCntStride * w.fparity;
+    static const int bg_mode = std::getenv("QLX_F32_BG_MODE") ? atoi(std::getenv("QLX_F32_BG_MODE")) : 0;
+    const int G = std::min(n, 2 * num_cus());                          // conv1 blocks
+    const int per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);   // samples of a list region, at most
+    const int cap2 = per_slot * 81, cap3 = per_slot * 49;
+    QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
+    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1), bg_mode};
     if (lists) w.fparity ^= 1;
     {
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
       hipEvent_t ea = nullptr, eb = nullptr;
       if (m->prof) m->prof->ext(sc, 2.0 * n * 400 * 32 * 256, &ea, &eb);
       auto kern = big ? k_conv1_fwd32<1> : k_conv1_fwd32<0>;
-      const int G = std::min(n, 2 * num_cus());
       constexpr int kMaxIt = 64;   // samples per block (flags kept in LDS until the block's lists are written)
       QLX_CHECK((n + G - 1) / G <= kMaxIt, QLX_E_STATE, "conv1 forward: too many samples per block");
       const size_t lds = 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
@@ -727,21 +737,30 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       debug_sync(s, sc);
     }
     if (lists) {
-      const int nw = std::min(256, std::max(16, n / 16));   // background-row blocks
-      const BgRows<4, 32> s2{nw, w.frl2, cnt, n * 81, p + voff(1), nullptr, p + voff(2), p + voff(3), w.fa2, w.fbgc + 32};
-      const BgRows<3, 64> s3{nw, w.frl3, cnt + 1, n * 49, nullptr, w.fbgc + 32, p + voff(4), p + voff(5), w.fa3, nullptr};
+      static const int tile = std::getenv("QLX_F32_BG_TILE") ? atoi(std::getenv("QLX_F32_BG_TILE")) : 0;
+      static const int nw_div = std::getenv("QLX_F32_BG_NW") ? atoi(std::getenv("QLX_F32_BG_NW")) : 8;
+      const int nw = bg_mode == 3 ? 0 : std::min(512, std::max(16, n / nw_div));   // background-row blocks
+      const BgRows<4, 32> s2{nw, w.frl2, cnt, cap2, p + voff(1), nullptr, p + voff(2), p + voff(3), w.fa2, w.fbgc + 32};
+      const BgRows<3, 64> s3{nw, w.frl3, cnt + kCntStride, cap3, nullptr, w.fbgc + 32, p + voff(4), p + voff(5), w.fa3, nullptr};
+      auto lgrid = [&](int cap, int BM, int BN) { return Grid{bg_mode == 4 ? 0 : kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
+      auto run = [&](auto t2, auto t3, const char* sc2, const char* sc3) {
+        using P2 = decltype(t2);
+        using P3 = decltype(t3);
+        launch_list(m, P2{lgrid(cap2, P2::BM, P2::BN), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt}, s2, sc2,
+                    2.0 * n * 81 * 64 * 512, s);
+        launch_list(m, P3{lgrid(cap3, P3::BM, P3::BN), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride}, s3, sc3,
+                    2.0 * n * 49 * 64 * 576, s);
+      };
       if (big) {
-        launch_list(m, PConv2FwdL<64, 64, 2, 2>{grid(n * 81, 64, 64, 64, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cnt}, s2,
-                    "f32_conv2_fwd_big", 2.0 * n * 81 * 64 * 512, s);
-        launch_list(m, PConv3FwdL<64, 64, 2, 2>{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cnt + 1},
-                    s3, "f32_conv3_fwd_big", 2.0 * n * 49 * 64 * 576, s);
+        run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd_big", "f32_conv3_fwd_big");
         launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
                2.0 * n * 3136 * 512, s);
       } else {
-        launch_list(m, PConv2FwdL<64, 32, 2, 2>{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cnt}, s2,
-                    "f32_conv2_fwd", 2.0 * n * 81 * 64 * 512, s);
-        launch_list(m, PConv3FwdL<64, 32, 2, 2>{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cnt + 1},
-                    s3, "f32_conv3_fwd", 2.0 * n * 49 * 64 * 576, s);
+        if (tile == 1) run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        else if (tile == 2) run(PConv2FwdL<32, 64, 2, 2>{}, PConv3FwdL<32, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        else if (tile == 3) run(PConv2FwdL<16, 64, 1, 4>{}, PConv3FwdL<16, 64, 1, 4>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        else if (tile == 4) run(PConv2FwdL<32, 32, 2, 2>{}, PConv3FwdL<32, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        else run(PConv2FwdL<64, 32, 2, 2>{}, PConv3FwdL<64, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
         launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);
       }

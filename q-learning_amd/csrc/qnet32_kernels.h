@@ -23,6 +23,9 @@ namespace q32 {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;   // reduction depth staged per LDS slab
+// background-row lists (C1Lists): regions per list (one per XCD) and the counter stride (128 bytes)
+constexpr int kListSlots = 8;
+constexpr int kCntStride = 16;   // [region][layer] at (region * 2 + layer) * kCntStride
 
 // Operand tile in LDS for MFMA shape MF (16: v_mfma_f32_16x16x4_f32, 32: v_mfma_f32_32x32x2_f32).  RMAJ: t[row][k]
 // (pitch BK + 4); KMAJ: t[k][row] (pitch = rows padded to MF mod 64, so the MF rows x (64 / MF) k of a fragment read
@@ -682,9 +685,10 @@ struct RowShift : Base {
 using PConv2FwdR = RowShift<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 1, 4>>;
 using PConv3FwdR = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 1, 4>>;
 
-// conv2 / conv3 forward over the non-background rows (see C1Lists): GEMM row r is output row list[r] (chunk-local
-// b * OH * OW + p) for r < the list's count (device memory); tiles past the count return at once.  Tiles are taken in
-// hardware block order, so the live ones (the first) spread over all XCDs.  Every output is the chain PConvFwd computes.
+// conv2 / conv3 forward over the non-background rows (see C1Lists): row tile tm is tile tm / kListSlots of region tm % kListSlots,
+// whose row lr is output row list[region][lr] (chunk-local b * OH * OW + p) for lr < the region's count (device memory);
+// tiles past it return at once.  Tiles are taken in hardware block order with the regions fastest, so the live ones (the
+// first) spread over all XCDs.  Every output is the chain PConvFwd computes.
 template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
 struct PConvFwdL {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
@@ -693,29 +697,43 @@ struct PConvFwdL {
   static constexpr int R = OH * OW;
   using OA = Opnd<BM, false, 16>;
   static constexpr int T = WM * WN * 64, NA = (OA::F4 + T - 1) / T;
-  Grid g;
+  Grid g;            // tiles_m = kListSlots * tiles per region
   const float* in;
   const float* w;    // [KS][KS][C][OC]
   const float* bias;
   float* out;        // [rows][OC]
-  const int* list;
-  const unsigned long long* cnt;   // non-background rows << 32 | background rows
+  const int* list;   // [kListSlots][cap]
+  int cap;
+  const unsigned long long* cnt;   // this layer's counter of region 0 (region x at x * 2 * kCntStride)
   struct ACtx { int off[NA]; };
   struct Pre { float b; int o[4]; };
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return KS * KS * C / BK; }
-  __device__ int rows() const { return (int)(*cnt >> 32); }
-  __device__ bool active(int, int row0) const { return row0 < rows(); }
+  // region of a GEMM row and its index there
+  __device__ static void where(int row, int& x, int& lr) {
+    const int tm = row / BM;
+    x = tm % kListSlots;
+    lr = (tm / kListSlots) * BM + row % BM;
+  }
+  __device__ int count(int x) const { return (int)(cnt[x * 2 * kCntStride] >> 32); }
+  __device__ bool active(int, int row0) const {
+    int x, lr;
+    where(row0, x, lr);
+    return lr < count(x);
+  }
+  __device__ int entry(int row) const {
+    int x, lr;
+    where(row, x, lr);
+    return lr < count(x) ? list[x * cap + lr] : -1;
+  }
   // input offsets of the thread's NA operand rows (-1: past the count)
   __device__ ACtx a_ctx(int, int row0, int tid) const {
     ACtx c;
-    const int n = rows();
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int r, k;
       OA::coord(tid + i * T, r, k);
-      const int row = row0 + r;
-      const int e = row < n ? list[row] : -1;
+      const int e = entry(row0 + r);
       const int b = e / R, p = e - b * R, oh = p / OW, ow = p - oh * OW;
       c.off[i] = e >= 0 ? ((b * H + oh * S) * W + ow * S) * C : -1;
     }
@@ -728,11 +746,13 @@ struct PConvFwdL {
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w + (size_t)(s * BK + k) * OC + col); }
   __device__ Pre epi_pre(int, int row, int col) const {
-    const int n = rows();
     Pre q;
     q.b = bias[col];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) q.o[r] = row + r < n ? list[row + r] * OC : -1;
+    for (int r = 0; r < 4; ++r) {
+      const int e = entry(row + r);
+      q.o[r] = e >= 0 ? e * OC : -1;
+    }
     return q;
   }
   __device__ void epi_post(int, int, int col, f32x4 v, const Pre& q) const {
@@ -752,13 +772,16 @@ using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN>;
 // writes c to its share of the background rows (the list's back end).  Block 0 also stores c (the next layer's x).
 template <int KS, int C>
 struct BgRows {
-  static constexpr int K = KS * KS * C, KC = 32, NCH = K / KC;   // W staged in LDS KC k-rows at a time (double-buffered)
-  static_assert(K % KC == 0 && C % KC == 0, "chunks of KC k-rows within one tap");
-  static constexpr size_t LDS = (128 + 2 * KC * 64) * sizeof(float);   // below the GEMM tiles' LDS
+  // W staged through LDS in groups of GR k-rows: the next group's loads are in flight in registers while wave 0 chains
+  // the current one from LDS (one memory latency per group, not per slab)
+  static constexpr int K = KS * KS * C, GR = 128, NG = (K + GR - 1) / GR, NF = GR * 64 / 4 / 256;
+  static_assert(C % 32 == 0, "channel halves");
+  static constexpr size_t LDS = (128 + GR * 64) * sizeof(float);
+  static constexpr int U = 8;   // background rows per thread group per round (their list entries loaded together)
   int nblk;
-  const int* list;
-  const unsigned long long* cnt;
-  int total;               // list length (n * rows per sample)
+  const int* list;         // [kListSlots][cap]
+  const unsigned long long* cnt;   // this layer's counter of region 0
+  int cap;                 // rows per region
   const float* x_bias;     // conv2: b0 (x = relu(0 + b0)); null: x = x_row
   const float* x_row;      // conv3: c2
   const float* w;          // [KS][KS][C][64]
@@ -770,30 +793,28 @@ struct BgRows {
     const int tid = threadIdx.x;
     float* xs = lds;         // x [C]
     float* cs = lds + 64;    // c [64]
-    float* wb = lds + 128;   // [2][KC k][64 oc]
+    float* wg = lds + 128;   // [GR k][64 oc]
     if (tid < C) xs[tid] = x_bias ? relu(0.0f + x_bias[tid]) : x_row[tid];
-    f32x4 r[KC / 16];
-    auto ldw = [&](int q) {
+    f32x4 r[NF];
+    auto ldg = [&](int g) {
 #pragma unroll
-      for (int i = 0; i < KC / 16; ++i) r[i] = ld4(w + (size_t)q * KC * 64 + 4 * (tid + 256 * i));
-    };
-    auto stw = [&](int q) {
-#pragma unroll
-      for (int i = 0; i < KC / 16; ++i) *reinterpret_cast<f32x4*>(wb + (q & 1) * KC * 64 + 4 * (tid + 256 * i)) = r[i];
-    };
-    ldw(0);
-    stw(0);
-    __syncthreads();
-    float acc = 0.0f;
-    for (int q = 0; q < NCH; ++q) {
-      if (q + 1 < NCH) ldw(q + 1);
-      if (tid < 64) {   // wave 0: the chain, k = KC q + kk in order (channel (KC q + kk) % C)
-        const float* wq = wb + (q & 1) * KC * 64;
-        const float* xq = xs + (q * KC) % C;
-#pragma unroll
-        for (int kk = 0; kk < KC; ++kk) acc = __builtin_fmaf(xq[kk], wq[kk * 64 + tid], acc);
+      for (int i = 0; i < NF; ++i) {
+        const int e = 4 * (tid + 256 * i), row = g * GR + e / 64;   // float index in the group, its k-row
+        r[i] = ld4m(w + (size_t)g * GR * 64 + e, row < K);
       }
-      if (q + 1 < NCH) stw(q + 1);
+    };
+    ldg(0);
+    float acc = 0.0f;
+    for (int g = 0; g < NG; ++g) {
+#pragma unroll
+      for (int i = 0; i < NF; ++i) *reinterpret_cast<f32x4*>(wg + 4 * (tid + 256 * i)) = r[i];
+      __syncthreads();
+      if (g + 1 < NG) ldg(g + 1);
+      if (tid < 64) {   // wave 0: the chain over k = GR g + kk in order (channel k % C)
+        const int kn = K - g * GR < GR ? K - g * GR : GR;
+#pragma unroll 32
+        for (int kk = 0; kk < kn; ++kk) acc = __builtin_fmaf(xs[(g * GR + kk) % C], wg[kk * 64 + tid], acc);
+      }
       __syncthreads();
     }
     if (tid < 64) {
@@ -802,10 +823,20 @@ struct BgRows {
       if (blk == 0 && c_out) c_out[tid] = c;
     }
     __syncthreads();
-    const int nbg = (int)(uint32_t)*cnt, q = tid & 15;
+    const int q = tid & 15;
     const f32x4 v = ld4(cs + 4 * q);
-    for (int i = blk * 16 + (tid >> 4); i < nbg; i += nblk * 16)
-      *reinterpret_cast<f32x4*>(out + (size_t)list[total - 1 - i] * 64 + 4 * q) = v;
+    for (int x = 0; x < kListSlots; ++x) {
+      const int nbg = (int)(uint32_t)cnt[x * 2 * kCntStride];
+      const int* back = list + (size_t)(x + 1) * cap - 1;
+      for (int i0 = blk * 16 * U + (tid >> 4); i0 < nbg; i0 += nblk * 16 * U) {
+        int e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) e[u] = i0 + 16 * u < nbg ? back[-(i0 + 16 * u)] : -1;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (e[u] >= 0) *reinterpret_cast<f32x4*>(out + (size_t)e[u] * 64 + 4 * q) = v;
+      }
+    }
   }
 };
 
@@ -1415,15 +1446,19 @@ __device__ __forceinline__ float ubyte(uint32_t w, int i) { return (float)((w >>
 // chains on the same operands, whatever row a GEMM tile holds them in.
 // The forward's conv1 kernel classifies each sample while its frames are staged: a 4 x 4 pixel block (one s2d chunk per
 // frame) marks bit by of the row mask rm[bx] (21 x 21 blocks) when any of its bytes is non-zero, and a conv2 (conv3) row is
-// background when the 5 x 5 (9 x 9) blocks from (2 i, 2 j) are unmarked.  Row lists: rl[n * R] per layer (R = 81 / 49
-// rows per sample), entries b * R + p; the non-background rows from the front, the background rows from the back, their
-// counts in cnt (non-background << 32 | background), claimed per wave with one atomic (so the order of a list's entries
-// varies between runs; the values do not).
+// background when the 5 x 5 (9 x 9) blocks from (2 i, 2 j) are unmarked.  Row lists (entries b * R + p, R = 81 / 49 rows
+// per sample) in kListSlots regions, one per XCD (conv1 block g writes region g % kListSlots): a region's non-background rows from
+// its front, its background rows from its back, their counts in the region's counter (non-background << 32 |
+// background), claimed once per wave after the block's last sample.  One counter per XCD instead of one per list: the
+// claims of all blocks arrive together at the end of the launch, and on one address they serialise (measured: +11.5 us
+// on a 46 us conv1 launch at B = 1024).  The order of a region's entries varies between runs; the values do not.
 struct C1Lists {
   int* rl2;                       // null: no lists (every row computed)
   int* rl3;
-  unsigned long long* cnt;        // this forward's counters: [0] conv2, [1] conv3
+  int cap2, cap3;                 // rows per region
+  unsigned long long* cnt;        // this forward's counters
   unsigned long long* cnt_next;   // the next forward's (double-buffered by forward parity), zeroed here
+  int mode;                       // (experiment) 1: no flush, 2: flush without stores
 };
 constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
 
@@ -1485,15 +1520,19 @@ __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int
     tot += ((unsigned long long)__builtin_popcountll(cl[(it * 3 + wave) * 2]) << 32) |
            (unsigned long long)__builtin_popcountll(cl[(it * 3 + wave) * 2 + 1]);
   unsigned long long old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(L.cnt + (wave < 2 ? 0 : 1), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int slot = blockIdx.x % kListSlots, cap = wave < 2 ? L.cap2 : L.cap3;
+  rl += slot * cap;
+  if (lane == 0)
+    old = __hip_atomic_fetch_add(L.cnt + (slot * 2 + (wave < 2 ? 0 : 1)) * kCntStride, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __shfl(old, 0);
   int on = (int)(old >> 32), og = (int)(uint32_t)old;
   const unsigned long long below = (1ull << lane) - 1ull;
+  if (L.mode == 2) { if (old == 12345) rl[0] = 0; return; }
   for (int it = 0; it < nit; ++it) {
     const unsigned long long bn = cl[(it * 3 + wave) * 2], bb = cl[(it * 3 + wave) * 2 + 1];
     const int e = (b0 + it * G) * R + p;
     if ((bn >> lane) & 1ull) rl[on + __builtin_popcountll(bn & below)] = e;
-    else if ((bb >> lane) & 1ull) rl[B * R - 1 - (og + __builtin_popcountll(bb & below))] = e;
+    else if ((bb >> lane) & 1ull) rl[cap - 1 - (og + __builtin_popcountll(bb & below))] = e;
     on += __builtin_popcountll(bn);
     og += __builtin_popcountll(bb);
   }
@@ -1519,7 +1558,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (lists) {
-    if (blockIdx.x == 0 && tid < 2) L.cnt_next[tid] = 0ull;
+    if (blockIdx.x == 0 && tid < 2 * kListSlots) L.cnt_next[tid * kCntStride] = 0ull;
     if (tid < 3 * kC1RmDw) rm[tid] = 0u;
     __syncthreads();
   }
@@ -1596,7 +1635,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
     }
     __syncthreads();
   }
-  if (lists && wave < 3) c1_lists_flush(cl, (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x, blockIdx.x, gridDim.x, L, wave, tid, B);
+  if (lists && wave < 3 && L.mode != 1) c1_lists_flush(cl, (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x, blockIdx.x, gridDim.x, L, wave, tid, B);
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of

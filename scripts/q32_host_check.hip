@@ -131,20 +131,25 @@ int main(int argc, char** argv) {
   // forward over n
   replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
   replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
-  {  // row-list forwards (background rows): the lists hold a permutation of the rows, 2 / 3 of them non-background
-    int* rl2 = buf<int>((size_t)n * 81);
-    int* rl3 = buf<int>((size_t)n * 49);
-    for (int i = 0; i < n * 81; ++i) rl2[i] = (int)(((long)i * 7919) % (n * 81));
-    for (int i = 0; i < n * 49; ++i) rl3[i] = (int)(((long)i * 7919) % (n * 49));
-    unsigned long long* cnt = buf<unsigned long long>(2);
+  {  // row-list forwards (background rows): per region a permutation of the rows, 2 / 3 of them non-background (or all)
+    const int G = std::min(n, 512), per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);
+    const int cap2 = per_slot * 81, cap3 = per_slot * 49;
+    int* rl2 = buf<int>((size_t)kListSlots * cap2);
+    int* rl3 = buf<int>((size_t)kListSlots * cap3);
+    for (int i = 0; i < kListSlots * cap2; ++i) rl2[i] = (int)(((long)i * 7919) % (n * 81));
+    for (int i = 0; i < kListSlots * cap3; ++i) rl3[i] = (int)(((long)i * 7919) % (n * 49));
+    unsigned long long* cnt = buf<unsigned long long>(2 * kListSlots * kCntStride);
     for (int full = 0; full < 2; ++full) {
-      const unsigned long long k2 = full ? n * 81 : n * 81 * 2 / 3, k3 = full ? n * 49 : n * 49 * 2 / 3;
-      cnt[0] = k2 << 32 | (n * 81 - k2);
-      cnt[1] = k3 << 32 | (n * 49 - k3);
-      replay(PConv2FwdL<64, 64, 2, 2>{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, rl2, cnt}, "conv2_fwd L");
-      replay(PConv3FwdL<64, 64, 2, 2>{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, rl3, cnt + 1}, "conv3_fwd L");
-      replay(PConv2FwdL<64, 32, 2, 2>{grid(n * 81, 64, 64, 32, 1), a1, w1, b1, a2, rl2, cnt}, "conv2_fwd LS");
-      replay(PConv3FwdL<64, 32, 2, 2>{grid(n * 49, 64, 64, 32, 1), a2, w2, b2, a3, rl3, cnt + 1}, "conv3_fwd LS");
+      for (int x = 0; x < kListSlots; ++x) {
+        const unsigned long long k2 = full ? cap2 : cap2 * 2 / 3, k3 = full ? cap3 : cap3 * 2 / 3;
+        cnt[(x * 2) * kCntStride] = k2 << 32 | (cap2 - k2);
+        cnt[(x * 2 + 1) * kCntStride] = k3 << 32 | (cap3 - k3);
+      }
+      auto lg = [&](int cap, int BM, int BN) { return Grid{kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
+      replay(PConv2FwdL<64, 64, 2, 2>{lg(cap2, 64, 64), a1, w1, b1, a2, rl2, cap2, cnt}, "conv2_fwd L");
+      replay(PConv3FwdL<64, 64, 2, 2>{lg(cap3, 64, 64), a2, w2, b2, a3, rl3, cap3, cnt + kCntStride}, "conv3_fwd L");
+      replay(PConv2FwdL<64, 32, 2, 2>{lg(cap2, 64, 32), a1, w1, b1, a2, rl2, cap2, cnt}, "conv2_fwd LS");
+      replay(PConv3FwdL<64, 32, 2, 2>{lg(cap3, 64, 32), a2, w2, b2, a3, rl3, cap3, cnt + kCntStride}, "conv3_fwd LS");
     }
   }
   replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
