@@ -740,8 +740,11 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       static const int tile = std::getenv("QLX_F32_BG_TILE") ? atoi(std::getenv("QLX_F32_BG_TILE")) : 0;
       static const int nw_div = std::getenv("QLX_F32_BG_NW") ? atoi(std::getenv("QLX_F32_BG_NW")) : 8;
       const int nw = bg_mode == 3 ? 0 : std::min(512, std::max(16, n / nw_div));   // background-row blocks
-      const BgRows<4, 32> s2{nw, w.frl2, cnt, cap2, p + voff(1), nullptr, p + voff(2), p + voff(3), w.fa2, w.fbgc + 32};
-      const BgRows<3, 64> s3{nw, w.frl3, cnt + kCntStride, cap3, nullptr, w.fbgc + 32, p + voff(4), p + voff(5), w.fa3, nullptr};
+      const int nw3 = bg_mode == 3 ? 0 : std::min(256, std::max(8, n / 32));
+      // conv2's side blocks compute c2 (and block 0 c3 into fbgc); conv3's read c3
+      const BgRows<4, 32, 3, 64> s2{nw, w.frl2, cnt, cap2, p + voff(1), p + voff(2), p + voff(3), nullptr, p + voff(4), p + voff(5),
+                                    w.fbgc, w.fa2};
+      const BgRows<0, 64> s3{nw3, w.frl3, cnt + kCntStride, cap3, nullptr, nullptr, nullptr, w.fbgc, nullptr, nullptr, nullptr, w.fa3};
       auto lgrid = [&](int cap, int BM, int BN) { return Grid{bg_mode == 4 ? 0 : kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
       auto run = [&](auto t2, auto t3, const char* sc2, const char* sc3) {
         using P2 = decltype(t2);

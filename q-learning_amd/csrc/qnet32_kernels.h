@@ -766,61 +766,74 @@ using PConv2FwdL = PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, BM, BN, WM, WN>;
 template <int BM, int BN, int WM, int WN>
 using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN>;
 
-// Leading blocks of a list launch: the background rows.  Wave 0 of every block computes the constant output row
-// c[oc] = relu(chain over k = (kh, kw, ch) of x[ch] W[kh][kw][ch][oc] + bias[oc]) - the GEMM's chain on the constant
-// input row x: conv2: x = relu(0 + b0) (every conv1 output over background pixels), conv3: x = c2 - then the block
-// writes c to its share of the background rows (the list's back end).  Block 0 also stores c (the next layer's x).
+// The constant row's chain for output channel tid (tid < 64; every thread of the block calls it: it has barriers):
+// acc = chain over k = (kh, kw, ch) of x[ch] W[kh][kw][ch][tid] - the GEMM's chain on the constant input row x (LDS).  W is
+// staged through LDS (wg, GR k-rows) a group at a time, the next group's loads in flight in registers while wave 0 chains
+// the current one (one memory latency per group).  Measured alternatives: the chain on v_mfma_f32_16x16x4_f32 with W
+// streamed to registers 16 k-steps ahead (each batch waited out its loads: 3x slower), one LDS round of 16 weights per
+// 16 fmas (unroll 1: 1.6x slower), every round unrolled (238 VGPRs for the whole launch: the GEMM tiles lost occupancy).
 template <int KS, int C>
+__device__ __forceinline__ float const_chain(const float* xs, const float* w, float* wg, int tid) {
+  constexpr int K = KS * KS * C, GR = 128, NG = (K + GR - 1) / GR, NF = GR * 64 / 4 / 256;
+  static_assert(GR % C == 0, "groups of whole channel runs");
+  f32x4 r[NF];
+  auto ldg = [&](int g) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = 4 * (tid + 256 * i);   // float index in the group; its k-row e / 64
+      r[i] = ld4m(w + (size_t)g * GR * 64 + e, g * GR + e / 64 < K);
+    }
+  };
+  ldg(0);
+  float acc = 0.0f;
+  for (int g = 0; g < NG; ++g) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) *reinterpret_cast<f32x4*>(wg + 4 * (tid + 256 * i)) = r[i];
+    __syncthreads();
+    if (g + 1 < NG) ldg(g + 1);
+    if (tid < 64) {   // wave 0: k = GR g + kk in order (channel kk % C)
+      const int kn = K - g * GR < GR ? K - g * GR : GR;
+#pragma unroll 32
+      for (int kk = 0; kk < kn; ++kk) acc = __builtin_fmaf(xs[kk % C], wg[kk * 64 + tid], acc);
+    }
+    __syncthreads();
+  }
+  return acc;
+}
+
+// Leading blocks of a list launch (256 threads): the background rows.  The constant output row c[oc] = relu(const_chain +
+// bias[oc]):
+// conv2 (KS = 4, C = 32): every block computes it from x = relu(0 + b0) (every conv1 output over background pixels), and
+// block 0 then also computes the next layer's constant row c3 from c (KS2 = 3, C2 = 64) into c_next; conv3 (KS = 0): c is
+// read from there.  Each block writes c to its share of the background rows (the back ends of the list regions).
+template <int KS, int C, int KS2 = 0, int C2 = 0>
 struct BgRows {
-  // W staged through LDS in groups of GR k-rows: the next group's loads are in flight in registers while wave 0 chains
-  // the current one from LDS (one memory latency per group, not per slab)
-  static constexpr int K = KS * KS * C, GR = 128, NG = (K + GR - 1) / GR, NF = GR * 64 / 4 / 256;
-  static_assert(C % 32 == 0, "channel halves");
-  static constexpr size_t LDS = (128 + GR * 64) * sizeof(float);
-  static constexpr int U = 8;   // background rows per thread group per round (their list entries loaded together)
+  static constexpr size_t LDS = (128 + 128 * 64) * sizeof(float);
+  static constexpr int U = 8;   // background rows per 16-lane group per round (their list entries loaded together)
   int nblk;
   const int* list;         // [kListSlots][cap]
   const unsigned long long* cnt;   // this layer's counter of region 0
   int cap;                 // rows per region
-  const float* x_bias;     // conv2: b0 (x = relu(0 + b0)); null: x = x_row
-  const float* x_row;      // conv3: c2
+  const float* x_bias;     // conv2: b0 (x = relu(0 + b0))
   const float* w;          // [KS][KS][C][64]
   const float* bias;
+  const float* c_in;       // KS = 0: the constant row
+  const float* w2;         // KS2 > 0: the next layer's weights [KS2][KS2][C2][64] and bias
+  const float* bias2;
+  float* c_next;           // KS2 > 0: block 0 stores the next layer's constant row here
   float* out;              // [rows][64]
-  float* c_out;            // block 0 stores c here (null: not needed)
   __host__ __device__ int blocks() const { return nblk; }
   __device__ void run(int blk, float* lds) const {
     const int tid = threadIdx.x;
     float* xs = lds;         // x [C]
     float* cs = lds + 64;    // c [64]
-    float* wg = lds + 128;   // [GR k][64 oc]
-    if (tid < C) xs[tid] = x_bias ? relu(0.0f + x_bias[tid]) : x_row[tid];
-    f32x4 r[NF];
-    auto ldg = [&](int g) {
-#pragma unroll
-      for (int i = 0; i < NF; ++i) {
-        const int e = 4 * (tid + 256 * i), row = g * GR + e / 64;   // float index in the group, its k-row
-        r[i] = ld4m(w + (size_t)g * GR * 64 + e, row < K);
-      }
-    };
-    ldg(0);
-    float acc = 0.0f;
-    for (int g = 0; g < NG; ++g) {
-#pragma unroll
-      for (int i = 0; i < NF; ++i) *reinterpret_cast<f32x4*>(wg + 4 * (tid + 256 * i)) = r[i];
-      __syncthreads();
-      if (g + 1 < NG) ldg(g + 1);
-      if (tid < 64) {   // wave 0: the chain over k = GR g + kk in order (channel k % C)
-        const int kn = K - g * GR < GR ? K - g * GR : GR;
-#pragma unroll 32
-        for (int kk = 0; kk < kn; ++kk) acc = __builtin_fmaf(xs[(g * GR + kk) % C], wg[kk * 64 + tid], acc);
-      }
-      __syncthreads();
-    }
-    if (tid < 64) {
-      const float c = relu(acc + bias[tid]);
-      cs[tid] = c;
-      if (blk == 0 && c_out) c_out[tid] = c;
+    float* wg = lds + 128;   // W group [128][64]
+    if constexpr (KS > 0) {
+      if (tid < C) xs[tid] = relu(0.0f + x_bias[tid]);
+      const float acc = const_chain<KS, C>(xs, w, wg, tid);   // (its first barrier orders xs)
+      if (tid < 64) cs[tid] = relu(acc + bias[tid]);
+    } else {
+      if (tid < 64) cs[tid] = c_in[tid];
     }
     __syncthreads();
     const int q = tid & 15;
@@ -835,6 +848,12 @@ struct BgRows {
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (e[u] >= 0) *reinterpret_cast<f32x4*>(out + (size_t)e[u] * 64 + 4 * q) = v;
+      }
+    }
+    if constexpr (KS2 > 0) {
+      if (blk == 0) {
+        const float acc = const_chain<KS2, C2>(cs, w2, wg, tid);
+        if (tid < 64) c_next[tid] = relu(acc + bias2[tid]);
       }
     }
   }
