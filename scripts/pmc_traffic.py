@@ -18,10 +18,11 @@ SCOPES = {
     "fp32": {
         "f32_conv1_fwd": "k_conv1_fwd32<0>",
         "f32_conv1_fwd_big": "k_conv1_fwd32<1>",
-        "f32_conv2_fwd": "k_gemm32_pair<qlx::q32::PConvFwd<20, 20,",   # the balanced grid (whole + 16-row tiles)
-        "f32_conv2_fwd_big": "k_gemm32<qlx::q32::PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 64, 64, 2, 2,",
-        "f32_conv3_fwd": "k_gemm32_pair<qlx::q32::PConvFwd<9, 9,",
-        "f32_conv3_fwd_big": "k_gemm32<qlx::q32::PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 64, 64, 2, 2,",
+        # row-list forwards (non-background rows + the background rows' side blocks)
+        "f32_conv2_fwd": "k_gemm32_side<qlx::q32::PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, 64, 32,",
+        "f32_conv2_fwd_big": "k_gemm32_side<qlx::q32::PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, 64, 64,",
+        "f32_conv3_fwd": "k_gemm32_side<qlx::q32::PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, 64, 32,",
+        "f32_conv3_fwd_big": "k_gemm32_side<qlx::q32::PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, 64, 64,",
         "f32_fc1_fwd": "k_gemm32<qlx::q32::PFc1FwdT<32, 32, 2, 2,",
         "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<64, 64, 2, 2,",
         "f32_fc1_bwd": "k_gemm32_pair<qlx::q32::PFc1WgradT",
@@ -31,7 +32,7 @@ SCOPES = {
         "f32_norms": "k_norm32",
         "f32_head": "k_head32<3>",
         "f32_wgrad_reduce": "k_wreduce32",
-        "f32_adam": "k_adam32",
+        "f32_adam": "k_update32",   # update schedule 2 (default): every variable's clip_by_norm + Adam in one launch
     },
     "bf16": {
         "trunk_fwd": "k_trunk_fwd<true>",
