@@ -720,7 +720,8 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     const int per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);   // samples of a list region, at most
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
-    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1), bg_mode};
+    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1), bg_mode,
+                    w.fbgc};
     if (lists) w.fparity ^= 1;
     {
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
@@ -737,22 +738,26 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       debug_sync(s, sc);
     }
     if (lists) {
+      // conv2: the non-background rows, the constant rows c2 and c3 in its first block (ConstRows); conv3: the non-background
+      // rows (background conv2 taps read from c2), side blocks writing c2 / c3 to the background rows of a2 / a3
       static const int tile = std::getenv("QLX_F32_BG_TILE") ? atoi(std::getenv("QLX_F32_BG_TILE")) : 0;
-      static const int nw_div = std::getenv("QLX_F32_BG_NW") ? atoi(std::getenv("QLX_F32_BG_NW")) : 8;
-      const int nw = bg_mode == 3 ? 0 : std::min(512, std::max(16, n / nw_div));   // background-row blocks
-      const int nw3 = bg_mode == 3 ? 0 : std::min(256, std::max(8, n / 32));
-      // conv2's side blocks compute c2 (and block 0 c3 into fbgc); conv3's read c3
-      const BgRows<4, 32, 3, 64> s2{nw, w.frl2, cnt, cap2, p + voff(1), p + voff(2), p + voff(3), nullptr, p + voff(4), p + voff(5),
-                                    w.fbgc, w.fa2};
-      const BgRows<0, 64> s3{nw3, w.frl3, cnt + kCntStride, cap3, nullptr, nullptr, nullptr, w.fbgc, nullptr, nullptr, nullptr, w.fa3};
-      auto lgrid = [&](int cap, int BM, int BN) { return Grid{bg_mode == 4 ? 0 : kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
+      const int nw = bg_mode == 3 ? 0 : std::min(256, std::max(16, n / 16));   // background-row blocks per job
+      float* c2 = w.fbgc + 32;
+      float* c3 = w.fbgc + 96;
+      const BgRows2 s23{{nw, w.frl2, cnt, cap2, c2, w.fa2}, {nw, w.frl3, cnt + kCntStride, cap3, c3, w.fa3}};
+      using PC2 = PConv2FwdL<16, 64, 1, 4>;
+      using PC3 = PConv3FwdL<16, 64, 1, 4>;
+      const ConstRows<PC2, PC3> cr{PC2{Grid{1, 1, 1}, w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, c2},
+                                   PC3{Grid{1, 1, 1}, w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride, c2, c3}};
+      auto lgrid = [&](int cap, int BM, int BN) { return Grid{1 + (bg_mode == 4 ? 0 : kListSlots * ((cap + BM - 1) / BM)), 64 / BN, 1}; };
       auto run = [&](auto t2, auto t3, const char* sc2, const char* sc3) {
         using P2 = decltype(t2);
         using P3 = decltype(t3);
-        launch_list(m, P2{lgrid(cap2, P2::BM, P2::BN), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt}, s2, sc2,
-                    2.0 * n * 81 * 64 * 512, s);
-        launch_list(m, P3{lgrid(cap3, P3::BM, P3::BN), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride}, s3, sc3,
-                    2.0 * n * 49 * 64 * 576, s);
+        // (the list tiles start at row tile 1; row tile 0, the constant row, is ConstRows' work: its blocks return)
+        launch_list(m, P2{lgrid(cap2, P2::BM, P2::BN), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, nullptr}, cr,
+                    sc2, 2.0 * n * 81 * 64 * 512, s);
+        launch_list(m, P3{lgrid(cap3, P3::BM, P3::BN), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride, c2, nullptr},
+                    s23, sc3, 2.0 * n * 49 * 64 * 576, s);
       };
       if (big) {
         run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd_big", "f32_conv3_fwd_big");
@@ -760,9 +765,6 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
                2.0 * n * 3136 * 512, s);
       } else {
         if (tile == 1) run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
-        else if (tile == 2) run(PConv2FwdL<32, 64, 2, 2>{}, PConv3FwdL<32, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
-        else if (tile == 3) run(PConv2FwdL<16, 64, 1, 4>{}, PConv3FwdL<16, 64, 1, 4>{}, "f32_conv2_fwd", "f32_conv3_fwd");
-        else if (tile == 4) run(PConv2FwdL<32, 32, 2, 2>{}, PConv3FwdL<32, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
         else run(PConv2FwdL<64, 32, 2, 2>{}, PConv3FwdL<64, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
         launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);

@@ -685,11 +685,16 @@ struct RowShift : Base {
 using PConv2FwdR = RowShift<PConvFwd<20, 20, 32, 4, 2, 9, 9, 64, 16, 64, 1, 4>>;
 using PConv3FwdR = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 1, 4>>;
 
-// conv2 / conv3 forward over the non-background rows (see C1Lists): row tile tm is tile tm / kListSlots of region tm % kListSlots,
-// whose row lr is output row list[region][lr] (chunk-local b * OH * OW + p) for lr < the region's count (device memory);
-// tiles past it return at once.  Tiles are taken in hardware block order with the regions fastest, so the live ones (the
-// first) spread over all XCDs.  Every output is the chain PConvFwd computes.
-template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2>
+// conv2 / conv3 forward over the non-background rows (see C1Lists).  Row tile 0 holds one row, the constant row: its input
+// is the constant vector cx at every tap (conv2: relu(0 + b0); conv3: c2) and its output goes to cbuf (c2; c3) - the
+// background rows' value, computed by the GEMM's own chain (ConstRows runs these as the first block of the conv2 launch).
+// Row tile 1 + t * kListSlots + x is tile t of list region x, whose row lr is output row list[x][lr] (chunk-local
+// b * OH * OW + p, bits 0..19) for lr < the region's count (device memory); tiles past it return at once.  Tiles run in
+// hardware block order (the live ones first, spread over the XCDs).  SEL (conv3): the taps whose input position is
+// background in the layer below (list entry bits 20..28, written by conv1) read cx = that layer's constant row instead of
+// `in` (those rows are written by this launch's side blocks).
+template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
+          bool SEL = false>
 struct PConvFwdL {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false, RAW_ORDER = true;
@@ -697,7 +702,7 @@ struct PConvFwdL {
   static constexpr int R = OH * OW;
   using OA = Opnd<BM, false, 16>;
   static constexpr int T = WM * WN * 64, NA = (OA::F4 + T - 1) / T;
-  Grid g;            // tiles_m = kListSlots * tiles per region
+  Grid g;            // tiles_m = 1 + kListSlots * tiles per region
   const float* in;
   const float* w;    // [KS][KS][C][OC]
   const float* bias;
@@ -705,44 +710,43 @@ struct PConvFwdL {
   const int* list;   // [kListSlots][cap]
   int cap;
   const unsigned long long* cnt;   // this layer's counter of region 0 (region x at x * 2 * kCntStride)
-  struct ACtx { int off[NA]; };
+  const float* cx;   // constant input row [C]
+  float* cbuf;       // constant output row [OC]
+  struct ACtx { int off[NA]; uint32_t m[NA]; };   // input offset (-1: no row), taps read from cx
   struct Pre { float b; int o[4]; };
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return KS * KS * C / BK; }
-  // region of a GEMM row and its index there
-  __device__ static void where(int row, int& x, int& lr) {
-    const int tm = row / BM;
-    x = tm % kListSlots;
-    lr = (tm / kListSlots) * BM + row % BM;
-  }
   __device__ int count(int x) const { return (int)(cnt[x * 2 * kCntStride] >> 32); }
-  __device__ bool active(int, int row0) const {
-    int x, lr;
-    where(row0, x, lr);
-    return lr < count(x);
-  }
+  // list entry of a GEMM row: >= 0 a row (SEL: with its constant-tap mask << 20), -1 none, -2 the constant row
   __device__ int entry(int row) const {
-    int x, lr;
-    where(row, x, lr);
+    const int tm = row / BM;
+    if (tm == 0) return row == 0 ? -2 : -1;
+    const int x = (tm - 1) % kListSlots, lr = ((tm - 1) / kListSlots) * BM + row % BM;
     return lr < count(x) ? list[x * cap + lr] : -1;
   }
-  // input offsets of the thread's NA operand rows (-1: past the count)
+  __device__ bool active(int, int row0) const {   // (row tile 0 only where the constant row has somewhere to go)
+    const int tm = row0 / BM;
+    return tm == 0 ? cbuf != nullptr : ((tm - 1) / kListSlots) * BM < count((tm - 1) % kListSlots);
+  }
   __device__ ACtx a_ctx(int, int row0, int tid) const {
     ACtx c;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int r, k;
       OA::coord(tid + i * T, r, k);
-      const int e = entry(row0 + r);
+      const int raw = entry(row0 + r), e = raw >= 0 ? raw & 0xFFFFF : raw;
       const int b = e / R, p = e - b * R, oh = p / OW, ow = p - oh * OW;
       c.off[i] = e >= 0 ? ((b * H + oh * S) * W + ow * S) * C : -1;
+      c.m[i] = e == -2 ? 0xFFFFFFFFu : (SEL && raw >= 0 ? (uint32_t)raw >> 20 : 0u);
     }
     return c;
   }
   __device__ f32x4 ldA_c(const ACtx& c, int i, int, int s, int, int k) const {
     const int tap = (s * BK) / C, c0 = (s * BK) % C, kh = tap / KS, kw = tap % KS;
     const int o = c.off[i];
-    return ld4m(in + (size_t)(o < 0 ? 0 : o) + (kh * W + kw) * C + c0 + k, o >= 0);
+    const bool cst = (c.m[i] >> tap) & 1u;
+    const float* src = cst ? cx + c0 + k : in + (size_t)(o < 0 ? 0 : o) + (kh * W + kw) * C + c0 + k;
+    return ld4m(src, cst || o >= 0);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w + (size_t)(s * BK + k) * OC + col); }
   __device__ Pre epi_pre(int, int row, int col) const {
@@ -750,94 +754,57 @@ struct PConvFwdL {
     q.b = bias[col];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int e = entry(row + r);
-      q.o[r] = e >= 0 ? e * OC : -1;
+      const int raw = entry(row + r);
+      q.o[r] = raw >= 0 ? (raw & 0xFFFFF) * OC : raw;
     }
     return q;
   }
   __device__ void epi_post(int, int, int col, f32x4 v, const Pre& q) const {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r) {
       if (q.o[r] >= 0) out[(size_t)q.o[r] + col] = relu(v[r] + q.b);
+      else if (q.o[r] == -2) cbuf[col] = relu(v[r] + q.b);
+    }
   }
 };
 template <int BM, int BN, int WM, int WN>
-using PConv2FwdL = PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, BM, BN, WM, WN>;
+using PConv2FwdL = PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, BM, BN, WM, WN, false>;
 template <int BM, int BN, int WM, int WN>
-using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN>;
+using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN, true>;
 
-// The constant row's chain for output channel tid (tid < 64; every thread of the block calls it: it has barriers):
-// acc = chain over k = (kh, kw, ch) of x[ch] W[kh][kw][ch][tid] - the GEMM's chain on the constant input row x (LDS).  W is
-// staged through LDS (wg, GR k-rows) a group at a time, the next group's loads in flight in registers while wave 0 chains
-// the current one (one memory latency per group).  Measured alternatives: the chain on v_mfma_f32_16x16x4_f32 with W
-// streamed to registers 16 k-steps ahead (each batch waited out its loads: 3x slower), one LDS round of 16 weights per
-// 16 fmas (unroll 1: 1.6x slower), every round unrolled (238 VGPRs for the whole launch: the GEMM tiles lost occupancy).
-template <int KS, int C>
-__device__ __forceinline__ float const_chain(const float* xs, const float* w, float* wg, int tid) {
-  constexpr int K = KS * KS * C, GR = 128, NG = (K + GR - 1) / GR, NF = GR * 64 / 4 / 256;
-  static_assert(GR % C == 0, "groups of whole channel runs");
-  f32x4 r[NF];
-  auto ldg = [&](int g) {
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int e = 4 * (tid + 256 * i);   // float index in the group; its k-row e / 64
-      r[i] = ld4m(w + (size_t)g * GR * 64 + e, g * GR + e / 64 < K);
-    }
-  };
-  ldg(0);
-  float acc = 0.0f;
-  for (int g = 0; g < NG; ++g) {
-#pragma unroll
-    for (int i = 0; i < NF; ++i) *reinterpret_cast<f32x4*>(wg + 4 * (tid + 256 * i)) = r[i];
+// The constant rows as the first block of the conv2 launch: the conv2 constant row (input relu(0 + b0) -> c2), then, from
+// c2, the conv3 constant row (-> c3), each as the constant-row tile of a 16 x 64 list policy (4 waves x 16 channels, the
+// GEMM's chains).  Both are ready when the conv3 launch starts, so its side blocks can write the background rows of a2
+// and a3 and the fc1 forward reads a complete a3.
+template <class PA, class PB>
+struct ConstRows {
+  static constexpr size_t LDS = gemm_lds_bytes<PA>() > gemm_lds_bytes<PB>() ? gemm_lds_bytes<PA>() : gemm_lds_bytes<PB>();
+  PA pa;
+  PB pb;
+  __host__ __device__ int blocks() const { return 1; }
+  __device__ void run(int, float* lds) const {
+    gemm_body(pa, 0, lds);
     __syncthreads();
-    if (g + 1 < NG) ldg(g + 1);
-    if (tid < 64) {   // wave 0: k = GR g + kk in order (channel kk % C)
-      const int kn = K - g * GR < GR ? K - g * GR : GR;
-#pragma unroll 32
-      for (int kk = 0; kk < kn; ++kk) acc = __builtin_fmaf(xs[kk % C], wg[kk * 64 + tid], acc);
-    }
-    __syncthreads();
+    __threadfence();   // c2 (stored by this block's epilogue) is pb's constant input
+    gemm_body(pb, 0, lds);
   }
-  return acc;
-}
+};
 
-// Leading blocks of a list launch (256 threads): the background rows.  The constant output row c[oc] = relu(const_chain +
-// bias[oc]):
-// conv2 (KS = 4, C = 32): every block computes it from x = relu(0 + b0) (every conv1 output over background pixels), and
-// block 0 then also computes the next layer's constant row c3 from c (KS2 = 3, C2 = 64) into c_next; conv3 (KS = 0): c is
-// read from there.  Each block writes c to its share of the background rows (the back ends of the list regions).
-template <int KS, int C, int KS2 = 0, int C2 = 0>
+// Leading blocks of a list launch (256 threads): the layer below's background rows get its constant row c_in, 16 lanes
+// (256 bytes) per row, 8 list entries per lane loaded together (the back ends of the list regions).
 struct BgRows {
-  static constexpr size_t LDS = (128 + 128 * 64) * sizeof(float);
-  static constexpr int U = 8;   // background rows per 16-lane group per round (their list entries loaded together)
+  static constexpr size_t LDS = 64 * sizeof(float);
+  static constexpr int U = 8;
   int nblk;
   const int* list;         // [kListSlots][cap]
-  const unsigned long long* cnt;   // this layer's counter of region 0
+  const unsigned long long* cnt;   // that layer's counter of region 0
   int cap;                 // rows per region
-  const float* x_bias;     // conv2: b0 (x = relu(0 + b0))
-  const float* w;          // [KS][KS][C][64]
-  const float* bias;
-  const float* c_in;       // KS = 0: the constant row
-  const float* w2;         // KS2 > 0: the next layer's weights [KS2][KS2][C2][64] and bias
-  const float* bias2;
-  float* c_next;           // KS2 > 0: block 0 stores the next layer's constant row here
+  const float* c_in;       // [64]
   float* out;              // [rows][64]
   __host__ __device__ int blocks() const { return nblk; }
   __device__ void run(int blk, float* lds) const {
-    const int tid = threadIdx.x;
-    float* xs = lds;         // x [C]
-    float* cs = lds + 64;    // c [64]
-    float* wg = lds + 128;   // W group [128][64]
-    if constexpr (KS > 0) {
-      if (tid < C) xs[tid] = relu(0.0f + x_bias[tid]);
-      const float acc = const_chain<KS, C>(xs, w, wg, tid);   // (its first barrier orders xs)
-      if (tid < 64) cs[tid] = relu(acc + bias[tid]);
-    } else {
-      if (tid < 64) cs[tid] = c_in[tid];
-    }
-    __syncthreads();
-    const int q = tid & 15;
-    const f32x4 v = ld4(cs + 4 * q);
+    const int tid = threadIdx.x, q = tid & 15;
+    const f32x4 v = ld4(c_in + 4 * q);
     for (int x = 0; x < kListSlots; ++x) {
       const int nbg = (int)(uint32_t)cnt[x * 2 * kCntStride];
       const int* back = list + (size_t)(x + 1) * cap - 1;
@@ -850,12 +817,15 @@ struct BgRows {
           if (e[u] >= 0) *reinterpret_cast<f32x4*>(out + (size_t)e[u] * 64 + 4 * q) = v;
       }
     }
-    if constexpr (KS2 > 0) {
-      if (blk == 0) {
-        const float acc = const_chain<KS2, C2>(cs, w2, wg, tid);
-        if (tid < 64) c_next[tid] = relu(acc + bias2[tid]);
-      }
-    }
+  }
+};
+struct BgRows2 {   // two background-row jobs (a2 and a3) in one launch's leading blocks
+  static constexpr size_t LDS = BgRows::LDS;
+  BgRows a, b;
+  __host__ __device__ int blocks() const { return a.nblk + b.nblk; }
+  __device__ void run(int blk, float* lds) const {
+    if (blk < a.nblk) a.run(blk, lds);
+    else b.run(blk - a.nblk, lds);
   }
 };
 
@@ -1478,6 +1448,7 @@ struct C1Lists {
   unsigned long long* cnt;        // this forward's counters
   unsigned long long* cnt_next;   // the next forward's (double-buffered by forward parity), zeroed here
   int mode;                       // (experiment) 1: no flush, 2: flush without stores
+  float* xbg;                     // relu(0 + b0) [32]
 };
 constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
 
@@ -1550,7 +1521,17 @@ __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int
   for (int it = 0; it < nit; ++it) {
     const unsigned long long bn = cl[(it * 3 + wave) * 2], bb = cl[(it * 3 + wave) * 2 + 1];
     const int e = (b0 + it * G) * R + p;
-    if ((bn >> lane) & 1ull) rl[on + __builtin_popcountll(bn & below)] = e;
+    int tap = 0;   // conv3 rows: the taps whose conv2 position is background (PConvFwdL SEL), bits 20..28 of the entry
+    if (wave == 2) {
+      const unsigned long long g0 = cl[(it * 3) * 2 + 1], g1 = cl[(it * 3 + 1) * 2 + 1];   // conv2 background, 0..63, 64..80
+      const int i = p / 7, j = p - 7 * (p / 7);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int q = (i + t / 3) * 9 + j + t % 3;
+        tap |= (int)(((q < 64 ? g0 >> q : g1 >> (q - 64)) & 1ull) << t);
+      }
+    }
+    if ((bn >> lane) & 1ull) rl[on + __builtin_popcountll(bn & below)] = e | (tap << 20);
     else if ((bb >> lane) & 1ull) rl[cap - 1 - (og + __builtin_popcountll(bb & below))] = e;
     on += __builtin_popcountll(bn);
     og += __builtin_popcountll(bb);
@@ -1578,6 +1559,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (lists) {
     if (blockIdx.x == 0 && tid < 2 * kListSlots) L.cnt_next[tid * kCntStride] = 0ull;
+    if (blockIdx.x == 0 && tid < 32) L.xbg[tid] = relu(0.0f + b0[tid]);   // conv2's constant input row
     if (tid < 3 * kC1RmDw) rm[tid] = 0u;
     __syncthreads();
   }

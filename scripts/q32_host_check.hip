@@ -131,26 +131,32 @@ int main(int argc, char** argv) {
   // forward over n
   replay(PConv2Fwd{grid(n * 81, 64, 64, 64, 1), a1, w1, b1, a2, n * 81}, "conv2_fwd");
   replay(PConv3Fwd{grid(n * 49, 64, 64, 64, 1), a2, w2, b2, a3, n * 49}, "conv3_fwd");
-  {  // row-list forwards (background rows): per region a permutation of the rows, 2 / 3 of them non-background (or all)
+  {  // row-list forwards (background rows): per region a permutation of the rows, 2 / 3 of them non-background (or all),
+     // conv3 entries carrying constant-tap masks; the constant-row tiles
     const int G = std::min(n, 512), per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     int* rl2 = buf<int>((size_t)kListSlots * cap2);
     int* rl3 = buf<int>((size_t)kListSlots * cap3);
     for (int i = 0; i < kListSlots * cap2; ++i) rl2[i] = (int)(((long)i * 7919) % (n * 81));
-    for (int i = 0; i < kListSlots * cap3; ++i) rl3[i] = (int)(((long)i * 7919) % (n * 49));
+    for (int i = 0; i < kListSlots * cap3; ++i) rl3[i] = (int)(((long)i * 7919) % (n * 49)) | ((i * 37) % 511) << 20;
     unsigned long long* cnt = buf<unsigned long long>(2 * kListSlots * kCntStride);
+    float* cx = buf<float>(64);
+    float* c2 = buf<float>(64);
+    float* c3 = buf<float>(64);
     for (int full = 0; full < 2; ++full) {
       for (int x = 0; x < kListSlots; ++x) {
         const unsigned long long k2 = full ? cap2 : cap2 * 2 / 3, k3 = full ? cap3 : cap3 * 2 / 3;
         cnt[(x * 2) * kCntStride] = k2 << 32 | (cap2 - k2);
         cnt[(x * 2 + 1) * kCntStride] = k3 << 32 | (cap3 - k3);
       }
-      auto lg = [&](int cap, int BM, int BN) { return Grid{kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
-      replay(PConv2FwdL<64, 64, 2, 2>{lg(cap2, 64, 64), a1, w1, b1, a2, rl2, cap2, cnt}, "conv2_fwd L");
-      replay(PConv3FwdL<64, 64, 2, 2>{lg(cap3, 64, 64), a2, w2, b2, a3, rl3, cap3, cnt + kCntStride}, "conv3_fwd L");
-      replay(PConv2FwdL<64, 32, 2, 2>{lg(cap2, 64, 32), a1, w1, b1, a2, rl2, cap2, cnt}, "conv2_fwd LS");
-      replay(PConv3FwdL<64, 32, 2, 2>{lg(cap3, 64, 32), a2, w2, b2, a3, rl3, cap3, cnt + kCntStride}, "conv3_fwd LS");
+      auto lg = [&](int cap, int BM, int BN) { return Grid{1 + kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
+      replay(PConv2FwdL<64, 64, 2, 2>{lg(cap2, 64, 64), a1, w1, b1, a2, rl2, cap2, cnt, cx, nullptr}, "conv2_fwd L");
+      replay(PConv3FwdL<64, 64, 2, 2>{lg(cap3, 64, 64), a2, w2, b2, a3, rl3, cap3, cnt + kCntStride, c2, nullptr}, "conv3_fwd L");
+      replay(PConv2FwdL<64, 32, 2, 2>{lg(cap2, 64, 32), a1, w1, b1, a2, rl2, cap2, cnt, cx, nullptr}, "conv2_fwd LS");
+      replay(PConv3FwdL<64, 32, 2, 2>{lg(cap3, 64, 32), a2, w2, b2, a3, rl3, cap3, cnt + kCntStride, c2, nullptr}, "conv3_fwd LS");
     }
+    replay(PConv2FwdL<16, 64, 1, 4>{Grid{1, 1, 1}, a1, w1, b1, a2, rl2, cap2, cnt, cx, c2}, "const row c2");
+    replay(PConv3FwdL<16, 64, 1, 4>{Grid{1, 1, 1}, a2, w2, b2, a3, rl3, cap3, cnt + kCntStride, c2, c3}, "const row c3");
   }
   replay(PFc1Fwd{grid(n, PFc1Fwd::BM, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd");
   replay(PFc1FwdB{grid(n, 64, 512, 64, 1), a3, w3, b3, a4, n}, "fc1_fwd B");
