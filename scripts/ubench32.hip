@@ -434,7 +434,7 @@ int main(int argc, char** argv) {
     {
       const int G = std::min(B, 512);
       CK(hipFuncSetAttribute((const void*)k_conv1_fwd32<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kC1Frames));
-      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32<0>, dim3(G), dim3(256), 2 * kC1Frames, 0, table, B, W0, W0 + 8192, a1, 1); });
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32<0>, dim3(G), dim3(256), 2 * kC1Frames, 0, table, B, W0, W0 + 8192, a1, 1, C1Lists{}); });
       const double f = 2.0 * B * 400 * 32 * 256;
       printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_fwd (k_conv1_fwd32)", G, 2 * kC1Frames, us, f / us / 1e6,
              f / us / 1e6 / 157.3 * 100);
