@@ -715,12 +715,11 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     // background rows: conv1 lists them, conv2 / conv3 run the rest (the list counters alternate between forwards)
     const bool lists = bg_rows();
     unsigned long long* cnt = w.frcnt + 2 * kListSlots * kCntStride * w.fparity;
-    static const int bg_mode = std::getenv("QLX_F32_BG_MODE") ? atoi(std::getenv("QLX_F32_BG_MODE")) : 0;
     const int G = std::min(n, 2 * num_cus());                          // conv1 blocks
     const int per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);   // samples of a list region, at most
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
-    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1), bg_mode,
+    const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1),
                     w.fbgc};
     if (lists) w.fparity ^= 1;
     {
@@ -741,7 +740,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       // conv2: the non-background rows, the constant rows c2 and c3 in its first block (ConstRows); conv3: the non-background
       // rows (background conv2 taps read from c2), side blocks writing c2 / c3 to the background rows of a2 / a3
       static const int tile = std::getenv("QLX_F32_BG_TILE") ? atoi(std::getenv("QLX_F32_BG_TILE")) : 0;
-      const int nw = bg_mode == 3 ? 0 : std::min(256, std::max(16, n / 16));   // background-row blocks per job
+      const int nw = std::min(256, std::max(16, n / 16));   // background-row blocks per job
       float* c2 = w.fbgc + 32;
       float* c3 = w.fbgc + 96;
       const BgRows2 s23{{nw, w.frl2, cnt, cap2, c2, w.fa2}, {nw, w.frl3, cnt + kCntStride, cap3, c3, w.fa3}};
@@ -749,7 +748,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       using PC3 = PConv3FwdL<16, 64, 1, 4>;
       const ConstRows<PC2, PC3> cr{PC2{Grid{1, 1, 1}, w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, c2},
                                    PC3{Grid{1, 1, 1}, w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride, c2, c3}};
-      auto lgrid = [&](int cap, int BM, int BN) { return Grid{1 + (bg_mode == 4 ? 0 : kListSlots * ((cap + BM - 1) / BM)), 64 / BN, 1}; };
+      auto lgrid = [&](int cap, int BM, int BN) { return Grid{1 + kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
       auto run = [&](auto t2, auto t3, const char* sc2, const char* sc3) {
         using P2 = decltype(t2);
         using P3 = decltype(t3);

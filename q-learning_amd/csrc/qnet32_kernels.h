@@ -1447,7 +1447,6 @@ struct C1Lists {
   int cap2, cap3;                 // rows per region
   unsigned long long* cnt;        // this forward's counters
   unsigned long long* cnt_next;   // the next forward's (double-buffered by forward parity), zeroed here
-  int mode;                       // (experiment) 1: no flush, 2: flush without stores
   float* xbg;                     // relu(0 + b0) [32]
 };
 constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
@@ -1517,7 +1516,6 @@ __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int
   old = __shfl(old, 0);
   int on = (int)(old >> 32), og = (int)(uint32_t)old;
   const unsigned long long below = (1ull << lane) - 1ull;
-  if (L.mode == 2) { if (old == 12345) rl[0] = 0; return; }
   for (int it = 0; it < nit; ++it) {
     const unsigned long long bn = cl[(it * 3 + wave) * 2], bb = cl[(it * 3 + wave) * 2 + 1];
     const int e = (b0 + it * G) * R + p;
@@ -1636,7 +1634,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
     }
     __syncthreads();
   }
-  if (lists && wave < 3 && L.mode != 1) c1_lists_flush(cl, (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x, blockIdx.x, gridDim.x, L, wave, tid, B);
+  if (lists && wave < 3) c1_lists_flush(cl, (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x, blockIdx.x, gridDim.x, L, wave, tid, B);
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
