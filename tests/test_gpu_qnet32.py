@@ -35,6 +35,15 @@ def rand_states(B, seed, sparse=False):
     return rng.integers(0, 256, size=(B, 84, 84, 4), dtype=np.uint8)
 
 
+def edge_states(B):
+    """One bright pixel per sample (every x and y over the batch, all four frames): the background classification's
+    block boundaries (4-pixel blocks, 20 / 36-pixel receptive fields at stride 8) are crossed at every offset."""
+    x = np.zeros((B, 84, 84, 4), np.uint8)
+    for b in range(B):
+        x[b, b % 84, (b * 13 + b // 84) % 84, b % 4] = 1 + b % 255
+    return x
+
+
 def env_states(B, seed=123):
     """Real Breakout observations from the oracle env (random play)."""
     out = []
@@ -78,7 +87,7 @@ def test_init_weights_bit_identical():
 
 
 @pytest.mark.parametrize("B,kind", [(1, "env"), (31, "rand"), (129, "sparse"), (256, "env"), (1024, "mixed"), (64, "zero"),
-                                    (3000, "env")])
+                                    (3000, "env"), (336, "edge"), (2600, "edge")])
 def test_forward_bit_exact(B, kind):
     """Every layer bit for bit.  The conv2 / conv3 forward computes the non-background rows as a GEMM and writes the
     constant rows of the background ones (qnet32_kernels.h C1Lists): env frames are mostly background, random frames
@@ -88,7 +97,7 @@ def test_forward_bit_exact(B, kind):
     ref = O.QNet(seed=2, f32=True)
     randomize(m, ref, B)
     x = {"env": lambda: env_states(B), "rand": lambda: rand_states(B, B), "sparse": lambda: rand_states(B, B, True),
-         "mixed": lambda: mixed_states(B, B), "zero": lambda: np.zeros((B, 84, 84, 4), np.uint8)}[kind]()
+         "mixed": lambda: mixed_states(B, B), "zero": lambda: np.zeros((B, 84, 84, 4), np.uint8), "edge": lambda: edge_states(B)}[kind]()
     q, a = m.q_values(x)
     qr, acts = ref.forward(x, acts=True)
     for layer in range(1, 5):
