@@ -859,7 +859,7 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
     f32_head(3, a, B, s);
   }
   {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its leading blocks
-    PFc1WgradS Pw{grid(3136, 64, 512, 32, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
+    PFc1WgradS Pw{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
     PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
     SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
     launch_pair(m, Pw, Pd, S, "f32_fc1_bwd", 2.0 * 2.0 * B * 512 * 3136, s);

@@ -939,7 +939,9 @@ struct PFc1WgradT {
   __device__ void epi_bias(int, int col, float v) const { db3[col] = v; }
 };
 using PFc1Wgrad = PFc1WgradT<>;
-using PFc1WgradS = PFc1WgradT<64, 32, 2, 2>;
+// training batch: 64 x 64 tiles (392 + the fc1 backward-data tiles; in place at C3: 68.6 -> 65.1 us per fc1 backward
+// against 64 x 32, 128 x 64 75.3, 64 x 128 77.3, 128 x 128 91.1 - gpurun_out/fc1b, fc1c)
+using PFc1WgradS = PFc1WgradT<64, 64, 2, 2>;
 
 // conv3 backward-data: dz2 [B][9][9][64] = convT(dz3, W2) * (a2 > 0); rows (b, ih, iw), k = (kh, kw, oc)
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>

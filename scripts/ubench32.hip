@@ -454,7 +454,7 @@ int main(int argc, char** argv) {
       uint8_t* act = nullptr;
       CK(hipMalloc(&act, B));
       CK(hipMemset(act, 1, B));
-      PFc1WgradS Pw{grid(3136, 64, 512, 32, 1), a3, dz4, gw, gw, B};
+      PFc1WgradS Pw{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), a3, dz4, gw, gw, B};
       PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B};
       SideFc2 S{a4, act, dz4, dz4 + 1024, B, gw, gw + 2000, gw + 3000};
       const size_t lds = std::max({gemm_lds_bytes<PFc1WgradS>(), gemm_lds_bytes<PFc1DgradS>(), SideFc2::LDS});
