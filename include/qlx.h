@@ -128,6 +128,9 @@ typedef struct qlx_model qlx_model;
 int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out);
 int32_t qlx_model_destroy(qlx_model* m);
 int32_t qlx_model_num_vars(void);
+/* The optimizer hyperparameters every model is created with, out[5] = {learning_rate, beta_1, beta_2, epsilon, clipnorm}
+ * (float32; the reference's Keras optimizer_config, keras_metadata.pb; no device needed). */
+int32_t qlx_model_hparams(float* out);
 int64_t qlx_model_var_size(int32_t var);
 /* which: 0 = weights, 1 = Adam m, 2 = Adam v.  Layout = Keras HWIO / [in,out]. */
 int32_t qlx_model_get_var(qlx_model* m, int32_t var, int32_t which, float* out);
@@ -315,6 +318,8 @@ typedef struct qlx_bg_model qlx_bg_model;
 /* Conv(32, 2x2 same)-Conv(32, 1x1)-Dense512-Dense5 in fp32; GlorotUniform from stream (seed, var, 1);
  * 8 variables k0 [2,2,4,32] b0 k1 [1,1,32,32] b1 k2 [288,512] b2 k3 [512,5] b3. */
 int32_t qlx_bg_model_create(uint64_t seed, int32_t device, qlx_bg_model** out);
+/* as qlx_model_hparams, for the BallGame model (create_ql_model_ballgame_3x3x4_5_512.py's Adam) */
+int32_t qlx_bg_model_hparams(float* out);
 int32_t qlx_bg_model_destroy(qlx_bg_model* m);
 int64_t qlx_bg_model_var_size(int32_t var);
 int32_t qlx_bg_model_get_var(qlx_bg_model* m, int32_t var, int32_t which, float* out);

@@ -415,7 +415,7 @@ void BgLearner::update(const uint64_t* idx, const float* isw, const float* y) {
   if (p.flags & 2u) {   // (|td| + eps)^alpha per drawn slot, the last draw wins
     const uint64_t start = (total_pushed - replay.size()) % p.history_buffer_len;
     for (int b = 0; b < B; ++b) {
-      const float pr = std::pow(td[b] + p.per_eps, p.per_alpha);
+      const float pr = det_powf(td[b] + p.per_eps, p.per_alpha);
       tree.set((start + idx[b]) % p.history_buffer_len, pr);
       per_max = std::max(per_max, pr);
     }

@@ -23,6 +23,35 @@ void generate_distinct_random_ids(uint64_t seed, uint32_t update_idx, uint32_t r
   }
 }
 
+float det_powf(float xf, float yf) {
+  if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : (yf < 0.0f ? INFINITY : 1.0f)) : NAN;
+  if (std::isinf(xf)) return yf > 0.0f ? INFINITY : (yf < 0.0f ? 0.0f : 1.0f);
+  int e = 0;
+  double m = std::frexp((double)xf, &e);   // x = m 2^e, m in [0.5, 1) -> [sqrt(1/2), sqrt(2))
+  if (m < 0.70710678118654752440) {
+    m *= 2.0;
+    e -= 1;
+  }
+  const double f = (m - 1.0) / (m + 1.0);
+  const double s = f * f;
+  double series = 1.0 / 23.0;   // sum_{i <= 11} s^i / (2 i + 1), Horner from the top term
+  for (int i = 10; i >= 0; --i) series = std::fma(series, s, 1.0 / (double)(2 * i + 1));
+  const double ln_x = std::fma((double)e, 0.69314718055994530942, (f * series) * 2.0);
+  const double z = (double)yf * ln_x;
+  if (z > 700.0) return INFINITY;
+  if (z < -745.0) return 0.0f;
+  const double k = std::rint(z * 1.44269504088896340736);   // z = k ln2 + r
+  double r = std::fma(-k, 6.93147180369123816490e-01, z);
+  r = std::fma(-k, 1.90821492927058770002e-10, r);
+  double factorial = 1307674368000.0;   // 15!
+  double poly = 1.0 / factorial;
+  for (int i = 14; i >= 0; --i) {
+    factorial = factorial / (double)(i + 1);
+    poly = std::fma(poly, r, 1.0 / factorial);
+  }
+  return (float)std::ldexp(poly, (int)k);
+}
+
 void per_sample(const SumTree& st, uint64_t seed, uint32_t update_idx, uint32_t rank, uint64_t len, float beta, int B,
                 uint64_t* slots, float* weights) {
   const float T = st.t[1];
@@ -34,7 +63,7 @@ void per_sample(const SumTree& st, uint64_t seed, uint32_t update_idx, uint32_t 
     const float u = seg * ((float)b + r);
     slots[b] = st.find(u);
     const float p = st.t[st.L + slots[b]] / T;
-    weights[b] = std::pow((float)len * p, -beta);
+    weights[b] = det_powf((float)len * p, -beta);
     wmax = std::max(wmax, weights[b]);
   }
   for (int b = 0; b < B; ++b) weights[b] = weights[b] / wmax;
@@ -255,7 +284,7 @@ void Learner::update(const uint64_t* idx, const float* isw, const float* y) {
   if (p.flags & 2u) {   // new priorities (|td| + eps)^alpha, in batch order (a repeated slot keeps its last value)
     const uint64_t start = (total_pushed - replay.len()) % p.history_buffer_len;
     for (int b = 0; b < B; ++b) {
-      const float pr = std::pow(td[b] + p.per_eps, p.per_alpha);
+      const float pr = det_powf(td[b] + p.per_eps, p.per_alpha);
       tree.set((start + idx[b]) % p.history_buffer_len, pr);
       per_max = std::max(per_max, pr);
     }

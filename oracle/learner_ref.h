@@ -94,6 +94,12 @@ struct SumTree {
     return i - L;
   }
 };
+// x^y of the prioritized replay (priorities (|td| + eps)^alpha, IS weights (len p)^-beta) as the build defines it
+// (the product's per.hip per_powf follows the same steps): exp(y ln x) evaluated in binary64 with IEEE basic
+// operations only (ln m by the atanh series in f = (m - 1) / (m + 1), exp by argument reduction + a degree-15 Taylor
+// polynomial, every multiply-add an explicit fma), rounded once to binary32.  Not the library powf: glibc and the device
+// libm each round their own way in the last bit, and one ulp in a leaf moves the sum tree's partial sums.
+float det_powf(float x, float y);
 // one prioritized batch: physical slots and normalised IS weights
 void per_sample(const SumTree& st, uint64_t seed, uint32_t update_idx, uint32_t rank, uint64_t len, float beta, int B,
                 uint64_t* slots, float* weights);

@@ -152,6 +152,10 @@ void orc_envs_run(uint64_t env_seed, uint32_t n_envs, uint32_t n_steps, uint64_t
 // ---------------- Q-network ----------------
 void* orc_qnet_new(uint64_t seed) { auto* q = new QNet; qnet_init_glorot(*q, seed); return q; }
 void orc_qnet_free(void* h) { delete (QNet*)h; }
+void orc_qnet_hparams(void* h, float* out) {   // lr, beta_1, beta_2, epsilon, clipnorm
+  const QNet* q = (const QNet*)h;
+  out[0] = q->lr; out[1] = q->beta1; out[2] = q->beta2; out[3] = q->eps; out[4] = q->clipnorm;
+}
 int orc_var_size(int v) { return kVarSize[v]; }
 void orc_qnet_get(void* h, int var, int which, float* out) {
   QNet* q = (QNet*)h;
@@ -287,6 +291,9 @@ void orc_per_sample(const float* leaves, uint64_t cap, uint64_t seed, uint32_t f
   for (uint32_t u = 0; u < n_updates; ++u)
     per_sample(st, seed, first_update + u, rank, len, beta, B, slots + (size_t)u * B, weights + (size_t)u * B);
 }
+void orc_det_powf(const float* x, const float* y, uint64_t n, float* out) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = det_powf(x[i], y[i]);
+}
 size_t orc_learner_params_size() { return sizeof(LearnerParams); }
 size_t orc_state_size() { return sizeof(OrcState); }
 int orc_num_threads() { return omp_get_max_threads(); }
@@ -323,6 +330,10 @@ uint64_t orc_gen_range_usize_single(uint64_t seed, uint32_t c1, uint32_t c2, uin
 
 void* orc_bg_net_new(uint64_t seed) { auto* n = new BgNet; bg_net_init_glorot(*n, seed); return n; }
 void orc_bg_net_free(void* h) { delete (BgNet*)h; }
+void orc_bg_net_hparams(void* h, float* out) {
+  const BgNet* n = (const BgNet*)h;
+  out[0] = n->lr; out[1] = n->beta1; out[2] = n->beta2; out[3] = n->eps; out[4] = n->clipnorm;
+}
 int orc_bg_var_size(int v) { return kBgVarSize[v]; }
 void orc_bg_net_get(void* h, int var, int which, float* out) {
   BgNet* n = (BgNet*)h;

@@ -767,6 +767,14 @@ int32_t qlx_bg_env_set_states(qlx_bg_env* e, const qlx_ballgame_state* in) {
 
 // ---------------- model ----------------
 
+int32_t qlx_bg_model_hparams(float* out) {
+  return guard([&] {
+    QLX_CHECK(out, QLX_E_INVALID, "null out");
+    const qlx_bg_model m;   // the defaults every created model starts from (no device state is touched)
+    out[0] = m.lr; out[1] = m.beta1; out[2] = m.beta2; out[3] = m.eps; out[4] = m.clipnorm;
+  });
+}
+
 int32_t qlx_bg_model_create(uint64_t seed, int32_t device, qlx_bg_model** out) {
   return guard([&] {
     QLX_CHECK(out, QLX_E_INVALID, "null argument");

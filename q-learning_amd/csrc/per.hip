@@ -30,6 +30,41 @@ namespace qlx {
 
 constexpr uint32_t kTreeChunk = 2048;
 
+// x^y for the priorities (|td| + eps)^alpha and the IS weights (len p)^-beta, as the build defines it (DESIGN.md §6;
+// oracle/learner_ref.cpp det_powf restates it): exp(y ln x) in binary64 from IEEE basic operations only (+ - * / fma,
+// rint, frexp / ldexp), rounded once to binary32.  Library powf differs between the device (OCML) and glibc in the last
+// bit now and then, and a one-ulp leaf changes the sum tree's partial sums and so, rarely, a draw; with this definition
+// the prioritized learner is bit-exact against the oracle.  Accuracy: relative error ~1e-15 in binary64 before the
+// final rounding (within one float ulp of the correctly rounded powf; tests/test_oracle_per.py).
+__device__ __forceinline__ float per_powf(float xf, float yf) {
+#pragma clang fp contract(off)
+  if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : (yf < 0.0f ? __builtin_inff() : 1.0f)) : __builtin_nanf("");
+  if (__builtin_isinf(xf)) return yf > 0.0f ? __builtin_inff() : (yf < 0.0f ? 0.0f : 1.0f);
+  int e;
+  double m = frexp((double)xf, &e);   // [0.5, 1)
+  if (m < 0.70710678118654752440) { m = m * 2.0; e -= 1; }
+  const double f = (m - 1.0) / (m + 1.0), s = f * f;
+  // ln m = 2 f (1 + s / 3 + s^2 / 5 + ...), |f| <= 0.1716: 12 terms
+  double p = 1.0 / 23.0;
+#pragma unroll
+  for (int i = 10; i >= 0; --i) p = fma(p, s, 1.0 / (double)(2 * i + 1));
+  const double lnx = fma((double)e, 0.69314718055994530942, (f * p) * 2.0);
+  const double z = (double)yf * lnx;
+  if (z > 700.0) return __builtin_inff();
+  if (z < -745.0) return 0.0f;
+  const double kd = rint(z * 1.44269504088896340736);
+  double r = fma(-kd, 6.93147180369123816490e-01, z);   // ln 2 = hi + lo (hi: 32 significant bits)
+  r = fma(-kd, 1.90821492927058770002e-10, r);
+  double q = 1.0 / 1307674368000.0;                      // 1 / 15!
+  double fact = 1307674368000.0;
+#pragma unroll
+  for (int i = 14; i >= 0; --i) {
+    fact = fact / (double)(i + 1);                       // i! (exact: integers < 2^53)
+    q = fma(q, r, 1.0 / fact);
+  }
+  return (float)ldexp(q, (int)kd);
+}
+
 // block j reduces nodes [W + j S, W + (j + 1) S) of one level up log2(S) levels, storing every parent
 __global__ __launch_bounds__(256) void k_tree_build(float* t, uint32_t W, uint32_t S) {
   __shared__ float cur[kTreeChunk];
@@ -89,7 +124,7 @@ __global__ __launch_bounds__(256) void k_per_sample(const float* t, uint32_t L, 
     }
     const uint64_t slot = i - L;
     const float p = t[i] / T;
-    const float w = powf((float)len * p, -beta);
+    const float w = per_powf((float)len * p, -beta);
     idx_out[(size_t)u * B + b] = (slot + cap - start) % cap;
     w_out[(size_t)u * B + b] = w;
     wmax = fmaxf(wmax, w);
@@ -131,7 +166,7 @@ __global__ void k_per_write(const uint64_t* idx, const float* td_abs, uint32_t n
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const uint64_t slot = (start + idx[k]) % cap;
-  const float pr = powf(td_abs[k] + eps, alpha);
+  const float pr = per_powf(td_abs[k] + eps, alpha);
   if (owner[slot] == k + 1) {
     leaves[slot] = pr;
     owner[slot] = 0;

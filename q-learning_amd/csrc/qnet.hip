@@ -783,6 +783,14 @@ using namespace qlx;
 extern "C" {
 
 int32_t qlx_model_num_vars(void) { return kNumVars; }
+
+int32_t qlx_model_hparams(float* out) {
+  return guard([&] {
+    QLX_CHECK(out, QLX_E_INVALID, "null out");
+    const qlx_model m;   // the defaults every created model starts from (no device state is touched)
+    out[0] = m.lr; out[1] = m.beta1; out[2] = m.beta2; out[3] = m.eps; out[4] = m.clipnorm;
+  });
+}
 int64_t qlx_model_var_size(int32_t v) { return (v >= 0 && v < kNumVars) ? kVarSize[v] : -1; }
 
 int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out) {

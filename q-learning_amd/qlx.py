@@ -127,7 +127,8 @@ def lib():
         "qlx_replay_sample_distinct": ([vp, u64, u32, u32, u32, vp], i32),
         "qlx_replay_get_many": ([vp, vp, u32, vp, vp, vp, vp, vp], i32),
         "qlx_model_create": ([i32, u64, i32, C.POINTER(vp)], i32), "qlx_model_destroy": ([vp], i32),
-        "qlx_model_num_vars": ([], i32), "qlx_model_var_size": ([i32], C.c_int64),
+        "qlx_model_num_vars": ([], i32), "qlx_model_var_size": ([i32], C.c_int64), "qlx_model_hparams": ([vp], i32),
+        "qlx_bg_model_hparams": ([vp], i32),
         "qlx_model_get_var": ([vp, i32, i32, vp], i32), "qlx_model_set_var": ([vp, i32, i32, vp], i32),
         "qlx_model_iterations": ([vp], C.c_int64), "qlx_model_copy_weights": ([vp, vp], i32),
         "qlx_model_predict": ([vp, vp, u32, vp, vp], i32), "qlx_model_batch_max_q": ([vp, vp, u32, vp], i32),
@@ -238,6 +239,13 @@ class _LearningStats:
 
     def learning_update_log(self):
         return _text(getattr(lib(), self._prefix + "_update_log"), self.h)
+
+
+def model_hparams(ballgame=False):
+    """(learning_rate, beta_1, beta_2, epsilon, clipnorm) every model is created with (float32, no device needed)"""
+    out = np.zeros(5, np.float32)
+    _check((lib().qlx_bg_model_hparams if ballgame else lib().qlx_model_hparams)(_p(out)))
+    return out
 
 
 def exported_symbols():

@@ -154,6 +154,9 @@ def lib():
         L.orc_learner_per.argtypes = [vp, vp, vp, vp]
         L.orc_per_sample.argtypes = [vp, u64, u64, u32, u32, u32, u64, f32, i32, vp, vp, vp]
         L.orc_bg_learner_per.argtypes = [vp, vp, vp]
+        L.orc_det_powf.argtypes = [vp, vp, u64, vp]
+        L.orc_qnet_hparams.argtypes = [vp, vp]
+        L.orc_bg_net_hparams.argtypes = [vp, vp]
         L.orc_dbscan_f32.argtypes = [vp, u64, f32, u64, vp]
         L.orc_dbscan_f32.restype = u64
         L.orc_dbscan_f32_format.argtypes = [vp, u64, f32, u64, C.c_char_p, C.c_size_t]
@@ -313,6 +316,12 @@ class QNet:
     def weights(self):
         return [self.get(v) for v in range(10)]
 
+    def hparams(self):
+        """(learning_rate, beta_1, beta_2, epsilon, clipnorm) as float32"""
+        out = np.zeros(5, np.float32)
+        lib().orc_qnet_hparams(self.h, _p(out))
+        return out
+
     def iterations(self):
         return lib().orc_qnet_iterations(self.h)
 
@@ -396,6 +405,15 @@ def per_sample(leaves, seed, first_update, n_updates, rank, length, beta, batch)
     lib().orc_per_sample(_p(x), x.shape[0], seed, first_update, n_updates, rank, length, beta, batch, _p(slots), _p(w),
                          C.byref(total))
     return slots.reshape(n_updates, batch), w.reshape(n_updates, batch), total.value
+
+
+def det_powf(x, y):
+    """oracle/learner_ref.cpp det_powf: the prioritized replay's x^y (binary64 from basic operations, one rounding)"""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.ascontiguousarray(np.broadcast_to(np.asarray(y, np.float32), x.shape), dtype=np.float32)
+    out = np.zeros(x.shape, np.float32)
+    lib().orc_det_powf(_p(x), _p(y), x.size, _p(out))
+    return out
 
 
 class Learner:
@@ -534,6 +552,11 @@ class BgNet:
 
     def weights(self):
         return [self.get(v) for v in range(8)]
+
+    def hparams(self):
+        out = np.zeros(5, np.float32)
+        lib().orc_bg_net_hparams(self.h, _p(out))
+        return out
 
     def forward(self, x, acts=False):
         x = np.ascontiguousarray(x, dtype=np.uint8)

@@ -57,6 +57,30 @@ def test_stratified_draws_follow_prefix_sums():
         assert w[u].max() == 1.0
 
 
+def test_det_powf_accuracy():
+    """det_powf (the x^y both sides of the prioritized replay evaluate) against the correctly rounded
+    float32 of the binary64 power: within one ulp everywhere, equal almost everywhere; the edge values of powf."""
+    rng = np.random.default_rng(7)
+    n = 400_000
+    x = np.concatenate([rng.random(n // 4) * 3 + 1e-6,                       # |td| + eps
+                        np.exp(rng.uniform(-20, 20, n // 4)),                # wide magnitudes
+                        rng.uniform(1e-3, 4096.0, n // 4),                   # len p of the IS weights
+                        rng.integers(1, 1 << 20, n // 4).astype(np.float64)]).astype(np.float32)
+    y = np.concatenate([np.full(n // 4, 0.6), rng.uniform(-3, 3, n // 4), np.full(n // 4, -0.4),
+                        rng.uniform(-1, 1, n // 4)]).astype(np.float32)
+    got = O.det_powf(x, y)
+    ref = np.power(x.astype(np.float64), y.astype(np.float64))
+    ok = np.isfinite(ref) & (ref < 3e38) & (ref > 1e-37)
+    exp32 = ref[ok].astype(np.float32)
+    ulps = np.abs(got[ok].view(np.int32).astype(np.int64) - exp32.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1, ulps.max()
+    assert (ulps == 0).mean() > 0.999, (ulps == 0).mean()
+    e = O.det_powf(np.array([0, 0, 0, 1, 2, np.inf, np.inf, np.nan, -1], np.float32),
+                   np.array([0.6, -0.4, 0, 0.6, 0, 1, -1, 1, 0.5], np.float32))
+    assert e[0] == 0 and np.isinf(e[1]) and e[2] == 1 and e[3] == 1 and e[4] == 1
+    assert np.isinf(e[5]) and e[6] == 0 and np.isnan(e[7]) and np.isnan(e[8])
+
+
 def test_high_priority_dominates():
     cap, B = 512, 512
     leaves = np.full(cap, 1e-3, np.float32)
