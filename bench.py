@@ -254,7 +254,8 @@ class Run:
         staggered start - over T steps, step k ends the current episode of the envs e = k (mod T) (the
         max_steps_per_episode path, qlx_learner_end_episodes); (3) step until one window of T vector steps has its
         episode ends per step averaging within STEADY_MEAN_TOL of n_envs / T with a coefficient of variation of at most
-        STEADY_MAX_CV.  Decisions are global (every rank runs the same number
+        STEADY_MAX_CV, for at most 3 T vector steps - when no window qualifies the bench still measures, but the JSON line
+        carries steady_state.steady = false and the log warns.  Decisions are global (every rank runs the same number
         of vector steps: each one carries collectives)."""
         import numpy as np
         N, ctl = self.args.envs, self.ctl
@@ -295,6 +296,8 @@ class Run:
         self.mean_len, self.expect_ends, self.steady_ok = mean_len, expect, ok
         self.steady_window = {"steps": T, "mean_ends": round(mean, 2), "cv": round(cv, 3), "min": int(min(ends[-T:])),
                               "max": int(max(ends[-T:]))}
+        if not ok:
+            log(f"WARNING {self.precision}: no steady window within {3 * T} vector steps; the line says steady: false")
         log(f"{self.precision}: {n} more vector steps to steady episode ends (mean episode {mean_len:.1f} env-steps, "
             f"staggered over {T}; {expect:.1f} ends expected per vector step; last window {self.steady_window}, steady {ok})")
         return n

@@ -184,8 +184,9 @@ typedef struct qlx_params { /* Parameter (self_driving_tf_q_learner.rs:20-67) + 
   uint32_t qnet_precision;     /* QLX_PREC_F32 (0, the reference's arithmetic) or QLX_PREC_BF16 */
   uint64_t stats_after_steps;  /* every this many env-steps: checkpoint + learning_update_log (0 = never) */
   char checkpoint_file[256];   /* write_checkpoint target of those events and of solved() (empty = not written) */
-  float episode_reward_goal;   /* goal solved() tests (Environment::episode_reward_goal_mean, prelude.rs); 0 = the env's
-                                  own (Breakout: bricks - 1, breakout_environment.rs:203-206); other values mock it */
+  float episode_reward_goal;   /* goal solved() tests (Environment::episode_reward_goal_mean, prelude.rs); NaN (the
+                                  qlx_params_default value) = the env's own (Breakout: bricks - 1,
+                                  breakout_environment.rs:203-206); any other value, 0 included, mocks it */
 } qlx_params;
 
 #define QLX_PREC_F32 0u
@@ -217,7 +218,8 @@ int32_t qlx_learner_prefill(qlx_learner* l, uint64_t n_vector_steps);
 /* End the current episode of every env with mask[e] != 0 now, as reaching max_steps_per_episode does (learn_episode
  * :214-224: the episode's reward enters the reward history, episode_count advances, the env resets); no transition is
  * added.  mask: host array [n_envs].  Lets a measurement start the envs' episodes at staggered steps (all envs launch
- * together, so with a short-lived policy their episodes otherwise end in waves).  Not in the reference loop. */
+ * together, so with a short-lived policy their episodes otherwise end in waves).  Not in the reference loop.  Data
+ * parallel: a collective (the global solved() statistics are all-reduced), so every rank calls it. */
 int32_t qlx_learner_end_episodes(qlx_learner* l, const uint8_t* mask);
 /* learn_till_mastered (self_driving_tf_q_learner.rs:127-132): vector steps until solved() or max_vector_steps. */
 int32_t qlx_learner_learn_till_mastered(qlx_learner* l, uint64_t max_vector_steps, uint64_t* steps_run);

@@ -4,6 +4,7 @@
 // The reference itself cannot be built here (no Rust toolchain, no libtensorflow); see DESIGN.md.
 #include <chrono>
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <omp.h>
 
@@ -24,6 +25,7 @@ int main(int argc, char** argv) {
   p.episode_reward_history_buffer_len = 100;
   p.n_envs = n_envs; p.batch_size = batch;
   p.env_seed = 0x51A5EED; p.learner_seed = 1; p.init_seed = 2; p.rank = 0;
+  p.episode_reward_goal = NAN;   // the env's own goal
   Learner l(p);
   l.pack_like_reference = true;   // the reference's per-element f32 tensor packing (learner_ref.h)
   const auto t0 = std::chrono::steady_clock::now();

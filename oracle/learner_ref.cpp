@@ -300,7 +300,7 @@ void Learner::update(const uint64_t* idx, const float* isw, const float* y) {
 bool Learner::solved() const {   // :134-139
   if (episode_rewards.empty()) return false;
   // episode_reward_goal_mean (breakout_environment.rs:203-206), or the mocked goal
-  const float goal = p.episode_reward_goal != 0.0f ? p.episode_reward_goal : (float)(kNumBricks - 1);
+  const float goal = std::isnan(p.episode_reward_goal) ? (float)(kNumBricks - 1) : p.episode_reward_goal;
   float mn = episode_rewards.front();
   for (float v : episode_rewards) mn = std::min(mn, v);
   return running_reward >= goal && mn >= goal * p.lowest_episode_reward_goal_threshold_pct;

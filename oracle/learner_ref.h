@@ -52,7 +52,7 @@ struct LearnerParams {   // layout mirrored by tests/oracle.py (ctypes)
   uint32_t qnet_precision;     // 0 fp32 (qnet32_ref.cpp, bit-exact definition), 1 bf16 product (double-accumulating oracle)
   uint64_t stats_after_steps;  // learning_update_log + write_checkpoint every this many env-steps (0 = never)
   char checkpoint_file[256];
-  float episode_reward_goal;   // 0 = the env's own (kNumBricks - 1); other values mock it (qlx.h)
+  float episode_reward_goal;   // NaN = the env's own (kNumBricks - 1); any other value mocks it (qlx.h)
 };
 
 using StateRef = std::shared_ptr<std::vector<uint8_t>>;   // Rc<BreakoutState> tensor view [x][y][slot]

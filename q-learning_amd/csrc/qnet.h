@@ -89,19 +89,10 @@ struct qlx_model {
   // conv1 weight gradient as channel-half blocks (k_conv1_wgrad_h); QLX_CONV1_HALVES=0 at create time selects the
   // one-block-per-chunk k_conv1_wgrad (bit-identical gradients)
   bool conv1_halves = true;
-  // fp32: clip_by_norm + Adam of the dense variables run inside the conv backward launches (their norm partials as
-  // trailing blocks of the conv3 pair, the update beside the conv2 pair's tiles) and the conv variables' in one small
-  // launch after the weight-gradient reduction, when the caller allows it (no all-reduce between backward and Adam).
-  // Opt-in (QLX_F32_FUSED_ADAM=1 at create time): measured at C3 200.6K vs 199.9K env-steps/s with the separate k_norm32 +
-  // k_adam32 launches (within run-to-run spread), while it puts Adam's HBM work inside the conv2 backward pair - the
-  // roofline kernel (111.7 -> 115.7 us).  (Update schedule 1.)
-  bool f32_fuse_enabled = false;
-  int f32_adam_pos = 0;   // QLX_F32_ADAM_POS: 0 leading blocks of the conv2 pair (measured best), 1 trailing blocks
-  // update schedule 2 (default when the caller allows it; QLX_F32_TAIL=0: off): the dense variables' norm partials as
-  // extra blocks of the weight-gradient reduction launch, then every variable's clip_by_norm + Adam in one launch
-  // (k_update32) - the update's tail is two launches instead of three
-  bool f32_tail_enabled = true;
-  int f32_update_mode = 0;   // set by a backward that scheduled the update (1 / 2), consumed by model_norms / model_adam
+  // fp32 update schedule (when the caller allows it: no all-reduce between backward and Adam): the dense variables' norm
+  // partials as extra blocks of the weight-gradient reduction launch, then every variable's clip_by_norm + Adam in one
+  // launch (k_update32) - the update's tail is two launches.  Set by the backward, consumed by model_norms / model_adam.
+  bool f32_update_scheduled = false;
   // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
   // sample's result does not depend on the batch it is evaluated in (the learner's target net)
   bool fc1_single = false;

@@ -801,12 +801,6 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     m->f32 = arch == QLX_ARCH_NATURE_DQN;
     const char* ch = std::getenv("QLX_CONV1_HALVES");
     m->conv1_halves = !(ch && ch[0] == '0');
-    const char* fa = std::getenv("QLX_F32_FUSED_ADAM");
-    m->f32_fuse_enabled = fa && fa[0] == '1';
-    const char* tl = std::getenv("QLX_F32_TAIL");
-    m->f32_tail_enabled = !(tl && tl[0] == '0');
-    const char* ap = std::getenv("QLX_F32_ADAM_POS");
-    m->f32_adam_pos = ap && ap[0] == '1' ? 1 : 0;
     try {   // a failure part-way releases what was built
       m->device = device;
       QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));

@@ -216,16 +216,6 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
   norm32_block(A, blockIdx.x, wsum);
 }
 
-// trailing blocks of a pair launch (k_gemm32_pair's T): the segment partials of the variables whose gradient is final
-// before that launch (the dense ones, after the fc1 backward), blocks first_seg ..
-struct NormTail {
-  static constexpr size_t LDS = 16;
-  NormArgs A;
-  int first_seg, nblocks;
-  __host__ __device__ int blocks() const { return nblocks; }
-  __device__ void run(int t, float* lds) const { norm32_block(A, first_seg + t, lds); }
-};
-
 // Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
 // [16 q, 16 q + 16)), S_q = chain over its chunks in order, dW = chain over q of S_q (each chain t = 0; t = t + x).
 // Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order, the last row of each the bias.
@@ -389,9 +379,8 @@ __global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
   }
 }
 
-// Blocks of a pair launch (k_gemm32_pair's S or T) running clip_by_norm + Adam of the dense variables (W3, b3, W4, b4 -
-// 95 % of the update's Adam bytes) once their norm partials exist, so that HBM-bound work runs beside the conv backward's
-// MFMA tiles instead of after the whole backward.  Same arithmetic as k_adam32 on those elements.
+// The dense variables' blocks of k_update32: clip_by_norm + Adam of W3, b3, W4, b4 (95 % of the update's Adam bytes)
+// from their norm partials.  Same arithmetic as k_adam32 on those elements.
 struct AdamDense {
   static constexpr size_t LDS = 64;
   Adam32Args A;
@@ -546,9 +535,8 @@ __device__ __forceinline__ void conv_adam_block(const Adam32Args& A, const NormA
   }
 }
 
-__global__ __launch_bounds__(1024) void k_conv_adam32(Adam32Args A, NormArgs N) { conv_adam_block(A, N, blockIdx.x); }
-
-// Update schedule 2 (qnet.h): clip_by_norm + Adam of every variable in one launch after the weight-gradient reduction -
+// The scheduled update (qnet.h f32_update_scheduled): clip_by_norm + Adam of every variable in one launch after the
+// weight-gradient reduction -
 // blocks [0, nconv) the conv variables (conv_adam_block: norm from the gradient itself), the rest the dense variables
 // (their segment partials came from the reduction launch; AdamDense arithmetic).  No block depends on another.
 __global__ __launch_bounds__(1024) void k_update32(Adam32Args A, NormArgs N, int nconv, int ndense) {
@@ -575,11 +563,16 @@ using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
 static_assert((1605632 + kNormSeg - 1) / kNormSeg <= kNormSegMax, "norm partials per variable");
 static_assert((36864 + kNormSeg - 1) / kNormSeg <= 4 * kConvSegsPerGroup && (32768 + kNormSeg - 1) / kNormSeg <= 4 * kConvSegsPerGroup,
-              "conv variable segments per k_conv_adam32 block");
+              "conv variable segments per conv_adam_block");
 static_assert((512 * 3 + kNormSeg - 1) / kNormSeg <= 64 && (32768 + kNormSeg - 1) / kNormSeg <= 64 &&
               (36864 + kNormSeg - 1) / kNormSeg <= 64 && (8192 + kNormSeg - 1) / kNormSeg <= 64, "<= 64 partials but W3");
 
 static int num_cus();
+
+// conv1 forward blocks for n samples: two per CU, but never more than kC1MaxIt samples per block (a block keeps its samples'
+// background flags in LDS until it writes its lists) - so a part with few CUs (a CPX partition) runs more blocks
+constexpr int kC1MaxIt = 64;
+static int c1_blocks(int n) { return std::max(std::min(n, 2 * num_cus()), (n + kC1MaxIt - 1) / kC1MaxIt); }
 
 void f32_workspace(qlx_model* m, int B) {
   if (B <= m->ws_batch) return;
@@ -600,8 +593,11 @@ void f32_workspace(qlx_model* m, int B) {
   for (int v = 0; v < kNumVars; ++v) nseg += segs_of(v);
   const size_t o_part = take((size_t)nseg * 4);
   const size_t o_loss = take(64);
-  // row lists: kListSlots regions of ceil(G / kListSlots) blocks x ceil(n / G) samples each (G = conv1 blocks), at most frl_cap samples
-  const int frl_cap = C + kListSlots * (C / std::max(1, std::min(C, 2 * num_cus())) + 1) + 2 * num_cus() + kListSlots;
+  // row lists: kListSlots regions of ceil(G / kListSlots) blocks x ceil(n / G) samples each (G = c1_blocks(n) for a chunk of
+  // n <= C samples): kListSlots x that <= (G + kListSlots)(n / G + 1) = n + G + kListSlots n / G + kListSlots, with
+  // G >= min(n, 2 CUs) and G <= max(2 CUs, C / kC1MaxIt + 1)
+  const int frl_cap = C + kListSlots * (C / std::max(1, std::min(C, 2 * num_cus())) + 1) +
+                      std::max(2 * num_cus(), C / kC1MaxIt + 1) + kListSlots;
   const size_t o_rl2 = take((size_t)frl_cap * 81 * 4), o_rl3 = take((size_t)frl_cap * 49 * 4);
   const size_t o_rcnt = take(2 * 2 * kListSlots * kCntStride * 8), o_bgc = take(160 * 4);
   QLX_HIP(hipMalloc(&m->ws, off));
@@ -672,12 +668,18 @@ static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side,
   debug_sync(s, scope);
 }
 
+// CUs of the device (QLX_NUM_CUS overrides it: tests of the grid-shape logic of a part with fewer CUs)
 static int num_cus() {
   static int n = 0;
   if (!n) {
-    int dev = 0;
-    QLX_HIP(hipGetDevice(&dev));
-    QLX_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    const char* e = std::getenv("QLX_NUM_CUS");
+    if (e && atoi(e) > 0) {
+      n = atoi(e);
+    } else {
+      int dev = 0;
+      QLX_HIP(hipGetDevice(&dev));
+      QLX_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    }
   }
   return n;
 }
@@ -698,9 +700,8 @@ static int c1_skip() {
 // a multiple of the CU count, plus the remaining rows as 16 x 64 tiles; 0 when the shape has no such split (fewer whole
 // tiles than CUs, or more than half a tile per CU left over) and the plain grid runs.  At B = 1024 (784 / 1296 whole
 // tiles: 16 left over after 3 / 5 per CU) in place at C3: conv3 forward 42.4 -> 38.4 us, conv2 forward 56.2 -> 53.3 us
-// (`QLX_F32_FWD_BALANCED=0`: the plain 64 x 32 grid).
+// against the plain 64 x 32 grid.
 static int balanced_whole_tiles(int M) {
-  if (std::getenv("QLX_F32_FWD_BALANCED") && std::getenv("QLX_F32_FWD_BALANCED")[0] == '0') return 0;
   const int ncu = num_cus(), t = M / 64, whole = t - t % ncu;
   if (whole < ncu || M - whole * 64 > 32 * ncu) return 0;
   return whole;
@@ -755,7 +756,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     // background rows: conv1 lists them, conv2 / conv3 run the rest (the list counters alternate between forwards)
     const bool lists = bg_rows();
     unsigned long long* cnt = w.frcnt + 2 * kListSlots * kCntStride * w.fparity;
-    const int G = std::min(n, 2 * num_cus());                          // conv1 blocks
+    const int G = c1_blocks(n);                                        // conv1 blocks
     const int per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);   // samples of a list region, at most
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
@@ -767,10 +768,9 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       hipEvent_t ea = nullptr, eb = nullptr;
       if (m->prof) m->prof->ext(sc, 2.0 * n * 400 * 32 * 256, &ea, &eb);
       auto kern = big ? k_conv1_fwd32<1> : k_conv1_fwd32<0>;
-      constexpr int kMaxIt = 64;   // samples per block (flags kept in LDS until the block's lists are written)
-      QLX_CHECK((n + G - 1) / G <= kMaxIt, QLX_E_STATE, "conv1 forward: too many samples per block");
+      QLX_CHECK((n + G - 1) / G <= kC1MaxIt, QLX_E_STATE, "conv1 forward: too many samples per block");
       const size_t lds = 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
-      set_lds_limit((const void*)kern, 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)kMaxIt * 6 * 8);
+      set_lds_limit((const void*)kern, 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)kC1MaxIt * 6 * 8);
       hipExtLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
                             p + voff(0), p + voff(1), w.fa1, c1_skip(), L);
       QLX_HIP(hipGetLastError());
@@ -779,7 +779,6 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     if (lists) {
       // conv2: the non-background rows, the constant rows c2 and c3 in its first block (ConstRows); conv3: the non-background
       // rows (background conv2 taps read from c2), side blocks writing c2 / c3 to the background rows of a2 / a3
-      static const int tile = std::getenv("QLX_F32_BG_TILE") ? atoi(std::getenv("QLX_F32_BG_TILE")) : 0;
       const int nw = std::min(256, std::max(16, n / 16));   // background-row blocks per job
       float* c2 = w.fbgc + 32;
       float* c3 = w.fbgc + 96;
@@ -803,8 +802,8 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
         launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
                2.0 * n * 3136 * 512, s);
       } else {
-        if (tile == 1) run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
-        else run(PConv2FwdL<64, 32, 2, 2>{}, PConv3FwdL<64, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        // (64 x 64 / 32 x 64 / 16 x 64 / 32 x 32 list tiles at B = 1024: within +-1 % of 64 x 32)
+        run(PConv2FwdL<64, 32, 2, 2>{}, PConv3FwdL<64, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
         launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);
       }
@@ -901,47 +900,27 @@ static Adam32Args adam_args(qlx_model* m, float scale) {
   return a;
 }
 
-constexpr int kAdamDenseBlocks = 512;   // blocks of the dense update inside the conv2 pair launch
-
 void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update) {
   ModelWs& w = m->w;
-  // the dense variables' clip norms and Adam beside the conv backward (qnet.h f32_fuse_enabled)
-  const bool fuse = fuse_update && m->f32_fuse_enabled;
-  m->f32_update_mode = fuse ? 1 : (fuse_update && m->f32_tail_enabled ? 2 : 0);
+  m->f32_update_scheduled = fuse_update;
   const NormArgs N = norm_args(m, 1.0f);
-  const NormTail ntail{N, N.seg_first[6], fuse ? N.seg_first[kNumVars] - N.seg_first[6] : 0};
-  const AdamDense adense{adam_args(m, 1.0f), fuse ? kAdamDenseBlocks : 0};
   const float* p = m->d_params;
   float* G = m->d_grads;
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   // algorithmic FLOPs (backward-data + weight gradient of the layer; the pixel-major dgrad tiles multiply only the
   // valid taps, so MFMA work = algorithmic work)
-  // conv3 pixel-major backward data as balanced pixel groups (chained sub-tiles; QLX_F32_PXG=0: one pixel per tile).  conv2
-  // keeps one pixel per tile: grouped, its dgrad ran 71 -> 97 us (scripts/ubench32.hip bwd; its 8-slab sub-tiles pay
-  // the in-loop epilogue's wait on the slab loads in flight, where conv3's 18-slab groups gain: pair 104.6 -> 97.6 us)
-  static const bool pxg = [] { const char* e = std::getenv("QLX_F32_PXG"); return !(e && e[0] == '0'); }();
-  {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
+  // conv3 pixel-major backward data as balanced pixel groups (chained sub-tiles).  conv2 keeps one pixel per tile:
+  // grouped, its dgrad ran 71 -> 97 us (scripts/ubench32.hip bwd; its 8-slab sub-tiles pay the in-loop epilogue's wait on
+  // the slab loads in flight, where conv3's 18-slab groups gain: pair 104.6 -> 97.6 us; one-pixel conv3 tiles 95.4 us)
+  {  // conv3: dz2 pixel-group tiles + weight-gradient chunk tiles
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-    if (pxg) {   // + the dense variables' norm partials as trailing blocks (their gradients are final)
-      PConv3DgradPxG<32, 64, 2, 2> Pd{{Grid{(B + 31) / 32, 1, PConv3DgradPxG<>::GROUPS}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B}};
-      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s, ntail);
-    } else {
-      PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
-      launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s, ntail);
-    }
+    PConv3DgradPxG<32, 64, 2, 2> Pd{{Grid{(B + 31) / 32, 1, PConv3DgradPxG<>::GROUPS}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B}};
+    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
-    static const bool pxg2 = [] { const char* e = std::getenv("QLX_F32_PXG2"); return e && e[0] == '1'; }();
-    if (pxg2) {   // (A/B: conv2 pixel groups too)
-      PConv2DgradPxG<64, 64, 2, 2> Pd{{Grid{(B + 63) / 64, 2, PConv2DgradPxG<>::GROUPS}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B}};
-      if (m->f32_adam_pos == 0) launch_pair(m, Pw, Pd, adense, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
-      else launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s, adense);
-    } else {
-      PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
-      if (m->f32_adam_pos == 0) launch_pair(m, Pw, Pd, adense, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);   // + dense Adam
-      else launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s, adense);
-    }
+    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
+    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
     constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
@@ -960,9 +939,9 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
     const int total = R.count[0] + R.count[1] + R.count[2];
     QLX_CHECK(std::max({z1, z2, z3}) <= kWGroup * kWGroupsMax, QLX_E_INVALID, "too many weight-gradient chunks");
-    // update schedule 2: + the dense variables' clip-norm segment partials (4 per block)
+    // the scheduled update: + the dense variables' clip-norm segment partials (4 per block)
     const int nred = (total + 63) / 64;
-    const int dseg = m->f32_update_mode == 2 ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
+    const int dseg = m->f32_update_scheduled ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
     hipLaunchKernelGGL(k_wreduce32, dim3(nred + (dseg + 3) / 4), dim3(1024), 0, s, R, N, nred, N.seg_first[6], dseg);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_wreduce32");
@@ -970,7 +949,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
 }
 
 void f32_norms(qlx_model* m, hipStream_t s, float scale) {
-  if (m->f32_update_mode != 0) return;   // the backward scheduled them (f32_backward_conv)
+  if (m->f32_update_scheduled) return;   // the backward scheduled them (f32_backward_conv)
   ProfScope ps(m->prof, "f32_norms", s, 4.0 * kNumParams);
   const NormArgs A = norm_args(m, scale);
   hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
@@ -981,24 +960,14 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
 void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const int64_t t = m->iterations + 1;
   const Adam32Args a = adam_args(m, scale);
-  if (m->f32_update_mode == 1) {   // dense variables done beside the conv backward; the six conv variables here
-    QLX_CHECK(scale == 1.0f, QLX_E_STATE, "fused fp32 update with a gradient scale");
-    ProfScope ps(m->prof, "f32_conv_adam", s, 28.0 * kVarOffsetDense);
-    hipLaunchKernelGGL(k_conv_adam32, dim3(conv_adam_blocks()), dim3(1024), 0, s, a, norm_args(m, 1.0f));
-    QLX_HIP(hipGetLastError());
-    debug_sync(s, "k_conv_adam32");
-    m->f32_update_mode = 0;
-    m->iterations = t;
-    return;
-  }
-  if (m->f32_update_mode == 2) {   // every variable in one launch; the dense norm partials came with the reduction
-    QLX_CHECK(scale == 1.0f, QLX_E_STATE, "fp32 update schedule 2 with a gradient scale");
+  if (m->f32_update_scheduled) {   // every variable in one launch; the dense norm partials came with the reduction
+    QLX_CHECK(scale == 1.0f, QLX_E_STATE, "scheduled fp32 update with a gradient scale");
     ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
     const int nconv = conv_adam_blocks(), ndense = (int)((kNumParams - kVarOffsetDense) / 4 / 2048 + 1);   // 2 groups / thread
     hipLaunchKernelGGL(k_update32, dim3(nconv + ndense), dim3(1024), 0, s, a, norm_args(m, 1.0f), nconv, ndense);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_update32");
-    m->f32_update_mode = 0;
+    m->f32_update_scheduled = false;
     m->iterations = t;
     return;
   }

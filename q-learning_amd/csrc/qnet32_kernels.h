@@ -42,33 +42,23 @@ __host__ __device__ constexpr int kmaj_pitch(int rows, int mf) {
 static_assert(kmaj_pitch(32, 16) == 48 && kmaj_pitch(64, 16) == 80 && kmaj_pitch(128, 16) == 144 && kmaj_pitch(64, 32) == 96,
               "KMAJ pitches");
 
-// RMAJ with MF 16 and QLX_Q32_SWZ defined (SWZ): rows with bit 3 set hold their k in the order k ^ 2 (the two k pairs of
-// each float4 swapped).  ds_read_b32 is serviced in two 32-lane groups on 32 banks, (address / 4) mod 32: a fragment
-// read's group is 16 rows x 2 k, and with pitch 36 alone rows i and i + 8 land on one bank (2-way on every read);
-// swapped, the group covers 32 distinct banks with the float4 stores kept 16-byte (a register permutation).  Measured at
-// C3 (round 3): slower - fc1 forward 39.0 -> 43.1 us, conv2 / conv3 forward +1.7 / +1.5 us, 198.6K -> 194.9K env-steps/s -
-// so the read conflicts are not what limits these loops; off by default.
+// (RMAJ pitch 36 leaves ds_read_b32 fragment reads 2-way conflicted: rows i and i + 8 share a bank.  A k-pair swap for rows
+// 8..15 that removes it measured slower at C3 in round 3 - fc1 forward 39.0 -> 43.1 us, 198.6K -> 194.9K env-steps/s.)
 template <int ROWS, bool KMAJ, int MF = 16>
 struct Opnd {
   static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS, MF) : BK + 4;
   static constexpr int FLOATS = KMAJ ? BK * PITCH : ROWS * PITCH;
   static constexpr int F4 = ROWS * BK / 4;   // float4 per slab
   static constexpr int KG = 64 / MF;         // k per MFMA (lane groups)
-#ifdef QLX_Q32_SWZ
-  static constexpr bool SWZ = !KMAJ && MF == 16;
-#else
-  static constexpr bool SWZ = false;
-#endif
   __host__ __device__ static void coord(int idx, int& row, int& k) {
     if (KMAJ) { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
     else { row = idx >> 3; k = (idx & 7) * 4; }
   }
   __device__ static void put(float* t, int row, int k, f32x4 v) {
-    if (SWZ && (row & 8)) v = f32x4{v[2], v[3], v[0], v[1]};
     *reinterpret_cast<f32x4*>(t + (KMAJ ? k * PITCH + row : row * PITCH + k)) = v;
   }
   __device__ static float at(const float* t, int row, int k) {
-    return KMAJ ? t[k * PITCH + row] : t[row * PITCH + (SWZ ? (k ^ ((row & 8) >> 2)) : k)];
+    return KMAJ ? t[k * PITCH + row] : t[row * PITCH + k];
   }
   // MFMA operand of the MF rows from r0, k step kk: lane l holds (r0 + l % MF, KG kk + l / MF)
   __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & (MF - 1)), KG * kk + lane / MF); }
@@ -165,10 +155,8 @@ struct ACtxOf<P, true> { using type = typename P::ACtx; };
 // epilogue waits on nothing (a load issued after the loop would wait behind every slab load still in flight).
 template <class P, class = void>
 struct HasEpiPre : std::false_type {};
-#ifndef QLX_Q32_NO_EPIPRE   // (A/B builds: epilogue loads after the loop)
 template <class P>
 struct HasEpiPre<P, std::void_t<decltype(std::declval<const P&>().epi_pre(0, 0, 0))>> : std::true_type {};
-#endif
 // the type epi_pre returns (f32x4 unless the policy says otherwise)
 template <class P, bool = HasEpiPre<P>::value>
 struct PreOf { using type = f32x4; };
@@ -389,6 +377,19 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
 // backward data: 1..9 valid taps) this removes the per-tile pipeline ramp and epilogue wait that dominate a short tile.
 // The sub-tile queue is kept as shifting scalars (no runtime-indexed arrays or captured references: those end up in
 // scratch memory): a load cursor and an epilogue cursor each advance through (z_i, end slab e_i) in order.
+// (gemm_body_chain) the streams type of a policy, or an empty placeholder
+template <class P, class = void>
+struct HasStreamsC : std::false_type {};
+template <class P>
+struct HasStreamsC<P, std::void_t<typename P::Streams>> : std::bool_constant<!std::is_void_v<typename P::Streams>> {};
+struct NoStreams { struct Regs {}; };
+template <class P, bool = HasStreamsC<P>::value>
+struct StreamsOf { using type = NoStreams; };
+template <class P>
+struct StreamsOf<P, true> { using type = typename P::Streams; };
+template <class P>
+struct StreamsRegsOf { using type = typename StreamsOf<P>::type::Regs; };
+
 struct ChainQ {
   int z0, e0, z1, e1, z2, e2, z3, e3;
   __device__ __forceinline__ void pop() { z0 = z1; e0 = e1; z1 = z2; e1 = e2; z2 = z3; e2 = e3; }
@@ -427,52 +428,67 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
   float* Bs1 = Bs0 + OB::FLOATS;
-  f32x4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
+  // slab staging: the policy's streams (lane offsets per block; a sub-tile's slab offsets on the scalar unit) or ldA / ldB
+  constexpr bool STR = HasStreamsC<P>::value;
+  using St = typename StreamsOf<P>::type;
+  St st{};
+  if constexpr (STR) st = p.streams(0, row0, col0, tid);
+  struct RegsL { f32x4 a[NA], b[NB]; };
+  using Regs = std::conditional_t<STR, typename StreamsRegsOf<P>::type, RegsL>;
+  Regs x0, x1;
   // slab s of the concatenation (s never decreases between calls; past the end the last slab again)
-  auto load = [&](int s, f32x4(&ra)[NA], f32x4(&rb)[NB]) {
+  auto load = [&](int s, Regs& x) {
     if (s >= lq.e0 && s < ns) {
       lbase = lq.e0;
       lq.pop();
     }
     const int z = lq.z0, sl = s - lbase;
+    if constexpr (STR) {
+      st.load_z(z, sl, x);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * T;
-      if (OA::F4 % T == 0 || idx < OA::F4) {
-        int r, k;
-        OA::coord(idx, r, k);
-        ra[i] = p.ldA(z, sl, row0 + r, k);
+      for (int i = 0; i < NA; ++i) {
+        const int idx = tid + i * T;
+        if (OA::F4 % T == 0 || idx < OA::F4) {
+          int r, k;
+          OA::coord(idx, r, k);
+          x.a[i] = p.ldA(z, sl, row0 + r, k);
+        }
       }
-    }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + i * T;
-      if (OB::F4 % T == 0 || idx < OB::F4) {
-        int r, k;
-        OB::coord(idx, r, k);
-        rb[i] = p.ldB(z, sl, col0 + r, k);
+      for (int i = 0; i < NB; ++i) {
+        const int idx = tid + i * T;
+        if (OB::F4 % T == 0 || idx < OB::F4) {
+          int r, k;
+          OB::coord(idx, r, k);
+          x.b[i] = p.ldB(z, sl, col0 + r, k);
+        }
       }
     }
   };
-  auto store = [&](int s, const f32x4(&ra)[NA], const f32x4(&rb)[NB]) {
+  auto store = [&](int s, const Regs& x) {
     float* as = (s & 1) ? As1 : As0;
     float* bs = (s & 1) ? Bs1 : Bs0;
+    if constexpr (STR) {
+      st.store(as, bs, x);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * T;
-      if (OA::F4 % T == 0 || idx < OA::F4) {
-        int r, k;
-        OA::coord(idx, r, k);
-        OA::put(as, r, k, ra[i]);
+      for (int i = 0; i < NA; ++i) {
+        const int idx = tid + i * T;
+        if (OA::F4 % T == 0 || idx < OA::F4) {
+          int r, k;
+          OA::coord(idx, r, k);
+          OA::put(as, r, k, x.a[i]);
+        }
       }
-    }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + i * T;
-      if (OB::F4 % T == 0 || idx < OB::F4) {
-        int r, k;
-        OB::coord(idx, r, k);
-        OB::put(bs, r, k, rb[i]);
+      for (int i = 0; i < NB; ++i) {
+        const int idx = tid + i * T;
+        if (OB::F4 % T == 0 || idx < OB::F4) {
+          int r, k;
+          OB::coord(idx, r, k);
+          OB::put(bs, r, k, x.b[i]);
+        }
       }
     }
   };
@@ -525,23 +541,23 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
     fq.pop();
     if (s + 1 < ns) fetch_pre(fq.z0);
   };
-  auto iter = [&](int s, f32x4(&xa)[NA], f32x4(&xb)[NB], f32x4(&ya)[NA], f32x4(&yb)[NB]) {
-    load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
+  auto iter = [&](int s, Regs& xs, Regs& ys) {
+    load(s + 2 < ns ? s + 2 : ns - 1, ys);
     if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);
     compute(s);
     flush(s);
-    if (s + 1 < ns) store(s + 1, xa, xb);
+    if (s + 1 < ns) store(s + 1, xs);
     lds_barrier();
   };
   fetch_pre(q.z0);
   if (ns > 0) {
-    load(0, ra1, rb1);
-    store(0, ra1, rb1);
-    load(ns > 1 ? 1 : 0, ra0, rb0);
+    load(0, x1);
+    store(0, x1);
+    load(ns > 1 ? 1 : 0, x0);
     lds_barrier();
     for (int s = 0; s < ns; s += 2) {
-      iter(s, ra0, rb0, ra1, rb1);
-      if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
+      iter(s, x0, x1);
+      if (s + 1 < ns) iter(s + 1, x1, x0);
     }
   }
 }
@@ -572,6 +588,261 @@ struct Grid {
   __host__ __device__ int blocks() const { return tiles_m * tiles_n * nz; }
 };
 
+// ---------------------------------------------------------------------------------------------------------------
+// Operand streams: slab staging with no per-slab vector address arithmetic.
+//
+// On gfx950 the fp32 MFMA and the VALU do not overlap: an MFMA loop and a VALU loop on one SIMD take the sum of their
+// times (scripts/coexec_probe.hip), so every vector instruction of a slab loop is MFMA time lost.  The ldA / ldB form of
+// the policies recomputes each load's 64-bit address per slab (divisions, masks, selects: 40 to 100 VALU instructions per
+// slab of 32 MFMAs).  A stream computes its per-lane byte offsets once per tile; per slab it adds a wave-uniform offset
+// (SALU) and issues raw buffer loads, whose range check returns zeros for a lane offset past the buffer (rows past the
+// batch) or for a whole-slab descriptor of zero records (gather rows past a chunk).
+//   load(s, regs)  - issue the slab's loads (s wave-uniform)
+//   store(t, regs) - write them into the operand's LDS image t (the Opnd layout the fragment reads use)
+constexpr uint32_t kOob = 0x80000000u;   // lane offset past any buffer: the load returns zeros
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  // descriptor words from provably wave-uniform inputs (otherwise each load is wrapped in a waterfall loop)
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ float buf_ld1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// Affine stream over an Opnd<ROWS, KMAJ> image: element (row, k) of slab s at lane_off(row, k) + slab_off(s) bytes.
+// RMAJ: k runs along memory (16-byte chunks of 4 k), KMAJ: rows run along memory (chunks of 4 rows).  KMASK: lanes whose
+// k is at or past the slab's valid count read zeros (a partial last slab of a reduction along k).
+template <int ROWS, bool KMAJ, int T, bool KMASK = false>
+struct AffineStream {
+  using O = Opnd<ROWS, KMAJ, 16>;
+  static constexpr int N = (O::F4 + T - 1) / T;
+  using Regs = f32x4[N];
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t vo[N];
+  int kk[N];        // (KMASK) the lane's k of each load
+  int tid;
+  template <class F>
+  __device__ void init(const void* base, uint32_t bytes, int tid_, F lane_off) {
+    rs = buf_rsrc(base, bytes);
+    tid = tid_;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = tid + i * T;
+      int r = 0, k = 0;
+      if (O::F4 % T == 0 || idx < O::F4) O::coord(idx, r, k);
+      vo[i] = lane_off(r, k);
+      kk[i] = k;
+    }
+  }
+  // slab s at byte offset soff (wave-uniform); kvalid: k < kvalid are live (KMASK)
+  __device__ void load(uint32_t soff, int kvalid, Regs& rg) const {
+    if (!KMASK || kvalid >= BK) {   // (wave-uniform: the masked form only in a partial last slab)
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (O::F4 % T == 0 || tid + i * T < O::F4) rg[i] = buf_ld4(rs, vo[i], soff);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (O::F4 % T == 0 || tid + i * T < O::F4) rg[i] = buf_ld4(rs, kk[i] < kvalid ? vo[i] : kOob, soff);
+    }
+  }
+  __device__ void store(float* t, const Regs& rg) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = tid + i * T;
+      if (O::F4 % T == 0 || idx < O::F4) {
+        int r, k;
+        O::coord(idx, r, k);
+        O::put(t, r, k, rg[i]);
+      }
+    }
+  }
+};
+
+// Gather stream for a KMAJ image whose k (the reduction index) is not affine in memory (the conv weight gradient's im2col
+// operand: k = (b, oh, ow)).  Each wave instruction loads one k for all ROWS = 64 rows (a dword per lane, row = lane), so
+// the k's byte offset is wave-uniform: the policy's kofs(k) is evaluated on the scalar unit, and a k past the valid count
+// reads through a zero-record descriptor.  Wave w of the tile stages k = w * (32 / W) + j, j < 32 / W.
+template <int T>
+struct GatherKStream {
+  static constexpr int W = T / 64, NJ = BK / W;
+  using O = Opnd<64, true, 16>;
+  using Regs = float[NJ];
+  __amdgpu_buffer_rsrc_t rs, rz;
+  uint32_t vo;   // the lane's row offset
+  int lane, k0;
+  __device__ void init(const void* base, uint32_t bytes, int tid, uint32_t row_off) {
+    rs = buf_rsrc(base, bytes);
+    rz = buf_rsrc(base, 0u);
+    lane = tid & 63;
+    k0 = __builtin_amdgcn_readfirstlane(tid >> 6) * NJ;
+    vo = row_off;
+  }
+  // kofs(k): byte offset of reduction index k (slab-relative k0 + j, absolute k = kbase + k0 + j)
+  // ofs[j]: byte offset of this wave's k = kbase + k0 + j (wave-uniform, from the policy's generator)
+  __device__ void load(const uint32_t (&ofs)[NJ], int kvalid, Regs& rg) const {
+    if (kvalid >= BK) {   // (wave-uniform: the masked form only in a partial last slab)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) rg[j] = buf_ld1(rs, vo, ofs[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bool live = k0 + j < kvalid;
+        rg[j] = buf_ld1(live ? rs : rz, vo, live ? ofs[j] : 0u);
+      }
+    }
+  }
+  __device__ void store(float* t, const Regs& rg) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) t[(k0 + j) * O::PITCH + lane] = rg[j];
+  }
+};
+
+// Two affine streams (A, B) whose slab offsets are s * the policies' per-slab strides
+template <class SA, class SB, uint32_t DA, uint32_t DB, bool KMASK = false>
+struct PairStreams {
+  SA a;
+  SB b;
+  int kmax;   // (KMASK) the reduction length: slab s has kmax - s * BK live k
+  struct Regs {
+    typename SA::Regs a;
+    typename SB::Regs b;
+  };
+  __device__ void load(int s, Regs& x) const {
+    const int kv = kmax - s * BK;
+    a.load((uint32_t)s * DA, kv, x.a);
+    b.load((uint32_t)s * DB, kv, x.b);
+  }
+  __device__ void store(float* as, float* bs, const Regs& x) const {
+    a.store(as, x.a);
+    b.store(bs, x.b);
+  }
+};
+
+// Stream form of gemm_body (policies with a member type Streams): the same pipeline, fragments, MFMA chains, bias chains
+// and epilogue, with the slab staging done by the policy's streams:
+//   typename P::Streams st = p.streams(z, row0, col0, tid);   per tile
+//   st.load(s, x) / st.store(s, x, As, Bs)                    x: a P::Streams::Regs register set
+template <class P, class = void>
+struct HasStreams : std::false_type {};
+template <class P>
+struct HasStreams<P, std::void_t<typename P::Streams>> : std::bool_constant<!std::is_void_v<typename P::Streams>> {};
+
+template <class P>
+__device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
+  constexpr int MF = 16;
+  using OA = Opnd<P::BM, P::A_KMAJ, MF>;
+  using OB = Opnd<P::BN, P::B_KMAJ, MF>;
+  using Acc = f32x4;
+  constexpr int T = P::WM * P::WN * 64;
+  constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
+  static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
+  using St = typename P::Streams;
+  using Regs = typename St::Regs;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % P::WM, wn = wave / P::WM;
+  int tm, tn, z;
+  p.decode(lb, tm, tn, z);
+  const int row0 = tm * P::BM, col0 = tn * P::BN;
+  const int ns = p.nslabs(z);
+  const St st = p.streams(z, row0, col0, tid);
+  float* As0 = lds;
+  float* As1 = lds + OA::FLOATS;
+  float* Bs0 = lds + 2 * OA::FLOATS;
+  float* Bs1 = Bs0 + OB::FLOATS;
+  Regs x0, x1;
+  Acc acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  float bsum[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bsum[j] = 0.0f;
+  // the bias chains run in the waves that own them only: the slab loop is compiled twice (a runtime test per k step
+  // keeps the B fragments' registers and the adds in every wave's loop)
+  const bool do_bias = P::BIAS && tm == 0 && wm == 0;
+  auto slab_loop = [&](auto bias_tag) {
+    constexpr bool DB = decltype(bias_tag)::value;
+    auto compute = [&](int s) {
+      const float* a = (s & 1) ? As1 : As0;
+      const float* b = (s & 1) ? Bs1 : Bs0;
+      if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
+#pragma unroll
+      for (int kk = 0; kk < BK / OA::KG; ++kk) {
+        float af[TM], bf[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
+        if constexpr (DB)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bsum[j] = __fadd_rn(bsum[j], bf[j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    auto iter = [&](int s, Regs& xs, Regs& ys) {
+      st.load(s + 2 < ns ? s + 2 : ns - 1, ys);
+      if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);
+      compute(s);
+      if (s + 1 < ns) st.store((s + 1) & 1 ? As1 : As0, (s + 1) & 1 ? Bs1 : Bs0, xs);
+      lds_barrier();
+    };
+    if (ns > 0) {
+      st.load(0, x1);
+      st.store(As0, Bs0, x1);
+      st.load(ns > 1 ? 1 : 0, x0);
+      lds_barrier();
+      for (int s = 0; s < ns; s += 2) {
+        iter(s, x0, x1);
+        if (s + 1 < ns) iter(s + 1, x1, x0);
+      }
+    }
+  };
+  constexpr bool PRE = HasEpiPre<P>::value;
+  typename PreOf<P>::type pre[TM][TN];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+  }
+  if constexpr (P::BIAS) {
+    if (do_bias) slab_loop(std::true_type{});
+    else slab_loop(std::false_type{});
+  } else {
+    slab_loop(std::false_type{});
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col = col0 + (wn * TN + j) * 16 + (lane & 15);
+      if constexpr (PRE) p.epi_post(z, row, col, acc[i][j], pre[i][j]);
+      else p.epi(z, row, col, acc[i][j]);
+    }
+  if constexpr (P::BIAS) {
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float c1 = __shfl(bsum[j], lane + 16), c2 = __shfl(bsum[j], lane + 32), c3 = __shfl(bsum[j], lane + 48);
+        if (lane < 16) p.epi_bias(z, col0 + (wn * TN + j) * 16 + lane, __fadd_rn(__fadd_rn(__fadd_rn(bsum[j], c1), c2), c3));
+      }
+    }
+  }
+}
+
 // a policy with NSUB (chained sub-tiles per block) runs gemm_body_chain
 template <class P, class = void>
 struct HasChain : std::false_type {};
@@ -580,6 +851,7 @@ struct HasChain<P, std::void_t<decltype(P::NSUB)>> : std::true_type {};
 template <class P>
 __device__ __forceinline__ void body(const P& p, int lb, float* lds) {
   if constexpr (HasChain<P>::value) gemm_body_chain(p, lb, lds);
+  else if constexpr (HasStreams<P>::value) gemm_body_s(p, lb, lds);
   else gemm_body(p, lb, lds);
 }
 
@@ -862,6 +1134,21 @@ struct PFc1FwdT {
     for (int r = 0; r < 4; ++r)
       if (row + r < M) a4[(size_t)(row + r) * 512 + col] = relu(v[r] + b[r]);
   }
+  // streams (gemm_body_s; MF 16): a3 rows (rows past M read zeros), W3 k rows
+  static constexpr int T = WM_ * WN_ * 64;
+  using SA = AffineStream<BM_, false, T>;
+  using SB = AffineStream<BN_, true, T>;
+  using Streams = std::conditional_t<MF_ == 16, PairStreams<SA, SB, BK * 4u, BK * 512u * 4u>, void>;
+  template <class S = Streams>
+  __device__ S streams(int, int row0, int col0, int tid) const {
+    S st;
+    const int m = M;
+    st.a.init(a3, (uint32_t)M * 3136u * 4u, tid,
+              [row0, m](int r, int k) { return row0 + r < m ? (uint32_t)((row0 + r) * 3136 + k) * 4u : kOob; });
+    st.b.init(w3, 3136u * 512u * 4u, tid, [col0](int r, int k) { return (uint32_t)(k * 512 + col0 + r) * 4u; });
+    st.kmax = 3136;
+    return st;
+  }
 };
 using PFc1Fwd = PFc1FwdT<>;
 // chunk-size batches: 64 x 64 tiles on v_mfma_f32_32x32x2_f32 (scripts/ubench32.hip at B = 8192: 231 vs 247 us)
@@ -905,6 +1192,21 @@ struct PFc1DgradT {
     for (int r = 0; r < 4; ++r)
       if (row + r < M) dz3[(size_t)(row + r) * 3136 + col] = m[r] > 0.0f ? v[r] : 0.0f;
   }
+  // streams (gemm_body_s): dz4 rows (rows past M read zeros), W3 rows (k = n contiguous)
+  static constexpr int T = WM_ * WN_ * 64;
+  using SA = AffineStream<BM_, false, T>;
+  using SB = AffineStream<BN_, false, T>;
+  using Streams = std::conditional_t<MF_ == 16, PairStreams<SA, SB, BK * 4u, BK * 4u>, void>;
+  template <class S = Streams>
+  __device__ S streams(int, int row0, int col0, int tid) const {
+    S st;
+    const int m = M;
+    st.a.init(dz4, (uint32_t)M * 512u * 4u, tid,
+              [row0, m](int r, int k) { return row0 + r < m ? (uint32_t)((row0 + r) * 512 + k) * 4u : kOob; });
+    st.b.init(w3, 3136u * 512u * 4u, tid, [col0](int r, int k) { return (uint32_t)((col0 + r) * 512 + k) * 4u; });
+    st.kmax = 512;
+    return st;
+  }
 };
 using PFc1Dgrad = PFc1DgradT<>;
 using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
@@ -937,6 +1239,19 @@ struct PFc1WgradT {
       if (row + r < 3136) dw3[(size_t)(row + r) * 512 + col] = v[r];
   }
   __device__ void epi_bias(int, int col, float v) const { db3[col] = v; }
+  // streams (gemm_body_s): a3 and dz4 rows of the slab's samples (k = b; samples past B read zeros)
+  static constexpr int T = WM_ * WN_ * 64;
+  using SA = AffineStream<BM_, true, T, true>;
+  using SB = AffineStream<BN_, true, T, true>;
+  using Streams = std::conditional_t<MF_ == 16, PairStreams<SA, SB, BK * 3136u * 4u, BK * 512u * 4u, true>, void>;
+  template <class S = Streams>
+  __device__ S streams(int, int row0, int col0, int tid) const {
+    S st;
+    st.a.init(a3, (uint32_t)B * 3136u * 4u, tid, [row0](int r, int k) { return (uint32_t)(k * 3136 + row0 + r) * 4u; });
+    st.b.init(dz4, (uint32_t)B * 512u * 4u, tid, [col0](int r, int k) { return (uint32_t)(k * 512 + col0 + r) * 4u; });
+    st.kmax = B;
+    return st;
+  }
 };
 using PFc1Wgrad = PFc1WgradT<>;
 // training batch: 64 x 64 tiles (392 + the fc1 backward-data tiles; in place at C3: 68.6 -> 65.1 us per fc1 backward
@@ -1048,6 +1363,38 @@ struct PConv3DgradPx {
     for (int r = 0; r < 4; ++r)
       if (row + r < B) dz2[((size_t)((row + r) * 9 + q.ih) * 9 + q.iw) * 64 + col] = m[r] > 0.0f ? v[r] : 0.0f;
   }
+  // streams (gemm_body_s, gemm_body_chain): dz3 rows of the tile's samples (rows past B read zeros), W2 rows of the tile's
+  // channels; a slab's pixel tap (kh, kw) and oc half are wave-uniform offsets (per sub-tile z in a chained group)
+  static constexpr int T = WM_ * WN_ * 64;
+  struct Streams {
+    AffineStream<BM_, false, T> a;
+    AffineStream<BN_, false, T> b;
+    struct Regs {
+      typename AffineStream<BM_, false, T>::Regs a;
+      typename AffineStream<BN_, false, T>::Regs b;
+    };
+    int z0;   // (gemm_body_s: the tile's pixel)
+    __device__ void load(int s, Regs& x) const { load_z(z0, s, x); }
+    __device__ void load_z(int z, int s, Regs& x) const {
+      const Px q = px(z);
+      const int t = s >> 1, kh = q.kh0 + t / q.nkw, kw = q.kw0 + t % q.nkw, h = (s & 1) * 32;
+      a.load((uint32_t)(((q.ih - kh) * 7 + q.iw - kw) * 64 + h) * 4u, 0, x.a);
+      b.load((uint32_t)((kh * 3 + kw) * 4096 + h) * 4u, 0, x.b);
+    }
+    __device__ void store(float* as, float* bs, const Regs& x) const {
+      a.store(as, x.a);
+      b.store(bs, x.b);
+    }
+  };
+  __device__ Streams streams(int z, int row0, int col0, int tid) const {
+    Streams st;
+    st.z0 = z;
+    const int nb = B;
+    st.a.init(dz3, (uint32_t)B * 3136u * 4u, tid,
+              [row0, nb](int r, int k) { return row0 + r < nb ? (uint32_t)((row0 + r) * 3136 + k) * 4u : kOob; });
+    st.b.init(w2, 9u * 4096u * 4u, tid, [col0](int r, int k) { return (uint32_t)((col0 + r) * 64 + k) * 4u; });
+    return st;
+  }
 };
 
 // conv2 backward-data, pixel-major over the class grid: z = (i, j) of 10 x 10; rows b; cols (py, px, c) = 128 (the four
@@ -1114,6 +1461,39 @@ struct PConv2DgradPx {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (row + r < B) dz1[((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31)] = m[r] > 0.0f ? v[r] : 0.0f;
+  }
+  // streams (gemm_body_s): A = dz2 rows of the tile's samples (rows past B read zeros), B = W1 rows of the tile's class
+  // channels; a slab's tap (th, tw) and oc half are wave-uniform offsets
+  static constexpr int T = WM_ * WN_ * 64;
+  struct Streams {
+    AffineStream<BM_, false, T> a;
+    AffineStream<BN_, false, T> b;
+    Px q;
+    struct Regs {
+      typename AffineStream<BM_, false, T>::Regs a;
+      typename AffineStream<BN_, false, T>::Regs b;
+    };
+    __device__ void load(int s, Regs& x) const {
+      const int t = s >> 1, th = q.th0 + t / q.ntw, tw = q.tw0 + t % q.ntw, h = (s & 1) * 32;
+      a.load((uint32_t)(((q.i - th) * 9 + q.j - tw) * 64 + h) * 4u, 0, x.a);
+      b.load((uint32_t)((8 * th + 2 * tw) * 2048 + h) * 4u, 0, x.b);
+    }
+    __device__ void store(float* as, float* bs, const Regs& x) const {
+      a.store(as, x.a);
+      b.store(bs, x.b);
+    }
+  };
+  __device__ Streams streams(int z, int row0, int col0, int tid) const {
+    Streams st;
+    st.q = px(z);
+    const int nb = B;
+    st.a.init(dz2, (uint32_t)B * 5184u * 4u, tid,
+              [row0, nb](int r, int k) { return row0 + r < nb ? (uint32_t)((row0 + r) * 5184 + k) * 4u : kOob; });
+    st.b.init(w1, 16u * 32u * 64u * 4u, tid, [col0](int r, int k) {
+      const int col = col0 + r, cls = col >> 5;
+      return (uint32_t)((((cls >> 1) * 4 + (cls & 1)) * 32 + (col & 31)) * 64 + k) * 4u;
+    });
+    return st;
   }
 };
 
@@ -1284,6 +1664,57 @@ struct PConvWgrad {
     for (int r = 0; r < 4; ++r) slab[((size_t)z * (MROWS + 1) + row + r) * OC + col] = v[r];
   }
   __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * OC + col] = v; }
+  // streams (gemm_body_s): A = the im2col rows gathered one reduction index r = (b, oh, ow) per wave instruction (its
+  // offset on the scalar unit), B = dz rows, affine in r; r past the chunk reads zeros
+  static constexpr int T = WM_ * WN_ * 64;
+  struct Streams {
+    GatherKStream<T> a;
+    AffineStream<BN_, true, T, true> b;
+    int z, rows;
+    struct Regs {
+      typename GatherKStream<T>::Regs a;
+      typename AffineStream<BN_, true, T, true>::Regs b;
+    };
+    __device__ void load(int s, Regs& x) const {
+      const int kbase = s * BK, kvalid = rows - kbase;
+      // the wave's NJ consecutive r = (b, oh, ow): the first by division, the rest by carries (all scalar)
+      constexpr int NJ = GatherKStream<T>::NJ;
+      const int r0 = kbase + a.k0, bl = r0 / P, pp = r0 - bl * P;
+      int oh = pp / OW, ow = pp - oh * OW;
+      uint32_t o = (uint32_t)((((z * SC + bl) * H + oh * S) * W + ow * S) * C) * 4u;
+      uint32_t ofs[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        ofs[j] = o;
+        o += S * C * 4u;
+        if (++ow == OW) {
+          ow = 0;
+          o += (uint32_t)(S * W * C - OW * S * C) * 4u;
+          if (++oh == OH) {
+            oh = 0;
+            o += (uint32_t)(H * W * C - OH * S * W * C) * 4u;
+          }
+        }
+      }
+      a.load(ofs, kvalid, x.a);
+      b.load((uint32_t)kbase * OC * 4u, kvalid, x.b);
+    }
+    __device__ void store(float* as, float* bs, const Regs& x) const {
+      a.store(as, x.a);
+      b.store(bs, x.b);
+    }
+  };
+  __device__ Streams streams(int z, int row0, int col0, int tid) const {
+    static_assert(BM_ == 64 && MF_ == 16, "gather stream: 64-row tiles");
+    Streams st;
+    st.z = z;
+    st.rows = rows_in(z);
+    const int m = row0 + (tid & 63), tap = m / C, c = m - tap * C, kh = tap / KS, kw = tap - kh * KS;
+    st.a.init(in, (uint32_t)B * H * W * C * 4u, tid, (uint32_t)((kh * W + kw) * C + c) * 4u);
+    st.b.init(dz + (size_t)z * SC * P * OC, (uint32_t)st.rows * OC * 4u, tid,
+              [col0](int r, int k) { return (uint32_t)(k * OC + col0 + r) * 4u; });
+    return st;
+  }
 };
 
 // dW4[k][n] = fmaf chain over b of a4[b][k] dq[b][n]; db4[n] = sum over b of dq[b][n]; loss = (sum over b of h_b) / B.

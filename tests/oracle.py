@@ -62,7 +62,8 @@ def default_params(**kw):
                       epsilon_pure_random_steps=50_000, history_buffer_len=1_000_000, update_after_actions=4,
                       target_sync_steps=0, episode_reward_history_buffer_len=100, n_envs=1, batch_size=32,
                       env_seed=0x51A5EED, learner_seed=1, init_seed=2, rank=0, flags=0, per_alpha=0.6,
-                      per_beta=0.4, per_eps=1e-6, qnet_precision=0, stats_after_steps=25_000, checkpoint_file=b"")
+                      per_beta=0.4, per_eps=1e-6, qnet_precision=0, stats_after_steps=25_000, checkpoint_file=b"",
+                      episode_reward_goal=float("nan"))
     for k, v in kw.items():
         if k == "checkpoint_file" and isinstance(v, str):
             v = v.encode()

@@ -65,26 +65,6 @@ def test_f32_pure_random_phase_bit_exact():
     assert sg["running_reward"] == sr["running_reward"] and sg["epsilon"] == sr["epsilon"]
 
 
-@pytest.mark.parametrize("pos", ["0", "1"])
-def test_f32_fused_update_schedule_bit_exact(monkeypatch, pos):
-    """The opt-in update schedule (QLX_F32_FUSED_ADAM=1: dense clip norms / Adam inside the conv backward launches as
-    leading (0) or trailing (1) blocks, the conv variables' in k_conv_adam32) is the same arithmetic: bit-exact against the
-    oracle over many updates, weights and Adam slots included."""
-    monkeypatch.setenv("QLX_F32_FUSED_ADAM", "1")
-    monkeypatch.setenv("QLX_F32_ADAM_POS", pos)
-    N, B = 16, 64
-    gpu, ref = make(N, B, max_steps_per_episode=45, update_after_actions=8)
-    n_updates = 0
-    for v in range(24):
-        gpu.vector_step()
-        ref.vector_step()
-        g, r = gpu.last(), ref.last()
-        assert_step_equal(g, r, v)
-        n_updates += len(r["losses"])
-    assert n_updates >= 30
-    assert_models_equal(gpu.model, ref.qnet(0))
-
-
 def test_f32_greedy_phase_bit_exact():
     """Greedy acting from the online net while it learns: the acting forward, argmax, every update and the
     resulting trajectories stay identical (epsilon 0.3 -> 0.05 over the run, one update per 16 env-steps)."""

@@ -1,9 +1,9 @@
 """The fp32 Q-net's A/B code paths are bit-exact too, not only the default one.
 
-Every switch the measurements in DESIGN.md §4.1 used is kept in the product as an exact alternative: the dense conv2 /
-conv3 forward (QLX_F32_BG=0), conv1 issuing its all-zero frame steps (QLX_F32_C1_SKIP=0), one-pixel conv3 backward-data
-tiles (QLX_F32_PXG=0), grouped conv2 backward-data tiles (QLX_F32_PXG2=1), 64 x 64 list tiles at the training batch
-(QLX_F32_BG_TILE=1), the plain forward grids (QLX_F32_FWD_BALANCED=0) and the three-launch update tail (QLX_F32_TAIL=0).
+The switches kept in the product (they have reporting roles: the bench's dense-frame figure) are exact alternatives:
+the dense conv2 / conv3 forward without background rows (QLX_F32_BG=0) and conv1 issuing its all-zero frame steps
+(QLX_F32_C1_SKIP=0), alone and together; and the grid shapes of a part with few CUs (QLX_NUM_CUS=8: a CPX partition
+of an MI300X / MI355X - conv1 then runs more than two blocks per CU so that no block holds more than 64 samples).
 Each must give the oracle's bits (oracle/qnet32_ref.cpp, the same chains as tests/test_gpu_qnet32.py): Q values and the
 conv2 / conv3 activations of a 1,024-sample forward, Q of a 3,000-sample (chunk-size kernels) forward, and one training
 step at B = 1,024 (loss, all ten gradients, the clip norms, w / m / v after Adam).
@@ -90,14 +90,13 @@ def case(tmp_path_factory):
     return d, inp, exp
 
 
-@pytest.mark.parametrize("env", [{}, {"QLX_F32_BG": "0"}, {"QLX_F32_C1_SKIP": "0"}, {"QLX_F32_PXG": "0"},
-                                 {"QLX_F32_PXG2": "1"}, {"QLX_F32_BG_TILE": "1"}, {"QLX_F32_FWD_BALANCED": "0"},
-                                 {"QLX_F32_TAIL": "0"}],
+@pytest.mark.parametrize("env", [{}, {"QLX_F32_BG": "0"}, {"QLX_F32_C1_SKIP": "0"},
+                                 {"QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"}, {"QLX_NUM_CUS": "8"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "default")
 def test_path_bit_exact(case, env):
     d, inp, exp = case
     out = str(d / ("out_" + ("_".join(f"{k}{v}" for k, v in env.items()) or "default") + ".npz"))
-    cenv = {k: v for k, v in os.environ.items() if not k.startswith("QLX_F32_")}
+    cenv = {k: v for k, v in os.environ.items() if not k.startswith("QLX_F32_") and k != "QLX_NUM_CUS"}
     cenv.update(env)
     r = subprocess.run([sys.executable, "-c", CHILD, inp, out, ROOT], env=cenv, capture_output=True, text=True,
                        timeout=240)
