@@ -909,12 +909,12 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   // algorithmic FLOPs (backward-data + weight gradient of the layer; the pixel-major dgrad tiles multiply only the
   // valid taps, so MFMA work = algorithmic work)
-  // conv3 pixel-major backward data as balanced pixel groups (chained sub-tiles).  conv2 keeps one pixel per tile:
-  // grouped, its dgrad ran 71 -> 97 us (scripts/ubench32.hip bwd; its 8-slab sub-tiles pay the in-loop epilogue's wait on
-  // the slab loads in flight, where conv3's 18-slab groups gain: pair 104.6 -> 97.6 us; one-pixel conv3 tiles 95.4 us)
-  {  // conv3: dz2 pixel-group tiles + weight-gradient chunk tiles
+  // pixel-major backward data, one pixel per tile.  On the operand-stream core (no per-slab address arithmetic) the
+  // one-pixel conv3 tiles beat the balanced pixel groups (chained sub-tiles: scripts/ubench32.hip bwd, B = 1024: pair 84.4
+  // vs 93.4 us; on the ldA / ldB core the groups had won, 97.1 vs 105.6 us); conv2 groups were slower on both cores
+  {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-    PConv3DgradPxG<32, 64, 2, 2> Pd{{Grid{(B + 31) / 32, 1, PConv3DgradPxG<>::GROUPS}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B}};
+    PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles

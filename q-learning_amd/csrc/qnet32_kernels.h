@@ -380,8 +380,10 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
 // (gemm_body_chain) the streams type of a policy, or an empty placeholder
 template <class P, class = void>
 struct HasStreamsC : std::false_type {};
+#ifndef QLX_Q32_NO_STREAMS
 template <class P>
 struct HasStreamsC<P, std::void_t<typename P::Streams>> : std::bool_constant<!std::is_void_v<typename P::Streams>> {};
+#endif
 struct NoStreams { struct Regs {}; };
 template <class P, bool = HasStreamsC<P>::value>
 struct StreamsOf { using type = NoStreams; };
@@ -725,14 +727,51 @@ struct PairStreams {
   }
 };
 
+// Gather stream, 16-byte form: a thread stages 4 consecutive rows (a float4) of one k; the 64 lanes of a wave instruction
+// cover 4 consecutive k (16 lanes each), whose wave-uniform offsets (computed on the scalar unit) the lane picks by its
+// group lane / 16 (3 selects per load).  Wave w stages k = 4 w + g and 16 + 4 w + g.  A k past the valid count reads zeros.
+template <int T>
+struct GatherK4Stream {
+  static_assert(T == 256, "gather stream: four waves");
+  using O = Opnd<64, true, 16>;
+  static constexpr int N = 2;   // float4 loads per thread per slab
+  using Regs = f32x4[N];
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t vo;   // the lane's row-group offset
+  int tid, g, k0;
+  __device__ void init(const void* base, uint32_t bytes, int tid_, uint32_t row_off) {
+    rs = buf_rsrc(base, bytes);
+    tid = tid_;
+    g = (tid & 63) >> 4;
+    k0 = __builtin_amdgcn_readfirstlane(tid >> 6) * 4;
+    vo = row_off;
+  }
+  // ofs[i][q]: byte offset of k = kbase + k0 + 16 i + q (wave-uniform)
+  __device__ void load(const uint32_t (&ofs)[N][4], int kvalid, Regs& rg) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint32_t o = g == 0 ? ofs[i][0] : (g == 1 ? ofs[i][1] : (g == 2 ? ofs[i][2] : ofs[i][3]));
+      uint32_t v = vo + o;
+      if (kvalid < BK) v = k0 + 16 * i + g < kvalid ? v : kOob;   // (wave-uniform test: partial last slab only)
+      rg[i] = buf_ld4(rs, v, 0u);
+    }
+  }
+  __device__ void store(float* t, const Regs& rg) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) O::put(t, (tid & 15) * 4, k0 + 16 * i + g, rg[i]);
+  }
+};
+
 // Stream form of gemm_body (policies with a member type Streams): the same pipeline, fragments, MFMA chains, bias chains
 // and epilogue, with the slab staging done by the policy's streams:
 //   typename P::Streams st = p.streams(z, row0, col0, tid);   per tile
 //   st.load(s, x) / st.store(s, x, As, Bs)                    x: a P::Streams::Regs register set
 template <class P, class = void>
 struct HasStreams : std::false_type {};
+#ifndef QLX_Q32_NO_STREAMS   // (A/B builds of the measurement harnesses: every policy on the ldA / ldB core)
 template <class P>
 struct HasStreams<P, std::void_t<typename P::Streams>> : std::bool_constant<!std::is_void_v<typename P::Streams>> {};
+#endif
 
 template <class P>
 __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
@@ -1473,6 +1512,11 @@ struct PConv2DgradPx {
       typename AffineStream<BM_, false, T>::Regs a;
       typename AffineStream<BN_, false, T>::Regs b;
     };
+    __device__ void load_z(int z, int s, Regs& x) const {   // (chained sub-tiles, PConv2DgradPxG)
+      Streams o = *this;
+      o.q = px(z);
+      o.load(s, x);
+    }
     __device__ void load(int s, Regs& x) const {
       const int t = s >> 1, th = q.th0 + t / q.ntw, tw = q.tw0 + t % q.ntw, h = (s & 1) * 32;
       a.load((uint32_t)(((q.i - th) * 9 + q.j - tw) * 64 + h) * 4u, 0, x.a);
@@ -1667,32 +1711,35 @@ struct PConvWgrad {
   // streams (gemm_body_s): A = the im2col rows gathered one reduction index r = (b, oh, ow) per wave instruction (its
   // offset on the scalar unit), B = dz rows, affine in r; r past the chunk reads zeros
   static constexpr int T = WM_ * WN_ * 64;
-  struct Streams {
-    GatherKStream<T> a;
+  struct StreamsImpl {
+    GatherK4Stream<T> a;
     AffineStream<BN_, true, T, true> b;
     int z, rows;
     struct Regs {
-      typename GatherKStream<T>::Regs a;
+      typename GatherK4Stream<T>::Regs a;
       typename AffineStream<BN_, true, T, true>::Regs b;
     };
     __device__ void load(int s, Regs& x) const {
       const int kbase = s * BK, kvalid = rows - kbase;
-      // the wave's NJ consecutive r = (b, oh, ow): the first by division, the rest by carries (all scalar)
-      constexpr int NJ = GatherKStream<T>::NJ;
-      const int r0 = kbase + a.k0, bl = r0 / P, pp = r0 - bl * P;
-      int oh = pp / OW, ow = pp - oh * OW;
-      uint32_t o = (uint32_t)((((z * SC + bl) * H + oh * S) * W + ow * S) * C) * 4u;
-      uint32_t ofs[NJ];
+      // the wave's r = (b, oh, ow): 4 consecutive from r0 and from r0 + 16, the first of each by division, the others by
+      // carries (all scalar)
+      uint32_t ofs[2][4];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        ofs[j] = o;
-        o += S * C * 4u;
-        if (++ow == OW) {
-          ow = 0;
-          o += (uint32_t)(S * W * C - OW * S * C) * 4u;
-          if (++oh == OH) {
-            oh = 0;
-            o += (uint32_t)(H * W * C - OH * S * W * C) * 4u;
+      for (int i = 0; i < 2; ++i) {
+        const int r0 = kbase + a.k0 + 16 * i, bl = r0 / P, pp = r0 - bl * P;
+        int oh = pp / OW, ow = pp - oh * OW;
+        uint32_t o = (uint32_t)((((z * SC + bl) * H + oh * S) * W + ow * S) * C) * 4u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ofs[i][q] = o;
+          o += S * C * 4u;
+          if (++ow == OW) {
+            ow = 0;
+            o += (uint32_t)(S * W * C - OW * S * C) * 4u;
+            if (++oh == OH) {
+              oh = 0;
+              o += (uint32_t)(H * W * C - OH * S * W * C) * 4u;
+            }
           }
         }
       }
@@ -1704,12 +1751,18 @@ struct PConvWgrad {
       b.store(bs, x.b);
     }
   };
-  __device__ Streams streams(int z, int row0, int col0, int tid) const {
-    static_assert(BM_ == 64 && MF_ == 16, "gather stream: 64-row tiles");
-    Streams st;
+  // (the gather stream stages 64-row tiles: other tile shapes keep the ldA / ldB core)
+#ifdef QLX_Q32_WGRAD_STREAMS
+  using Streams = std::conditional_t<BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4, StreamsImpl, void>;
+#else
+  using Streams = void;
+#endif
+  template <class ST = Streams>
+  __device__ ST streams(int z, int row0, int col0, int tid) const {
+    ST st;
     st.z = z;
     st.rows = rows_in(z);
-    const int m = row0 + (tid & 63), tap = m / C, c = m - tap * C, kh = tap / KS, kw = tap - kh * KS;
+    const int m = row0 + (tid & 15) * 4, tap = m / C, c = m - tap * C, kh = tap / KS, kw = tap - kh * KS;
     st.a.init(in, (uint32_t)B * H * W * C * 4u, tid, (uint32_t)((kh * W + kw) * C + c) * 4u);
     st.b.init(dz + (size_t)z * SC * P * OC, (uint32_t)st.rows * OC * 4u, tid,
               [col0](int r, int k) { return (uint32_t)(k * OC + col0 + r) * 4u; });
