@@ -790,6 +790,9 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   int tm, tn, z;
   p.decode(lb, tm, tn, z);
   const int row0 = tm * P::BM, col0 = tn * P::BN;
+  if constexpr (HasActive<P>::value) {
+    if (!p.active(z, row0)) return;
+  }
   const int ns = p.nslabs(z);
   const St st = p.streams(z, row0, col0, tid);
   float* As0 = lds;
@@ -1076,6 +1079,70 @@ struct PConvFwdL {
       if (q.o[r] >= 0) out[(size_t)q.o[r] + col] = relu(v[r] + q.b);
       else if (q.o[r] == -2) cbuf[col] = relu(v[r] + q.b);
     }
+  }
+  // streams (gemm_body_s; the list tiles, row tile >= 1 - the constant-row tile runs in ConstRows on the ldA core): A =
+  // the listed rows' im2col windows (rows past the list read zeros), a slab's tap and channel offset wave-uniform; SEL:
+  // a row's background taps read the constant row cx instead (one buffer spans `in` and cx: both live in the model's
+  // workspace), a per-lane select per slab.  B = the weight rows, affine.
+  struct StreamsImpl {
+    __amdgpu_buffer_rsrc_t ra;
+    uint32_t vo[NA], cxo[NA], msk[NA];
+    int tid;
+    AffineStream<BN_, true, T> b;
+    struct Regs {
+      f32x4 a[NA];
+      typename AffineStream<BN_, true, T>::Regs b;
+    };
+    __device__ void load(int s, Regs& x) const {
+      const int tap = (s * BK) / C, c0 = (s * BK) % C, kh = tap / KS, kw = tap - kh * KS;
+      const uint32_t so = (uint32_t)((kh * W + kw) * C + c0) * 4u;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        if (OA::F4 % T == 0 || tid + i * T < OA::F4) {
+          if constexpr (SEL) {
+            const bool cst = (msk[i] >> tap) & 1u;
+            x.a[i] = buf_ld4(ra, cst ? cxo[i] + (uint32_t)c0 * 4u : vo[i] + so, 0u);
+          } else {
+            x.a[i] = buf_ld4(ra, vo[i], so);
+          }
+        }
+      }
+      b.load((uint32_t)s * BK * OC * 4u, 0, x.b);
+    }
+    __device__ void store(float* as, float* bs, const Regs& x) const {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int idx = tid + i * T;
+        if (OA::F4 % T == 0 || idx < OA::F4) {
+          int r, k;
+          OA::coord(idx, r, k);
+          OA::put(as, r, k, x.a[i]);
+        }
+      }
+      b.store(bs, x.b);
+    }
+  };
+  using Streams = StreamsImpl;
+  __device__ Streams streams(int, int row0, int col0, int tid) const {
+    Streams st;
+    st.tid = tid;
+    // one descriptor over [min(in, cx), max end): both in the model's workspace (f32_forward)
+    const char* lo = (const char*)in;
+    const char* base = SEL && (const char*)cx < lo ? (const char*)cx : lo;
+    const uint32_t in_off = (uint32_t)(lo - base), cx_off = SEL ? (uint32_t)((const char*)cx - base) : 0u;
+    st.ra = buf_rsrc(base, 0x7FFFFFF0u);   // (row offsets are bounded by the list entries: b * R + p of this chunk)
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      int r = 0, k = 0;
+      OA::coord(tid + i * T, r, k);
+      const int raw = entry(row0 + r), e = raw >= 0 ? raw & 0xFFFFF : -1;
+      const int bb = e / R, pp = e - bb * R, oh = pp / OW, ow = pp - oh * OW;
+      st.vo[i] = e >= 0 ? in_off + (uint32_t)(((bb * H + oh * S) * W + ow * S) * C + k) * 4u : kOob;
+      st.cxo[i] = cx_off + (uint32_t)k * 4u;
+      st.msk[i] = SEL && raw >= 0 ? (uint32_t)raw >> 20 : 0u;
+    }
+    st.b.init(w, (uint32_t)KS * KS * C * OC * 4u, tid, [col0](int r, int k) { return (uint32_t)(k * OC + col0 + r) * 4u; });
+    return st;
   }
 };
 template <int BM, int BN, int WM, int WN>
