@@ -18,7 +18,9 @@ nearly one length, so their ends come in waves): after the first wave the envs' 
 steps (Run._steady), then one mean episode length of vector steps must each hold within +-50 % of the expected
 n_envs / mean-length episode ends.  Then W untimed training vector steps, then K timed ones (asserted to contain
 episode ends).  Beside the headline, measured in the same run: the same loop with the frozen target net evaluated per
-sampled batch as the reference does (value_no_target_memo), and the bf16 fast path (labelled, not the headline).
+sampled batch as the reference does (value_no_target_memo), fp32 with the exact zero skips off (value_dense_frames:
+every conv1 step and conv2 / conv3 row computed), the per-step fractions those skips leave out (skipped_fractions), and
+the bf16 fast path (labelled, not the headline).
 
 Multi-GPU: with --gpus N > 1 and no WORLD_SIZE in the environment, this process starts
 `torch.distributed.run --nproc-per-node N` on itself before touching the GPU and exits with its code; each rank owns
@@ -78,6 +80,12 @@ def parse():
     ap.add_argument("--nomemo-steps", type=int, default=5,
                     help="timed vector steps of the headline precision with the target net evaluated per sampled batch "
                          "(QLX_TARGET_CACHE=0, the reference's work; 0 = skip)")
+    ap.add_argument("--dense-steps", type=int, default=5,
+                    help="fp32: timed vector steps of a learner built with the exact zero skips off (QLX_F32_BG=0 "
+                         "QLX_F32_C1_SKIP=0: every conv1 step and conv2 / conv3 row computed; 0 = skip)")
+    ap.add_argument("--sparsity-steps", type=int, default=8,
+                    help="fp32: untimed vector steps after the timed window, each reporting the fractions of conv work "
+                         "the skips left out (qlx_learner_frame_sparsity)")
     ap.add_argument("--cpu-sample", type=int, default=4_000,
                     help="env-steps of the CPU baseline: the first N of C1's 10,000 (~26 s on the box's host; 0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=1)
@@ -209,7 +217,7 @@ def rate(work, us, div):
 class Run:
     """One learner measured on the steady-state workload."""
 
-    def __init__(self, args, ctl, precision, steps, warmup, flags):
+    def __init__(self, args, ctl, precision, steps, warmup, flags, sparsity_steps=0):
         import qlx
         self.args, self.ctl, self.precision = args, ctl, precision
         N, B = args.envs, args.batch
@@ -243,6 +251,7 @@ class Run:
             log(f"{precision}: timed {steps} vector steps")
             self._timed(steps)
             log(f"{precision}: {self.value():.1f} env-steps/s")
+            self.sparsity = self._sparsity(sparsity_steps) if sparsity_steps > 0 else None
         finally:
             L.close()
 
@@ -343,6 +352,30 @@ class Run:
         self.last_loss = s1["last_loss"]
         self.running_reward = s1["running_reward"]
         self.epsilon = s1["epsilon"]
+
+    def _sparsity(self, n):
+        """Per vector step (untimed, after the timed window): the fractions of the fp32 conv work the exact zero skips
+        left out - conv1 forward / weight-gradient all-zero steps, conv2 / conv3 background rows - over the step's sampled
+        training states and over its acting frames (qlx_learner_frame_sparsity, the kernels' own predicates)."""
+        import numpy as np
+        L = self.L
+        tr, ac = [], []
+        for _ in range(n):
+            L.run(1)
+            f = L.frame_sparsity()
+            if not np.isnan(f["train"][0]):
+                tr.append(f["train"])
+            ac.append(f["act"])
+        names = ("conv1_fwd_zero_steps", "conv1_wgrad_zero_steps", "conv2_background_rows", "conv3_background_rows")
+        def summ(rows):
+            if not rows:
+                return None
+            a = np.asarray(rows)
+            return {k: {"mean": round(float(a[:, i].mean()), 4), "min": round(float(a[:, i].min()), 4),
+                        "max": round(float(a[:, i].max()), 4)} for i, k in enumerate(names)}
+        return {"vector_steps": n, "train_batches": summ(tr), "acting": summ(ac),
+                "note": "fractions of the dense conv work not issued (exact skips, DESIGN.md 4.1), per vector step after "
+                        "the timed window; train = the step's U x B sampled states, acting = the n_envs frames"}
 
     def roofline(self):
         """The dominant kernel against the MFMA peak of this precision (the Q-net is MFMA class):
@@ -450,7 +483,8 @@ def main():
     assert args.batch % args.replay_ratio == 0
     import qlx
     flags = (qlx.DOUBLE_DQN if args.double_dqn else 0) | (qlx.PER if args.per else 0)
-    head = Run(args, ctl, args.precision, args.steps, args.warmup, flags)
+    f32 = args.precision == "fp32"
+    head = Run(args, ctl, args.precision, args.steps, args.warmup, flags, args.sparsity_steps if f32 else 0)
     nomemo = None
     if args.nomemo_steps > 0 and "target_memo" in head.comps:
         # the reference's per-batch target work (same values, tests/test_gpu_learner.py), measured in this run
@@ -464,6 +498,19 @@ def main():
             else:
                 os.environ["QLX_TARGET_CACHE"] = prev
         assert "target_memo" not in nomemo.comps
+    dense = None
+    if f32 and args.dense_steps > 0:
+        # the same loop on a learner built with the exact zero skips off (every conv1 step, every conv2 / conv3 row)
+        prev = {k: os.environ.get(k) for k in ("QLX_F32_BG", "QLX_F32_C1_SKIP")}
+        os.environ.update({"QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"})
+        try:
+            dense = Run(args, ctl, "fp32", args.dense_steps, 1, flags)
+        finally:
+            for k, v in prev.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
     other = "bf16" if args.precision == "fp32" else "fp32"
     beside = Run(args, ctl, other, args.beside_steps, 1, flags) if args.beside_steps > 0 else None
     # the measured window is the steady-state loop: greedy acting and episode ends inside it
@@ -524,6 +571,16 @@ def main():
             "note": "same loop and precision with the frozen target net evaluated per sampled batch (U*B target forwards "
                     "per vector step, the reference's work: self_driving_tf_q_learner.rs:189-199) instead of once per "
                     "transition at insertion; identical targets (tests/test_gpu_learner.py)"}
+    if dense is not None:
+        line["value_dense_frames"] = round(dense.value(), 1)
+        line["dense_frames"] = {
+            "value": round(dense.value(), 1), "unit": "env-steps/s", "steps": dense.steps,
+            "ms_per_step": round(dense.dt / dense.steps * 1e3, 3), "grad_updates_per_sec": round(dense.updates / dense.dt, 2),
+            "note": "fp32 with the exact zero skips off (QLX_F32_BG=0 QLX_F32_C1_SKIP=0, a learner built so in this run): "
+                    "every conv1 MFMA step and every conv2 / conv3 row computed - the rate on frames without black "
+                    "background; bit-identical results (tests/test_gpu_qnet32_paths.py)"}
+    if head.sparsity is not None:
+        line["skipped_fractions"] = head.sparsity
     if beside is not None:
         line[f"{other}_beside"] = {
             "value": round(beside.value(), 1), "unit": "env-steps/s", "steps": beside.steps,

@@ -132,6 +132,9 @@ int32_t qlx_model_num_vars(void);
  * (float32; the reference's Keras optimizer_config, keras_metadata.pb; no device needed). */
 int32_t qlx_model_hparams(float* out);
 int64_t qlx_model_var_size(int32_t var);
+/* Frame sparsity of a batch (diagnostic, as qlx_learner_frame_sparsity): table = device array of n x 4 frame pointers
+ * (84 x 84 u8 frames in the replay's s2d layout, NULL = a zero frame), out[4] as one half of that function's output. */
+int32_t qlx_frame_sparsity(const uint8_t* const* table, uint32_t n, int32_t device, double* out);
 /* which: 0 = weights, 1 = Adam m, 2 = Adam v.  Layout = Keras HWIO / [in,out]. */
 int32_t qlx_model_get_var(qlx_model* m, int32_t var, int32_t which, float* out);
 int32_t qlx_model_set_var(qlx_model* m, int32_t var, int32_t which, const float* in);
@@ -239,6 +242,11 @@ int32_t qlx_learner_last(qlx_learner* l, uint8_t* actions, float* rewards, uint8
  * [n_updates][B], the sum tree's leaves [history_buffer_len] (priority^alpha per physical replay slot), the
  * priority new transitions enter with; any may be NULL. */
 int32_t qlx_learner_priorities(qlx_learner* l, float* is_weights, float* leaves, float* per_max);
+/* Frame sparsity of the last vector step (diagnostic, not on the hot path; synchronises): the fractions of the fp32
+ * conv work the exact zero skips leave out, in the kernels' own units - out[0..3] over the step's sampled training
+ * states (NaN when the step ran no update), out[4..7] over the acting frames, each {conv1 forward all-zero steps,
+ * conv1 weight-gradient all-zero steps, conv2 background rows, conv3 background rows}. */
+int32_t qlx_learner_frame_sparsity(qlx_learner* l, double* out);
 /* Learning statistics (learning_update_log, self_driving_tf_q_learner.rs:235-273): per-action counts over the
  * replay's actions [3] (device histogram), the episode reward history oldest first (n = entries, up to cap
  * copied), and the log text itself (UTF-8; *len = full length, buf gets up to cap - 1 bytes + NUL).  Actions are

@@ -853,6 +853,17 @@ int32_t qlx_learner_priorities(qlx_learner* L, float* is_weights, float* leaves,
   });
 }
 
+// Frame sparsity of the last vector step (diagnostic; synchronises): out[0..3] over its sampled training states (NaN when
+// it ran no update), out[4..7] over the acting frames, each {conv1 forward zero steps, conv1 weight-gradient zero steps,
+// conv2 background rows, conv3 background rows} as fractions (qnet32.hip k_frame_sparsity)
+int32_t qlx_learner_frame_sparsity(qlx_learner* L, double* out) {
+  return guard([&] {
+    QLX_CHECK(L && out, QLX_E_INVALID, "null argument");
+    frame_sparsity(L->d_tab_s, (int)(L->last_updates * L->B), out, L->stream);
+    frame_sparsity(L->d_obs_table, (int)L->N, out + 4, L->stream);
+  });
+}
+
 // ---- learning statistics (learning_update_log, self_driving_tf_q_learner.rs:235-273; stats.hip) ----
 static std::vector<float> learner_episode_rewards(qlx_learner* L) {
   QLX_HIP(hipStreamSynchronize(L->stream));

@@ -89,6 +89,11 @@ struct qlx_model {
   // conv1 weight gradient as channel-half blocks (k_conv1_wgrad_h); QLX_CONV1_HALVES=0 at create time selects the
   // one-block-per-chunk k_conv1_wgrad (bit-identical gradients)
   bool conv1_halves = true;
+  // fp32 sparsity paths, read at create time (a learner built with them off runs the dense forward / weight gradient in
+  // the same process: bench.py value_dense_frames): QLX_F32_BG=0 computes every conv2 / conv3 forward row (no background
+  // rows), QLX_F32_C1_SKIP=0 issues conv1's all-zero frame steps.  Bit-identical results either way.
+  bool f32_bg_rows = true;
+  int f32_c1_skip = 1;
   // fp32 update schedule (when the caller allows it: no all-reduce between backward and Adam): the dense variables' norm
   // partials as extra blocks of the weight-gradient reduction launch, then every variable's clip_by_norm + Adam in one
   // launch (k_update32) - the update's tail is two launches.  Set by the backward, consumed by model_norms / model_adam.
@@ -160,4 +165,7 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
 void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update);
 void f32_norms(qlx_model* m, hipStream_t s, float scale);
 void f32_adam(qlx_model* m, hipStream_t s, float scale);
+// fractions of a batch's fp32 conv work the exact skips leave out (qnet32.hip k_frame_sparsity; synchronises s):
+// out = {conv1 forward zero steps, conv1 weight-gradient zero steps, conv2 background rows, conv3 background rows}
+void frame_sparsity(const uint8_t* const* table, int n, double* out, hipStream_t s);
 }  // namespace qlx

@@ -687,14 +687,8 @@ static int num_cus() {
 static Grid grid(int M, int BM, int N, int BN, int nz) { return Grid{(M + BM - 1) / BM, (N + BN - 1) / BN, nz}; }
 
 // conv1 forward / weight gradient: MFMA steps whose frame operands are all 0 are not issued (exact, see k_conv1_fwd32);
-// QLX_F32_C1_SKIP=0 issues every step (A/B measurement)
-static int c1_skip() {
-  static const int v = [] {
-    const char* e = std::getenv("QLX_F32_C1_SKIP");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v;
-}
+// a model created under QLX_F32_C1_SKIP=0 issues every step (qlx_model::f32_c1_skip)
+static int c1_skip(const qlx_model* m) { return m->f32_c1_skip; }
 
 // training-batch conv2 / conv3 forward over M rows on a balanced grid (PConv2FwdR / PConv3FwdR): `whole` 64 x 64 tiles,
 // a multiple of the CU count, plus the remaining rows as 16 x 64 tiles; 0 when the shape has no such split (fewer whole
@@ -718,14 +712,9 @@ static void launch_list(qlx_model* m, const P& p, const S& side, const char* sco
   debug_sync(s, scope);
 }
 
-// background rows (see C1Lists in qnet32_kernels.h): on by default; QLX_F32_BG=0 computes every conv2 / conv3 row (A/B)
-static bool bg_rows() {
-  static const bool v = [] {
-    const char* e = std::getenv("QLX_F32_BG");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
+// background rows (see C1Lists in qnet32_kernels.h): on by default; a model created under QLX_F32_BG=0 computes every
+// conv2 / conv3 row (qlx_model::f32_bg_rows)
+static bool bg_rows(const qlx_model* m) { return m->f32_bg_rows; }
 
 template <class PW, class PR, class PF>
 static void conv_fwd(qlx_model* m, int M, const float* in, const float* wt, const float* bias, float* out, const char* scope,
@@ -754,7 +743,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     // shapes are separate kernels and separate profiler scopes (suffix _big)
     const bool big = n > 2048;
     // background rows: conv1 lists them, conv2 / conv3 run the rest (the list counters alternate between forwards)
-    const bool lists = bg_rows();
+    const bool lists = bg_rows(m);
     unsigned long long* cnt = w.frcnt + 2 * kListSlots * kCntStride * w.fparity;
     const int G = c1_blocks(n);                                        // conv1 blocks
     const int per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);   // samples of a list region, at most
@@ -772,7 +761,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       const size_t lds = 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
       set_lds_limit((const void*)kern, 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)kC1MaxIt * 6 * 8);
       hipExtLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
-                            p + voff(0), p + voff(1), w.fa1, c1_skip(), L);
+                            p + voff(0), p + voff(1), w.fa1, c1_skip(m), L);
       QLX_HIP(hipGetLastError());
       debug_sync(s, sc);
     }
@@ -927,7 +916,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     hipEvent_t ea = nullptr, eb = nullptr;
     if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);
-    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1, c1_skip());
+    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1, c1_skip(m));
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv1_wgrad32");
   }
@@ -977,6 +966,86 @@ void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   QLX_HIP(hipGetLastError());
   debug_sync(s, "k_adam32");
   m->iterations = t;
+}
+
+
+// ---- frame sparsity of a batch (diagnostic, bench.py): how much of the fp32 conv work the exact skips leave out ----
+// Per sample, in the kernels' own units (the same predicates, re-evaluated from the frames): conv1 forward (tile, kq)
+// steps whose 64 frame dwords are all 0 (k_conv1_fwd32: 25 tiles x 16 per sample), conv1 weight-gradient (wave, rs)
+// steps likewise (k_conv1_wgrad32: 4 x 100), conv2 / conv3 background rows (c1_flags: 81 / 49).  Counts into cnt[4].
+__global__ __launch_bounds__(256) void k_frame_sparsity(const uint8_t* const* table, int n, unsigned long long* cnt) {
+  __shared__ uint32_t fr[4][84][21];   // row layout: pixels (x, 4 d .. 4 d + 3) at fr[slot][x][d]
+  __shared__ uint32_t bm[4][21];       // per block row bx: bit by = the 4 x 4 pixel block (bx, by) of any frame non-zero
+  __shared__ int tot[4];
+  int mine[4] = {0, 0, 0, 0};
+  for (int b = blockIdx.x; b < n; b += gridDim.x) {
+    __syncthreads();
+    if (threadIdx.x < 21) bm[0][threadIdx.x] = 0u;
+    __syncthreads();
+    for (int q = threadIdx.x; q < kC1Chunks; q += blockDim.x) {   // s2d chunk (slot, bx, by): rows 4 bx + xl, dword by
+      const int slot = q / 441, pos = q - slot * 441, bx = pos / 21, by = pos - bx * 21;
+      const uint8_t* f = table[(size_t)b * 4 + slot];
+      uint4 v = uint4{0u, 0u, 0u, 0u};
+      if (f) v = *reinterpret_cast<const uint4*>(f + (size_t)pos * 16);
+      fr[slot][4 * bx][by] = v.x;
+      fr[slot][4 * bx + 1][by] = v.y;
+      fr[slot][4 * bx + 2][by] = v.z;
+      fr[slot][4 * bx + 3][by] = v.w;
+      if ((v.x | v.y | v.z | v.w) != 0u) atomicOr(&bm[0][bx], 1u << by);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 400; i += blockDim.x) {
+      {  // forward step (tile t, kq): lanes (g = slot, l = patch position), dword (4 oh + kh, ow + hw)
+        const int t = i >> 4, kq = i & 15, kh = kq >> 1, hw = kq & 1;
+        uint32_t o = 0u;
+        for (int g = 0; g < 4; ++g)
+          for (int l = 0; l < 16; ++l) {
+            const int oh = 4 * (t / 5) + (l >> 2), ow = 4 * (t % 5) + (l & 3);
+            o |= fr[g][4 * oh + kh][ow + hw];
+          }
+        mine[0] += o == 0u;
+      }
+      {  // weight-gradient step (wave w, rs): lanes (g, l15), position r = 4 rs + g, slot l15 & 3, kh = 2 w + l15 / 8
+        const int w = i / 100, rs = i - 100 * w;
+        uint32_t o = 0u;
+        for (int g = 0; g < 4; ++g)
+          for (int l = 0; l < 16; ++l) {
+            const int r = 4 * rs + g, oh = r / 20, ow = r - 20 * oh, kh = 2 * w + (l >> 3), h = (l >> 2) & 1;
+            o |= fr[l & 3][4 * oh + kh][ow + h];
+          }
+        mine[1] += o == 0u;
+      }
+    }
+    for (int p = threadIdx.x; p < 81 + 49; p += blockDim.x) {   // background rows from the 4 x 4 block marks
+      const bool c2 = p < 81;
+      const int pp = c2 ? p : p - 81, R = c2 ? 9 : 7, i = pp / R, j = pp - R * i, span = c2 ? 5 : 9;
+      uint32_t mm = 0u;
+      for (int r = 0; r < span; ++r) mm |= bm[0][2 * i + r];
+      const bool bg = ((mm >> (2 * j)) & ((1u << span) - 1u)) == 0u;
+      mine[c2 ? 2 : 3] += bg;
+    }
+  }
+  if (threadIdx.x < 4) tot[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k = 0; k < 4; ++k) atomicAdd(&tot[k], mine[k]);
+  __syncthreads();
+  if (threadIdx.x < 4) atomicAdd(cnt + threadIdx.x, (unsigned long long)tot[threadIdx.x]);
+}
+
+void frame_sparsity(const uint8_t* const* table, int n, double* out, hipStream_t s) {
+  for (int k = 0; k < 4; ++k) out[k] = std::nan("");
+  if (n <= 0) return;
+  unsigned long long* d = nullptr;
+  QLX_HIP(hipMallocAsync((void**)&d, 4 * sizeof(unsigned long long), s));
+  QLX_HIP(hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_frame_sparsity, dim3(std::min(n, 4 * num_cus())), dim3(256), 0, s, table, n, d);
+  QLX_HIP(hipGetLastError());
+  unsigned long long h[4];
+  QLX_HIP(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s));
+  QLX_HIP(hipFreeAsync(d, s));
+  QLX_HIP(hipStreamSynchronize(s));
+  const double per[4] = {400.0, 400.0, 81.0, 49.0};
+  for (int k = 0; k < 4; ++k) out[k] = (double)h[k] / (per[k] * n);
 }
 
 }  // namespace qlx

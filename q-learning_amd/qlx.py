@@ -146,6 +146,7 @@ def lib():
         "qlx_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_learner_env": ([vp], vp), "qlx_learner_replay": ([vp], vp), "qlx_learner_model": ([vp, i32], vp),
         "qlx_learner_priorities": ([vp, vp, vp, vp], i32),
+        "qlx_learner_frame_sparsity": ([vp, vp], i32), "qlx_frame_sparsity": ([vp, C.c_uint32, i32, vp], i32),
         "qlx_learner_action_counts": ([vp, vp], i32), "qlx_bg_learner_action_counts": ([vp, vp], i32),
         "qlx_learner_episode_rewards": ([vp, vp, u64, C.POINTER(u64)], i32),
         "qlx_bg_learner_episode_rewards": ([vp, vp, u64, C.POINTER(u64)], i32),
@@ -245,6 +246,13 @@ def model_hparams(ballgame=False):
     """(learning_rate, beta_1, beta_2, epsilon, clipnorm) every model is created with (float32, no device needed)"""
     out = np.zeros(5, np.float32)
     _check((lib().qlx_bg_model_hparams if ballgame else lib().qlx_model_hparams)(_p(out)))
+    return out
+
+
+def frame_sparsity(table_ptr, n, device=0):
+    """qlx_frame_sparsity: table_ptr = device address of n x 4 frame pointers; returns the four fractions"""
+    out = np.zeros(4, np.float64)
+    _check(lib().qlx_frame_sparsity(C.c_void_p(table_ptr), n, device, _p(out)))
     return out
 
 
@@ -533,6 +541,14 @@ class SelfDrivingQLearner(_LearningStats):
         n = self.last()["losses"].shape[0]
         _check(lib().qlx_learner_priorities(self.h, _p(w), _p(leaves), C.byref(pmax)))
         return w[:n * B].reshape(n, B), leaves, pmax.value
+
+    def frame_sparsity(self):
+        """Fractions of the fp32 conv work the exact zero skips leave out in the last vector step (diagnostic):
+        {"train": [...], "act": [...]}, each [conv1 fwd zero steps, conv1 wgrad zero steps, conv2 bg rows, conv3 bg rows]
+        (train: the step's sampled states, NaN without an update; act: the acting frames)."""
+        out = np.zeros(8, np.float64)
+        _check(lib().qlx_learner_frame_sparsity(self.h, _p(out)))
+        return {"train": out[:4].tolist(), "act": out[4:].tolist()}
 
     def dist_init(self, world, rank, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))

@@ -8,8 +8,12 @@ Each must give the oracle's bits (oracle/qnet32_ref.cpp, the same chains as test
 conv2 / conv3 activations of a 1,024-sample forward, Q of a 3,000-sample (chunk-size kernels) forward, and one training
 step at B = 1,024 (loss, all ten gradients, the clip norms, w / m / v after Adam).
 
-Most switches are read once per process (static), so each variant runs in a child process (one at a time, so at most
-two processes hold the GPU) on inputs and weights the parent wrote; the parent compares against the oracle.
+QLX_F32_BG / QLX_F32_C1_SKIP are read when a model is created (bench.py builds its dense-frame learner in-process),
+QLX_NUM_CUS once per process; each variant runs in a child process (one at a time, so at most two processes hold the
+GPU) on inputs and weights the parent wrote; the parent compares against the oracle.
+
+test_frame_sparsity: the diagnostic that reports how much of that work the skips leave out (qlx_frame_sparsity,
+bench.py's per-step fractions) against a numpy restatement of the kernels' predicates.
 """
 import os
 import subprocess
@@ -108,3 +112,64 @@ def test_path_bit_exact(case, env):
             g = g.reshape(np.asarray(want).shape)
         bad = np.flatnonzero(np.asarray(g).ravel().view(np.uint32) != np.asarray(want, np.float32).ravel().view(np.uint32))
         assert same(g, want), f"{env}: {k}: {bad.size} elements differ (first {bad[:5]})"
+
+
+def _s2d(img):
+    """[n, 4, 84, 84] u8 frames -> the replay's s2d layout [n, 4, 7056]: byte (bx * 21 + by) * 16 + xl * 4 + yl holds
+    pixel (4 bx + xl, 4 by + yl)"""
+    n = img.shape[0]
+    return np.ascontiguousarray(img.reshape(n, 4, 21, 4, 21, 4).transpose(0, 1, 2, 4, 3, 5).reshape(n, 4, 7056))
+
+
+def _sparsity_ref(img):
+    """numpy restatement: conv1 forward (tile t, kq) steps - tile t = the 4 x 4 output patch (4 (t / 5), 4 (t % 5)),
+    kq = (kh, hw): pixels (4 oh + kh, 4 (ow + hw) .. + 3) of every frame; conv1 weight-gradient (wave w, rs) steps -
+    positions r = 4 rs + g (g < 4), pixels (4 oh + kh, 4 (ow + h) .. + 3), kh in {2 w, 2 w + 1}, h in {0, 1}; conv2 / conv3
+    background rows - the 20 x 20 / 36 x 36 pixel field from (8 i, 8 j) all zero"""
+    n = img.shape[0]
+    nz = (img != 0).any(axis=1)                                   # [n, 84, 84]
+    quad = nz.reshape(n, 84, 21, 4).any(axis=3)                   # [n, 84 rows, 21 dword columns]
+    f = 0
+    for t in range(25):
+        for kq in range(16):
+            kh, hw = kq >> 1, kq & 1
+            rows = [4 * (4 * (t // 5) + a) + kh for a in range(4)]
+            cols = [4 * (t % 5) + c + hw for c in range(4)]
+            f += int((~quad[:, rows][:, :, cols].reshape(n, -1).any(axis=1)).sum())
+    w_ = 0
+    for w in range(4):
+        for rs in range(100):
+            rows, cols = [], []
+            for g in range(4):
+                r = 4 * rs + g
+                oh, ow = divmod(r, 20)
+                for kh in (2 * w, 2 * w + 1):
+                    for h in (0, 1):
+                        rows.append(4 * oh + kh)
+                        cols.append(ow + h)
+            w_ += int((~quad[:, rows, cols].any(axis=1)).sum())
+    b2 = sum(int((~nz[:, 8 * i:8 * i + 20, 8 * j:8 * j + 20].reshape(n, -1).any(axis=1)).sum()) for i in range(9) for j in range(9))
+    b3 = sum(int((~nz[:, 8 * i:8 * i + 36, 8 * j:8 * j + 36].reshape(n, -1).any(axis=1)).sum()) for i in range(7) for j in range(7))
+    return np.array([f / (400.0 * n), w_ / (400.0 * n), b2 / (81.0 * n), b3 / (49.0 * n)])
+
+
+def test_frame_sparsity():
+    import torch
+    import qlx
+    n = 96
+    img = env_states(n, seed=5).transpose(0, 3, 1, 2).copy()     # [n, 4, 84, 84] u8 from the env kernel's play
+    img[n // 2:, :, 30:50, 10:60] = 0                            # more background in half of them
+    img[3] = 0
+    null = {(7, 1), (8, 0), (8, 1), (8, 2), (8, 3)}              # NULL table entries read zero frames
+    for b, s in null:
+        img[b, s] = 0
+    dev = torch.from_numpy(_s2d(img)).cuda()
+    base = dev.data_ptr()
+    tab = [0 if (b, s) in null else base + (b * 4 + s) * 7056 for b in range(n) for s in range(4)]
+    table = torch.tensor(tab, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    got = qlx.frame_sparsity(table.data_ptr(), n, torch.cuda.current_device())
+    want = _sparsity_ref(img)
+    assert np.array_equal(got, want), (got, want)
+    assert 0.2 < want[0] < 1.0 and 0.2 < want[2] < 1.0             # a real mix, not all-zero / all-live
+    assert np.isnan(qlx.frame_sparsity(table.data_ptr(), 0, torch.cuda.current_device())).all()
