@@ -132,9 +132,6 @@ int32_t qlx_model_num_vars(void);
  * (float32; the reference's Keras optimizer_config, keras_metadata.pb; no device needed). */
 int32_t qlx_model_hparams(float* out);
 int64_t qlx_model_var_size(int32_t var);
-/* Frame sparsity of a batch (diagnostic, as qlx_learner_frame_sparsity): table = device array of n x 4 frame pointers
- * (84 x 84 u8 frames in the replay's s2d layout, NULL = a zero frame), out[4] as one half of that function's output. */
-int32_t qlx_frame_sparsity(const uint8_t* const* table, uint32_t n, int32_t device, double* out);
 /* which: 0 = weights, 1 = Adam m, 2 = Adam v.  Layout = Keras HWIO / [in,out]. */
 int32_t qlx_model_get_var(qlx_model* m, int32_t var, int32_t which, float* out);
 int32_t qlx_model_set_var(qlx_model* m, int32_t var, int32_t which, const float* in);

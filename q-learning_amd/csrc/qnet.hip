@@ -791,13 +791,6 @@ int32_t qlx_model_hparams(float* out) {
     out[0] = m.lr; out[1] = m.beta1; out[2] = m.beta2; out[3] = m.eps; out[4] = m.clipnorm;
   });
 }
-int32_t qlx_frame_sparsity(const uint8_t* const* table, uint32_t n, int32_t device, double* out) {
-  return guard([&] {
-    QLX_CHECK(out && (table || n == 0), QLX_E_INVALID, "null argument");
-    current_device_checked(device);
-    frame_sparsity(table, (int)n, out, nullptr);
-  });
-}
 int64_t qlx_model_var_size(int32_t v) { return (v >= 0 && v < kNumVars) ? kVarSize[v] : -1; }
 
 int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model** out) {

@@ -146,7 +146,7 @@ def lib():
         "qlx_learner_last": ([vp, vp, vp, vp, vp, vp, vp, C.POINTER(u32)], i32),
         "qlx_learner_env": ([vp], vp), "qlx_learner_replay": ([vp], vp), "qlx_learner_model": ([vp, i32], vp),
         "qlx_learner_priorities": ([vp, vp, vp, vp], i32),
-        "qlx_learner_frame_sparsity": ([vp, vp], i32), "qlx_frame_sparsity": ([vp, C.c_uint32, i32, vp], i32),
+        "qlx_learner_frame_sparsity": ([vp, vp], i32),
         "qlx_learner_action_counts": ([vp, vp], i32), "qlx_bg_learner_action_counts": ([vp, vp], i32),
         "qlx_learner_episode_rewards": ([vp, vp, u64, C.POINTER(u64)], i32),
         "qlx_bg_learner_episode_rewards": ([vp, vp, u64, C.POINTER(u64)], i32),
@@ -246,13 +246,6 @@ def model_hparams(ballgame=False):
     """(learning_rate, beta_1, beta_2, epsilon, clipnorm) every model is created with (float32, no device needed)"""
     out = np.zeros(5, np.float32)
     _check((lib().qlx_bg_model_hparams if ballgame else lib().qlx_model_hparams)(_p(out)))
-    return out
-
-
-def frame_sparsity(table_ptr, n, device=0):
-    """qlx_frame_sparsity: table_ptr = device address of n x 4 frame pointers; returns the four fractions"""
-    out = np.zeros(4, np.float64)
-    _check(lib().qlx_frame_sparsity(C.c_void_p(table_ptr), n, device, _p(out)))
     return out
 
 

@@ -10,7 +10,7 @@ rm -rf "$OUT" && mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gputest.log" 2>&1 || exit 1
 timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o s -- \
-  python3 bench.py --steps 3 --warmup 1 --beside-steps 0 --nomemo-steps 0 --cpu-sample 0 --profile-steps 1 > "$OUT/stats.json" \
+  python3 bench.py --steps 3 --warmup 1 --beside-steps 0 --nomemo-steps 0 --dense-steps 0 --sparsity-steps 0 --cpu-sample 0 --profile-steps 1 > "$OUT/stats.json" \
   2> "$OUT/stats.err" || exit 1
 bash scripts/pmc.sh || exit 1
 mv gpurun_out/pmc "$OUT/pmc"

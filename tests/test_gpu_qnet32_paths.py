@@ -12,7 +12,7 @@ QLX_F32_BG / QLX_F32_C1_SKIP are read when a model is created (bench.py builds i
 QLX_NUM_CUS once per process; each variant runs in a child process (one at a time, so at most two processes hold the
 GPU) on inputs and weights the parent wrote; the parent compares against the oracle.
 
-test_frame_sparsity: the diagnostic that reports how much of that work the skips leave out (qlx_frame_sparsity,
+test_frame_sparsity: the diagnostic that reports how much of that work the skips leave out (qlx_learner_frame_sparsity,
 bench.py's per-step fractions) against a numpy restatement of the kernels' predicates.
 """
 import os
@@ -154,22 +154,24 @@ def _sparsity_ref(img):
 
 
 def test_frame_sparsity():
-    import torch
+    """qlx_learner_frame_sparsity against the numpy restatement on the same frames: the last vector step's sampled
+    states (replay get_many of its indices) and the acting frames (the learner's env)"""
     import qlx
-    n = 96
-    img = env_states(n, seed=5).transpose(0, 3, 1, 2).copy()     # [n, 4, 84, 84] u8 from the env kernel's play
-    img[n // 2:, :, 30:50, 10:60] = 0                            # more background in half of them
-    img[3] = 0
-    null = {(7, 1), (8, 0), (8, 1), (8, 2), (8, 3)}              # NULL table entries read zero frames
-    for b, s in null:
-        img[b, s] = 0
-    dev = torch.from_numpy(_s2d(img)).cuda()
-    base = dev.data_ptr()
-    tab = [0 if (b, s) in null else base + (b * 4 + s) * 7056 for b in range(n) for s in range(4)]
-    table = torch.tensor(tab, dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
-    got = qlx.frame_sparsity(table.data_ptr(), n, torch.cuda.current_device())
-    want = _sparsity_ref(img)
-    assert np.array_equal(got, want), (got, want)
-    assert 0.2 < want[0] < 1.0 and 0.2 < want[2] < 1.0             # a real mix, not all-zero / all-live
-    assert np.isnan(qlx.frame_sparsity(table.data_ptr(), 0, torch.cuda.current_device())).all()
+    p = qlx.Parameter(n_envs=256, batch_size=64, update_after_actions=8, history_buffer_len=20_000, env_seed=11,
+                      epsilon_pure_random_steps=0)
+    L = qlx.SelfDrivingQLearner(p)
+    try:
+        L.prefill(40)
+        L.run(3)
+        f = L.frame_sparsity()
+        last = L.last()
+        idx = last["indices"].ravel()
+        assert idx.size == last["losses"].shape[0] * 64 > 0
+        s = L.replay_buffer.get_many(idx)["state"].transpose(0, 3, 1, 2)
+        want_t = _sparsity_ref(np.ascontiguousarray(s))
+        want_a = _sparsity_ref(np.ascontiguousarray(L.environment.state().transpose(0, 3, 1, 2)))
+        assert np.array_equal(np.asarray(f["train"]), want_t), (f["train"], want_t)
+        assert np.array_equal(np.asarray(f["act"]), want_a), (f["act"], want_a)
+        assert 0.2 < want_t[0] < 1.0 and 0.2 < want_t[2] < 1.0   # a real mix, not all-zero / all-live
+    finally:
+        L.close()
