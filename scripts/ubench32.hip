@@ -429,6 +429,66 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 1 && std::string(argv[1]) == "sweep") {   // backward-pair tile shapes on the operand-stream core, B = 1024
+    const int B = 1024, z = B / 16;
+    const double ff = 4.0 * B * 512 * 3136, f3 = 4.0 * B * 49 * 64 * 576, f2 = 4.0 * B * 81 * 64 * 512;
+    using Wg3 = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, 16>;
+    using Wg2 = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, 16>;
+    for (int rep = 0; rep < 2; ++rep) {
+      printf("--- rep %d\n", rep);
+      run2("fc1 W64x64 D32x64 (shipped)", PFc1WgradT<64, 64, 2, 2>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<32, 64, 2, 2>{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B}, ff);
+      run2("fc1 W64x64 D64x64", PFc1WgradT<64, 64, 2, 2>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<64, 64, 2, 2>{grid(B, 64, 3136, 64, 1), dz4, W3, a3, dz3, B}, ff);
+      run2("fc1 W64x64 D32x32", PFc1WgradT<64, 64, 2, 2>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<32, 32, 2, 2>{grid(B, 32, 3136, 32, 1), dz4, W3, a3, dz3, B}, ff);
+      run2("fc1 W64x64 D64x32", PFc1WgradT<64, 64, 2, 2>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<64, 32, 2, 2>{grid(B, 64, 3136, 32, 1), dz4, W3, a3, dz3, B}, ff);
+      run2("fc1 W64x32 D32x64", PFc1WgradT<64, 32, 2, 2>{grid(3136, 64, 512, 32, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<32, 64, 2, 2>{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B}, ff);
+      run2("fc1 W128x64 D32x64", PFc1WgradT<128, 64, 2, 2>{grid(3136, 128, 512, 64, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<32, 64, 2, 2>{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B}, ff);
+      run2("conv3 W64x64 Dpx32x64 (shipped)", Wg3{grid(576, 64, 64, 64, z), a2, dz3, slab, B},
+           PConv3DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 1, 81}, dz3, W2, a2, dz2, B}, f3);
+      run2("conv3 W64x64 Dpx64x64", Wg3{grid(576, 64, 64, 64, z), a2, dz3, slab, B},
+           PConv3DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 1, 81}, dz3, W2, a2, dz2, B}, f3);
+      run2("conv3 W64x64 Dpx32x32", Wg3{grid(576, 64, 64, 64, z), a2, dz3, slab, B},
+           PConv3DgradPx<32, 32, 2, 2>{Grid{(B + 31) / 32, 2, 81}, dz3, W2, a2, dz2, B}, f3);
+      run2("conv3 W64x64 Dpx16x64", Wg3{grid(576, 64, 64, 64, z), a2, dz3, slab, B},
+           PConv3DgradPx<16, 64, 1, 4>{Grid{(B + 15) / 16, 1, 81}, dz3, W2, a2, dz2, B}, f3);
+      run2("conv3 W64x32 Dpx32x64", Wg3{grid(576, 64, 64, 32, z), a2, dz3, slab, B},
+           PConv3DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 1, 81}, dz3, W2, a2, dz2, B}, f3);
+      run2("conv2 W64x64 Dpx64x64 (shipped)", Wg2{grid(512, 64, 64, 64, z), a1, dz2, slab, B},
+           PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, W1, a1, dz1, B}, f2);
+      run2("conv2 W64x64 Dpx32x64", Wg2{grid(512, 64, 64, 64, z), a1, dz2, slab, B},
+           PConv2DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 2, 100}, dz2, W1, a1, dz1, B}, f2);
+      run2("conv2 W64x64 Dpx64x128", Wg2{grid(512, 64, 64, 64, z), a1, dz2, slab, B},
+           PConv2DgradPx<64, 128, 2, 2>{Grid{(B + 63) / 64, 1, 100}, dz2, W1, a1, dz1, B}, f2);
+      run2("conv2 W64x64 Dpx64x32", Wg2{grid(512, 64, 64, 64, z), a1, dz2, slab, B},
+           PConv2DgradPx<64, 32, 2, 2>{Grid{(B + 63) / 64, 4, 100}, dz2, W1, a1, dz1, B}, f2);
+      run2("conv2 W64x32 Dpx64x64", Wg2{grid(512, 64, 64, 32, z), a1, dz2, slab, B},
+           PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, W1, a1, dz1, B}, f2);
+    }
+    return 0;
+  }
+  if (argc > 1 && std::string(argv[1]) == "c1probe") {
+    // what the conv1 kernels cost besides their MFMAs: live frames (nothing skippable) vs all-zero frames (a null table:
+    // every step skippable) with the zero-step skip on / off, B = 1024
+    const uint8_t** ztab = nullptr;
+    CK(hipMalloc(&ztab, ht.size() * sizeof(void*)));
+    CK(hipMemset(ztab, 0, ht.size() * sizeof(void*)));
+    const int B = 1024, G = 512, nz = B / 4, lds = kC1Frames + 400 * 16 * 4;
+    CK(hipFuncSetAttribute((const void*)k_conv1_fwd32<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kC1Frames));
+    CK(hipFuncSetAttribute((const void*)k_conv1_wgrad32, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    for (int zero = 0; zero < 2; ++zero)
+      for (int skip = 0; skip < 2; ++skip) {
+        const uint8_t* const* t = zero ? ztab : table;
+        const double uf = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32<0>, dim3(G), dim3(256), 2 * kC1Frames, 0, t, B, W0, W0 + 8192, a1, skip, C1Lists{}); });
+        const double uw = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(kC1WgradThreads), lds, 0, t, dz1, B, nz, slab, skip); });
+        printf("conv1 B=%d frames %-5s skip %d: forward %8.2f us  weight gradient %8.2f us\n", B, zero ? "zero" : "live", skip, uf, uw);
+      }
+    return 0;
+  }
   for (int B : Bs) {
     printf("--- B = %d\n", B);
     {
