@@ -848,7 +848,7 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
   }
   {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its leading blocks
     PFc1WgradS Pw{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
-    PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
+    PFc1DgradS Pd{grid(B, PFc1DgradS::BM, 3136, PFc1DgradS::BN, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
     SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
     launch_pair(m, Pw, Pd, S, "f32_fc1_bwd", 2.0 * 2.0 * B * 512 * 3136, s);
   }
@@ -903,7 +903,12 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   // vs 93.4 us; on the ldA / ldB core the groups had won, 97.1 vs 105.6 us); conv2 groups were slower on both cores
   {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-    PConv3DgradPx<32, 64, 2, 2> Pd{Grid{(B + 31) / 32, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
+#ifndef QLX_Q32_OLD_TILES
+    using PD3 = PConv3DgradPx<64, 64, 2, 2>;   // (ubench32 sweep at B = 1024: pair 74.6 vs 75.7 us for 32 x 64)
+#else
+    using PD3 = PConv3DgradPx<32, 64, 2, 2>;
+#endif
+    PD3 Pd{Grid{(B + PD3::BM - 1) / PD3::BM, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles

@@ -572,11 +572,7 @@ struct RawOrder<P, std::void_t<decltype(P::RAW_ORDER)>> : std::integral_constant
 template <class P>
 __device__ __forceinline__ int block_order(int h, int G) { return RawOrder<P>::value ? h : xcd_logical(h, G); }
 
-template <class P>
-constexpr size_t gemm_lds_bytes() {
-  return (size_t)KSplitOf<P>::value * 2 *
-         (size_t)(Opnd<P::BM, P::A_KMAJ, MfOf<P>::value>::FLOATS + Opnd<P::BN, P::B_KMAJ, MfOf<P>::value>::FLOATS) * sizeof(float);
-}
+
 
 // grid layout shared by the policies: tile index fastest (col tile, then row tile), then z
 struct Grid {
@@ -667,45 +663,6 @@ struct AffineStream {
   }
 };
 
-// Gather stream for a KMAJ image whose k (the reduction index) is not affine in memory (the conv weight gradient's im2col
-// operand: k = (b, oh, ow)).  Each wave instruction loads one k for all ROWS = 64 rows (a dword per lane, row = lane), so
-// the k's byte offset is wave-uniform: the policy's kofs(k) is evaluated on the scalar unit, and a k past the valid count
-// reads through a zero-record descriptor.  Wave w of the tile stages k = w * (32 / W) + j, j < 32 / W.
-template <int T>
-struct GatherKStream {
-  static constexpr int W = T / 64, NJ = BK / W;
-  using O = Opnd<64, true, 16>;
-  using Regs = float[NJ];
-  __amdgpu_buffer_rsrc_t rs, rz;
-  uint32_t vo;   // the lane's row offset
-  int lane, k0;
-  __device__ void init(const void* base, uint32_t bytes, int tid, uint32_t row_off) {
-    rs = buf_rsrc(base, bytes);
-    rz = buf_rsrc(base, 0u);
-    lane = tid & 63;
-    k0 = __builtin_amdgcn_readfirstlane(tid >> 6) * NJ;
-    vo = row_off;
-  }
-  // kofs(k): byte offset of reduction index k (slab-relative k0 + j, absolute k = kbase + k0 + j)
-  // ofs[j]: byte offset of this wave's k = kbase + k0 + j (wave-uniform, from the policy's generator)
-  __device__ void load(const uint32_t (&ofs)[NJ], int kvalid, Regs& rg) const {
-    if (kvalid >= BK) {   // (wave-uniform: the masked form only in a partial last slab)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) rg[j] = buf_ld1(rs, vo, ofs[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const bool live = k0 + j < kvalid;
-        rg[j] = buf_ld1(live ? rs : rz, vo, live ? ofs[j] : 0u);
-      }
-    }
-  }
-  __device__ void store(float* t, const Regs& rg) const {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) t[(k0 + j) * O::PITCH + lane] = rg[j];
-  }
-};
-
 // Two affine streams (A, B) whose slab offsets are s * the policies' per-slab strides
 template <class SA, class SB, uint32_t DA, uint32_t DB, bool KMASK = false>
 struct PairStreams {
@@ -727,18 +684,22 @@ struct PairStreams {
   }
 };
 
-// Gather stream, 16-byte form: a thread stages 4 consecutive rows (a float4) of one k; the 64 lanes of a wave instruction
-// cover 4 consecutive k (16 lanes each), whose wave-uniform offsets (computed on the scalar unit) the lane picks by its
-// group lane / 16 (3 selects per load).  Wave w stages k = 4 w + g and 16 + 4 w + g.  A k past the valid count reads zeros.
+// Gather stream for a KMAJ image whose reduction index k is not affine in memory (the conv weight gradient's im2col
+// operand: k = (b, oh, ow)): a per-tile table in LDS holds each k's byte offset (kOob past the valid count), written once
+// by the block before its slab loop (prepare); per slab a thread reads its two k's offsets (two broadcast ds_read_b32)
+// and adds its row offset - no per-slab division or scalar offset arithmetic.  A thread stages 4 consecutive rows (a float4)
+// of one k; the 64 lanes of a wave instruction cover 4 consecutive k (16 lanes each): wave w stages k = 4 w + g and
+// 16 + 4 w + g.  (Measured slower and removed: the same offsets generated per slab on the scalar unit, 4 per wave load.)
 template <int T>
-struct GatherK4Stream {
-  static_assert(T == 256, "gather stream: four waves");
+struct TableK4Stream {
+  static_assert(T == 256, "table gather stream: four waves");
   using O = Opnd<64, true, 16>;
   static constexpr int N = 2;   // float4 loads per thread per slab
   using Regs = f32x4[N];
   __amdgpu_buffer_rsrc_t rs;
   uint32_t vo;   // the lane's row-group offset
   int tid, g, k0;
+  const uint32_t* tbl;   // LDS: byte offset of each k of the tile's reduction (kOob past its end)
   __device__ void init(const void* base, uint32_t bytes, int tid_, uint32_t row_off) {
     rs = buf_rsrc(base, bytes);
     tid = tid_;
@@ -746,21 +707,28 @@ struct GatherK4Stream {
     k0 = __builtin_amdgcn_readfirstlane(tid >> 6) * 4;
     vo = row_off;
   }
-  // ofs[i][q]: byte offset of k = kbase + k0 + 16 i + q (wave-uniform)
-  __device__ void load(const uint32_t (&ofs)[N][4], int kvalid, Regs& rg) const {
+  __device__ void load(int kbase, Regs& rg) const {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const uint32_t o = g == 0 ? ofs[i][0] : (g == 1 ? ofs[i][1] : (g == 2 ? ofs[i][2] : ofs[i][3]));
-      uint32_t v = vo + o;
-      if (kvalid < BK) v = k0 + 16 * i + g < kvalid ? v : kOob;   // (wave-uniform test: partial last slab only)
-      rg[i] = buf_ld4(rs, v, 0u);
-    }
+    for (int i = 0; i < N; ++i) rg[i] = buf_ld4(rs, vo + tbl[kbase + k0 + 16 * i + g], 0u);
   }
   __device__ void store(float* t, const Regs& rg) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) O::put(t, (tid & 15) * 4, k0 + 16 * i + g, rg[i]);
   }
 };
+
+// a policy's extra LDS after the operand buffers (EXTRA_LDS bytes; the streams' prepare(ptr) fills it per tile)
+template <class P, class = void>
+struct ExtraLdsOf : std::integral_constant<size_t, 0> {};
+template <class P>
+struct ExtraLdsOf<P, std::void_t<decltype(P::EXTRA_LDS)>> : std::integral_constant<size_t, P::EXTRA_LDS> {};
+
+template <class P>
+constexpr size_t gemm_lds_bytes() {
+  return (size_t)KSplitOf<P>::value * 2 *
+             (size_t)(Opnd<P::BM, P::A_KMAJ, MfOf<P>::value>::FLOATS + Opnd<P::BN, P::B_KMAJ, MfOf<P>::value>::FLOATS) * sizeof(float) +
+         ExtraLdsOf<P>::value;
+}
 
 // Stream form of gemm_body (policies with a member type Streams): the same pipeline, fragments, MFMA chains, bias chains
 // and epilogue, with the slab staging done by the policy's streams:
@@ -794,11 +762,15 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
     if (!p.active(z, row0)) return;
   }
   const int ns = p.nslabs(z);
-  const St st = p.streams(z, row0, col0, tid);
+  St st = p.streams(z, row0, col0, tid);
   float* As0 = lds;
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
   float* Bs1 = Bs0 + OB::FLOATS;
+  if constexpr (ExtraLdsOf<P>::value > 0) {   // the streams' per-tile LDS tables, complete before the first slab load
+    st.prepare(Bs1 + OB::FLOATS, ns);
+    __syncthreads();
+  }
   Regs x0, x1;
   Acc acc[TM][TN];
 #pragma unroll
@@ -1315,7 +1287,11 @@ struct PFc1DgradT {
   }
 };
 using PFc1Dgrad = PFc1DgradT<>;
+#ifndef QLX_Q32_OLD_TILES
+using PFc1DgradS = PFc1DgradT<64, 32, 2, 2>;   // (stream core, ubench32 sweep at B = 1024: 61.4 vs 66.0 us for 32 x 64)
+#else
 using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
+#endif
 
 // fc1 weight gradient: dW3 [3136][512] = a3^T dz4 over b ascending; db3 = column sums of dz4 (row-tile 0 blocks)
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
@@ -1775,55 +1751,49 @@ struct PConvWgrad {
     for (int r = 0; r < 4; ++r) slab[((size_t)z * (MROWS + 1) + row + r) * OC + col] = v[r];
   }
   __device__ void epi_bias(int z, int col, float v) const { slab[((size_t)z * (MROWS + 1) + MROWS) * OC + col] = v; }
-  // streams (gemm_body_s): A = the im2col rows gathered one reduction index r = (b, oh, ow) per wave instruction (its
-  // offset on the scalar unit), B = dz rows, affine in r; r past the chunk reads zeros
+  // streams (gemm_body_s): A = the im2col rows gathered through the tile's offset table (TableK4Stream: one entry per
+  // reduction index r = (b, oh, ow) of the chunk), B = dz rows, affine in r; r past the chunk reads zeros
   static constexpr int T = WM_ * WN_ * 64;
+  static constexpr int KMAX = (SC * P + BK - 1) / BK * BK;   // table entries: the chunk's r, padded to whole slabs
   struct StreamsImpl {
-    GatherK4Stream<T> a;
+    TableK4Stream<T> a;
     AffineStream<BN_, true, T, true> b;
     int z, rows;
     struct Regs {
-      typename GatherK4Stream<T>::Regs a;
+      typename TableK4Stream<T>::Regs a;
       typename AffineStream<BN_, true, T, true>::Regs b;
     };
-    __device__ void load(int s, Regs& x) const {
-      const int kbase = s * BK, kvalid = rows - kbase;
-      // the wave's r = (b, oh, ow): 4 consecutive from r0 and from r0 + 16, the first of each by division, the others by
-      // carries (all scalar)
-      uint32_t ofs[2][4];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r0 = kbase + a.k0 + 16 * i, bl = r0 / P, pp = r0 - bl * P;
-        int oh = pp / OW, ow = pp - oh * OW;
-        uint32_t o = (uint32_t)((((z * SC + bl) * H + oh * S) * W + ow * S) * C) * 4u;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          ofs[i][q] = o;
-          o += S * C * 4u;
-          if (++ow == OW) {
-            ow = 0;
-            o += (uint32_t)(S * W * C - OW * S * C) * 4u;
-            if (++oh == OH) {
-              oh = 0;
-              o += (uint32_t)(H * W * C - OH * S * W * C) * 4u;
-            }
-          }
+    // the chunk's r -> byte offset of its im2col row base in `in` (kOob past the chunk)
+    __device__ void prepare(float* ext, int ns) {
+      uint32_t* t = reinterpret_cast<uint32_t*>(ext);
+      for (int r = a.tid; r < ns * BK; r += T) {
+        uint32_t o = kOob;
+        if (r < rows) {
+          const int bl = r / P, pp = r - bl * P, oh = pp / OW, ow = pp - oh * OW;
+          o = (uint32_t)((((z * SC + bl) * H + oh * S) * W + ow * S) * C) * 4u;
         }
+        t[r] = o;
       }
-      a.load(ofs, kvalid, x.a);
-      b.load((uint32_t)kbase * OC * 4u, kvalid, x.b);
+      a.tbl = t;
+    }
+    __device__ void load(int s, Regs& x) const {
+      const int kbase = s * BK;
+      a.load(kbase, x.a);
+      b.load((uint32_t)kbase * OC * 4u, rows - kbase, x.b);
     }
     __device__ void store(float* as, float* bs, const Regs& x) const {
       a.store(as, x.a);
       b.store(bs, x.b);
     }
   };
-  // (the gather stream stages 64-row tiles: other tile shapes keep the ldA / ldB core)
-#ifdef QLX_Q32_WGRAD_STREAMS
-  using Streams = std::conditional_t<BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4, StreamsImpl, void>;
+  // (the table stream stages 64-row tiles on four waves: other tile shapes keep the ldA / ldB core)
+#ifndef QLX_Q32_NO_WGRAD_TABLE   // (A/B builds: the weight gradients on the ldA / ldB core)
+  static constexpr bool STREAMED = BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4;
 #else
-  using Streams = void;
+  static constexpr bool STREAMED = false;
 #endif
+  using Streams = std::conditional_t<STREAMED, StreamsImpl, void>;
+  static constexpr size_t EXTRA_LDS = STREAMED ? (size_t)KMAX * 4 : 0;
   template <class ST = Streams>
   __device__ ST streams(int z, int row0, int col0, int tid) const {
     ST st;

@@ -173,7 +173,8 @@ int main(int argc, char** argv) {
   replay(PFc1Wgrad{grid(3136, 64, 512, 64, 1), a3, dz4, gw3, gb3, B}, "fc1_wgrad");
   replay(PFc1Dgrad{grid(B, 64, 3136, 64, 1), dz4, w3, a3, dz3, B}, "fc1_dgrad");
   replay(PFc1WgradS{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), a3, dz4, gw3, gb3, B}, "fc1_wgrad S");
-  replay(PFc1DgradS{grid(B, 32, 3136, 64, 1), dz4, w3, a3, dz3, B}, "fc1_dgrad S");
+  replay(PFc1DgradS{grid(B, PFc1DgradS::BM, 3136, PFc1DgradS::BN, 1), dz4, w3, a3, dz3, B}, "fc1_dgrad S");
+  replay(PConv3DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 1, 81}, dz3, w2, a2, dz2, B}, "conv3_dgrad px 64");
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
   replay(PConv3Dgrad{grid(B * 81, 64, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad");
   replay(PConv3DgradS{grid(B * 81, 32, 64, 64, 1), dz3, w2, a2, dz2, B * 81}, "conv3_dgrad S");

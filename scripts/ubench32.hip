@@ -316,6 +316,51 @@ static void gen(int M, int N, int K, const float* A, const float* B, float* C) {
   run1(name, p, 2.0 * M * N * K);
 }
 
+// c1probe: the conv1 forward's a1 store pattern alone (lane (g, c) of wave (ct, rp) stores its 13 tiles x 4 rows per
+// sample, as k_conv1_fwd32 does) and its frame fetch + LDS staging alone, B samples over G blocks
+__global__ __launch_bounds__(256, 2) void k_probe_a1_stores(int B, float* a1, float v) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ct = wave & 1, rp = wave >> 1;
+  const int col = ct * 16 + (lane & 15), g = lane >> 4, nt = rp == 0 ? 13 : 12;
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < 13; ++j)
+      if (j < nt) {
+        const int t = rp + 2 * j, r0 = (4 * (t / 5) + g) * 20 + 4 * (t % 5);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = v + i;
+      }
+  }
+}
+__global__ __launch_bounds__(256, 2) void k_probe_a1_stores_row(int B, float* a1, float v) {   // the same bytes, row-contiguous
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    f32x4* d = reinterpret_cast<f32x4*>(a1 + (size_t)b * 12800);
+    for (int q = threadIdx.x; q < 3200; q += 256) d[q] = f32x4{v, v, v, v};
+  }
+}
+__global__ __launch_bounds__(256, 2) void k_probe_frames(const uint8_t* const* table, int B, float* out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];
+  int b = blockIdx.x;
+  if (b >= B) return;
+  uint4 pf[7];
+  c1_prefetch(c1_ptrs(table, b), pf);
+  C1Ptrs nxt = c1_ptrs(table, b + (int)gridDim.x < B ? b + (int)gridDim.x : b);
+  c1_stage(c1w, pf);
+  __syncthreads();
+  uint32_t acc = 0;
+  for (int it = 0; b < B; b += gridDim.x, ++it) {
+    const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
+    const int nb = b + gridDim.x;
+    if (nb < B) {
+      c1_prefetch(nxt, pf);
+      nxt = c1_ptrs(table, nb + (int)gridDim.x < B ? nb + (int)gridDim.x : nb);
+    }
+    acc += fr[threadIdx.x];
+    if (nb < B) c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);
+    __syncthreads();
+  }
+  if (acc == 0x12345678u) out[threadIdx.x] = 1.0f;
+}
+
 int main(int argc, char** argv) {
   const bool only_c1 = argc > 1 && std::string(argv[1]) == "conv1";   // just the two conv1 kernels
   const int Bs[2] = {1024, 8192};
@@ -487,6 +532,15 @@ int main(int argc, char** argv) {
         const double uw = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * nz), dim3(kC1WgradThreads), lds, 0, t, dz1, B, nz, slab, skip); });
         printf("conv1 B=%d frames %-5s skip %d: forward %8.2f us  weight gradient %8.2f us\n", B, zero ? "zero" : "live", skip, uf, uw);
       }
+    for (int nb : {1024, 8192}) {
+      const double us_st = time_us([&] { hipLaunchKernelGGL(k_probe_a1_stores, dim3(G), dim3(256), 0, 0, nb, a1, 1.0f); });
+      const double us_row = time_us([&] { hipLaunchKernelGGL(k_probe_a1_stores_row, dim3(G), dim3(256), 0, 0, nb, a1, 1.0f); });
+      CK(hipFuncSetAttribute((const void*)k_probe_frames, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kC1Frames));
+      const double us_fr = time_us([&] { hipLaunchKernelGGL(k_probe_frames, dim3(G), dim3(256), 2 * kC1Frames, 0, table, nb, a4); });
+      const double us_frz = time_us([&] { hipLaunchKernelGGL(k_probe_frames, dim3(G), dim3(256), 2 * kC1Frames, 0, ztab, nb, a4); });
+      printf("B=%d: a1 stores (conv1 pattern) %8.2f us (%.2f TB/s), row-contiguous %8.2f us; frame fetch + stage %8.2f us, zero table %8.2f us\n",
+             nb, us_st, nb * 51200.0 / us_st / 1e6, us_row, us_fr, us_frz);
+    }
     return 0;
   }
   for (int B : Bs) {
@@ -515,7 +569,7 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&act, B));
       CK(hipMemset(act, 1, B));
       PFc1WgradS Pw{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), a3, dz4, gw, gw, B};
-      PFc1DgradS Pd{grid(B, 32, 3136, 64, 1), dz4, W3, a3, dz3, B};
+      PFc1DgradS Pd{grid(B, PFc1DgradS::BM, 3136, PFc1DgradS::BN, 1), dz4, W3, a3, dz3, B};
       SideFc2 S{a4, act, dz4, dz4 + 1024, B, gw, gw + 2000, gw + 3000};
       const size_t lds = std::max({gemm_lds_bytes<PFc1WgradS>(), gemm_lds_bytes<PFc1DgradS>(), SideFc2::LDS});
       double us = time_us([&] {
