@@ -903,11 +903,8 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   // vs 93.4 us; on the ldA / ldB core the groups had won, 97.1 vs 105.6 us); conv2 groups were slower on both cores
   {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
     PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
-#ifndef QLX_Q32_OLD_TILES
-    using PD3 = PConv3DgradPx<64, 64, 2, 2>;   // (ubench32 sweep at B = 1024: pair 74.6 vs 75.7 us for 32 x 64)
-#else
-    using PD3 = PConv3DgradPx<32, 64, 2, 2>;
-#endif
+    // 64 x 64 pixel tiles on the stream core: pair 73.2 vs 75.0 us in place for 32 x 64 (gpurun_out/w3)
+    using PD3 = PConv3DgradPx<64, 64, 2, 2>;
     PD3 Pd{Grid{(B + PD3::BM - 1) / PD3::BM, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }

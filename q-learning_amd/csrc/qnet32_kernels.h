@@ -1287,11 +1287,8 @@ struct PFc1DgradT {
   }
 };
 using PFc1Dgrad = PFc1DgradT<>;
-#ifndef QLX_Q32_OLD_TILES
-using PFc1DgradS = PFc1DgradT<64, 32, 2, 2>;   // (stream core, ubench32 sweep at B = 1024: 61.4 vs 66.0 us for 32 x 64)
-#else
+// (64 x 32 on the stream core: 61.4 vs 66.0 us alone in scripts/ubench32.hip sweep, but 67.0 vs 65.2 us in place)
 using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
-#endif
 
 // fc1 weight gradient: dW3 [3136][512] = a3^T dz4 over b ascending; db3 = column sums of dz4 (row-tile 0 blocks)
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
@@ -1787,11 +1784,9 @@ struct PConvWgrad {
     }
   };
   // (the table stream stages 64-row tiles on four waves: other tile shapes keep the ldA / ldB core)
-#ifndef QLX_Q32_NO_WGRAD_TABLE   // (A/B builds: the weight gradients on the ldA / ldB core)
+  // (in place against the ldA / ldB core: 262.3K vs 263.0K env-steps/s, conv2 pair 102.0 vs 102.2 us - neutral; kept as the
+  // one path: the weight-gradient tiles then issue no per-slab address arithmetic)
   static constexpr bool STREAMED = BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4;
-#else
-  static constexpr bool STREAMED = false;
-#endif
   using Streams = std::conditional_t<STREAMED, StreamsImpl, void>;
   static constexpr size_t EXTRA_LDS = STREAMED ? (size_t)KMAX * 4 : 0;
   template <class ST = Streams>
