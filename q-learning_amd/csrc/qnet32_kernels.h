@@ -2116,34 +2116,34 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
     // iteration); (it + 1) % 3 gets the next sample's at the end of this iteration; (it + 2) % 3, read at the end of
     // it - 1, is cleared for it + 1
     if (lists && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
-    f32x4 acc[13];
+    // tile-outer: each tile's chain over (kq, kw) runs to completion and its four rows are stored before the next tile's
+    // chain, so the sample's a1 stores (51 KB) leave during its MFMAs instead of after the last one; the next tile's 16
+    // frame dwords are read while this tile multiplies (against the kq-outer loop over all 13 accumulators: 49.1 -> 47.9 us
+    // at B = 1024, 320 -> 309 us per 8,192-sample chunk, 256 -> 218 VGPRs; gpurun_out/w4).  One branch per (kq, tile) with
+    // its four kw steps back to back (a branch per MFMA: 60 vs 46 us at C3)
+    uint32_t dn[16];
+    auto tile_dwords = [&](int j, uint32_t (&d)[16]) {
+      const uint32_t base = (ob2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
 #pragma unroll
-    for (int j = 0; j < 13; ++j) acc[j] = zero4();
-#pragma unroll
-    for (int kq = 0; kq < 16; ++kq) {   // (kh, kw half): pixels (4 oh + kh, 4 ow + 4 hw .. + 3) per lane and tile
-      const int kh = kq >> 1, hw = kq & 1;
-      const int off = kh * 21 + hw;
-      uint32_t d[13];
-      bool on[13];
-#pragma unroll
-      for (int j = 0; j < 13; ++j) {
-        d[j] = j < nt ? fr[((ob2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) + off] : 0u;
-        on[j] = j < nt && (!skip || __builtin_amdgcn_ballot_w64(d[j] != 0u) != 0);   // wave-uniform
-      }
-      // one branch per (kq, tile): its four kw steps chain on one accumulator back to back (a branch per MFMA, kw outer:
-      // 60 vs 46 us at C3; the next step's dwords read before this step's branches: no gain, and 48 B of scratch)
-#pragma unroll
-      for (int j = 0; j < 13; ++j)
-        if (on[j])
-#pragma unroll
-          for (int kw = 0; kw < 4; ++kw) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[j], kw), wf[kq * 4 + kw], acc[j], 0, 0, 0);
-    }
+      for (int kq = 0; kq < 16; ++kq) d[kq] = fr[base + (kq >> 1) * 21 + (kq & 1)];   // (kh, kw half): pixels (4 oh + kh, 4 ow + 4 hw ..)
+    };
+    tile_dwords(0, dn);
 #pragma unroll
     for (int j = 0; j < 13; ++j)
       if (j < nt) {
+        uint32_t d[16];
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) d[kq] = dn[kq];
+        if (j + 1 < nt) tile_dwords(j + 1, dn);
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq)
+          if (!skip || __builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0)   // wave-uniform
+#pragma unroll
+            for (int kw = 0; kw < 4; ++kw) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[kq], kw), wf[kq * 4 + kw], acc, 0, 0, 0);
         const int t = rp + 2 * j, r0 = (4 * (t / 5) + g) * 20 + 4 * (t % 5);   // rows (oh, ow .. ow + 3) of the patch
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[j][i] + bias);
+        for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[i] + bias);
       }
     if (lists && wave < 3) c1_flags(rm + (it % 3) * kC1RmDw, cl + it * 6 + wave * 2, wave, tid);
     if (nb < B) {
