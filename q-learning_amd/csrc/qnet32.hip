@@ -793,7 +793,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       } else {
         // (64 x 64 / 32 x 64 / 16 x 64 / 32 x 32 list tiles at B = 1024: within +-1 % of 64 x 32)
         run(PConv2FwdL<64, 32, 2, 2>{}, PConv3FwdL<64, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
-        launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
+        launch(m, PFc1FwdS{grid(n, PFc1FwdS::BM, 512, PFc1FwdS::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);
       }
     } else if (big) {
@@ -809,7 +809,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
                                       PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81});
       conv_fwd<PConv3Fwd, PConv3FwdR>(m, n * 49, w.fa2, p + voff(4), p + voff(5), w.fa3, "f32_conv3_fwd", 2.0 * n * 49 * 64 * 576, s,
                                       PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49});
-      launch(m, PFc1FwdS{grid(n, 32, 512, 32, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
+      launch(m, PFc1FwdS{grid(n, PFc1FwdS::BM, 512, PFc1FwdS::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
              2.0 * n * 3136 * 512, s);
     }
   }
@@ -906,11 +906,13 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     // 64 x 64 pixel tiles on the stream core: pair 73.2 vs 75.0 us in place for 32 x 64 (gpurun_out/w3)
     using PD3 = PConv3DgradPx<64, 64, 2, 2>;
     PD3 Pd{Grid{(B + PD3::BM - 1) / PD3::BM, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
+    
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
     PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
+    
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {

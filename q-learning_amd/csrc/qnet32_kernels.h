@@ -1231,7 +1231,11 @@ struct PFc1FwdT {
 using PFc1Fwd = PFc1FwdT<>;
 // chunk-size batches: 64 x 64 tiles on v_mfma_f32_32x32x2_f32 (scripts/ubench32.hip at B = 8192: 231 vs 247 us)
 using PFc1FwdB = PFc1FwdT<64, 64, 2, 2, 32>;
+#ifndef QLX_Q32_FC1F
 using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
+#else
+using PFc1FwdS = PFc1FwdT<QLX_Q32_FC1F>;
+#endif
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
@@ -1335,7 +1339,9 @@ struct PFc1WgradT {
 using PFc1Wgrad = PFc1WgradT<>;
 // training batch: 64 x 64 tiles (392 + the fc1 backward-data tiles; in place at C3: 68.6 -> 65.1 us per fc1 backward
 // against 64 x 32, 128 x 64 75.3, 64 x 128 77.3, 128 x 128 91.1 - gpurun_out/fc1b, fc1c)
-using PFc1WgradS = PFc1WgradT<64, 64, 2, 2>;
+// (on the stream core: 64 x 32, 784 tiles - fc1 backward pair 64.8 -> 61.6 us in place, gpurun_out/w7; with it, backward
+// data 64 x 32 / 32 x 32 / 64 x 64 ran 62.6 / 63.2 / 64.3 us against 61.5 us for 32 x 64, w8)
+using PFc1WgradS = PFc1WgradT<64, 32, 2, 2>;
 
 // conv3 backward-data: dz2 [B][9][9][64] = convT(dz3, W2) * (a2 > 0); rows (b, ih, iw), k = (kh, kw, oc)
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
