@@ -787,12 +787,14 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
                     s23, sc3, 2.0 * n * 49 * 64 * 576, s);
       };
       if (big) {
+        // (64 x 32 list tiles here: conv2 / conv3 145 / 185 us against 139 / 181 us, gpurun_out/w10)
         run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd_big", "f32_conv3_fwd_big");
         launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
                2.0 * n * 3136 * 512, s);
       } else {
-        // (64 x 64 / 32 x 64 / 16 x 64 / 32 x 32 list tiles at B = 1024: within +-1 % of 64 x 32)
-        run(PConv2FwdL<64, 32, 2, 2>{}, PConv3FwdL<64, 32, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        // (on the stream core, in place: conv2 64 x 64 24.3 us against 27.9 us for 64 x 32 and 28.7 for 32 x 64; conv3 32 x 64
+        // 27.6 us against 28.5 / 29.8 for 64 x 32 / 64 x 64 - gpurun_out/w10)
+        run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<32, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
         launch(m, PFc1FwdS{grid(n, PFc1FwdS::BM, 512, PFc1FwdS::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);
       }

@@ -1231,11 +1231,8 @@ struct PFc1FwdT {
 using PFc1Fwd = PFc1FwdT<>;
 // chunk-size batches: 64 x 64 tiles on v_mfma_f32_32x32x2_f32 (scripts/ubench32.hip at B = 8192: 231 vs 247 us)
 using PFc1FwdB = PFc1FwdT<64, 64, 2, 2, 32>;
-#ifndef QLX_Q32_FC1F
+// (re-checked on the stream core in place: 32 x 64 / 64 x 32 / 16 x 64 ran 35.3 / 35.9 / 40.4 us against 34.1 us, w9)
 using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
-#else
-using PFc1FwdS = PFc1FwdT<QLX_Q32_FC1F>;
-#endif
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
