@@ -789,7 +789,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       if (big) {
         // (64 x 32 list tiles here: conv2 / conv3 145 / 185 us against 139 / 181 us, gpurun_out/w10)
         run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd_big", "f32_conv3_fwd_big");
-        launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
+        launch(m, PFc1FwdB{grid(n, PFc1FwdB::BM, 512, PFc1FwdB::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
                2.0 * n * 3136 * 512, s);
       } else {
         // (on the stream core, in place: conv2 64 x 64 24.3 us against 27.9 us for 64 x 32 and 28.7 for 32 x 64; conv3 32 x 64
@@ -804,7 +804,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
              2.0 * n * 81 * 64 * 512, s);
       launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd_big",
              2.0 * n * 49 * 64 * 576, s);
-      launch(m, PFc1FwdB{grid(n, 64, 512, 64, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
+      launch(m, PFc1FwdB{grid(n, PFc1FwdB::BM, 512, PFc1FwdB::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
              2.0 * n * 3136 * 512, s);
     } else {
       conv_fwd<PConv2Fwd, PConv2FwdR>(m, n * 81, w.fa1, p + voff(2), p + voff(3), w.fa2, "f32_conv2_fwd", 2.0 * n * 81 * 64 * 512, s,

@@ -1229,8 +1229,9 @@ struct PFc1FwdT {
   }
 };
 using PFc1Fwd = PFc1FwdT<>;
-// chunk-size batches: 64 x 64 tiles on v_mfma_f32_32x32x2_f32 (scripts/ubench32.hip at B = 8192: 231 vs 247 us)
-using PFc1FwdB = PFc1FwdT<64, 64, 2, 2, 32>;
+// chunk-size batches: 64 x 128 tiles on the stream core (in place: 208 us against 228 us for 64 x 64 on
+// v_mfma_f32_32x32x2_f32, 212 / 215 us for 64 x 64 / 128 x 64; gpurun_out/w12)
+using PFc1FwdB = PFc1FwdT<64, 128, 2, 2, 16>;
 // (re-checked on the stream core in place: 32 x 64 / 64 x 32 / 16 x 64 ran 35.3 / 35.9 / 40.4 us against 34.1 us, w9)
 using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
 
