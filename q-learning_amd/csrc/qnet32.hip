@@ -557,8 +557,10 @@ static int conv_adam_blocks() {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
-using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3>;
-using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2>;
+// weight-gradient chunk tiles 64 x 64 on 1 x 4 waves (each wave 64 rows x 16 channels): conv3 / conv2 pairs 73.0 -> 72.3 /
+// 102.2 -> 101.2 us in place against 2 x 2 (4 x 1: no change; gpurun_out/w14)
+using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4>;
+using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4>;
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
 static_assert((1605632 + kNormSeg - 1) / kNormSeg <= kNormSegMax, "norm partials per variable");
