@@ -128,13 +128,17 @@ struct IglpOf : std::integral_constant<int, 1> {};
 template <class P>
 struct IglpOf<P, std::void_t<decltype(P::IGLP)>> : std::integral_constant<int, P::IGLP> {};
 
+
 // LOAD_FENCE = false: no scheduling barrier between a slab's global loads and its MFMAs (the scheduler may sink the
 // loads); measured per layer with iglp_opt in place: the fc1 forward 39.8 -> 38.3 us, the chunk-size conv2 forward 404 ->
-// 389 us, the conv3 backward pair 98.8 -> 97.7 us without it; every other layer 2-5 % slower without it.
+// 389 us, the conv3 backward pair 98.8 -> 97.7 us without it; every other layer 2-5 % slower without it.  Re-measured on
+// the stream core (round 4, gpurun_out/w17: every policy with / without it, iglp 0 / none for all): off for the conv2 pair's
+// two policies too; strategy 1 stays the best default.
 template <class P, class = void>
 struct LoadFenceOf : std::true_type {};
 template <class P>
 struct LoadFenceOf<P, std::void_t<decltype(P::LOAD_FENCE)>> : std::integral_constant<bool, P::LOAD_FENCE> {};
+
 
 // Optional per-tile A-operand context: a policy with a member type ACtx provides
 //   ACtx a_ctx(int z, int row0, int tid) const                       once per tile, per thread (e.g. the frame pointers of its rows)
@@ -1486,6 +1490,7 @@ struct PConv3DgradPx {
 template <int BM_ = 32, int BN_ = 128, int WM_ = 2, int WN_ = 2, bool DIRECT = false>
 struct PConv2DgradPx {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr bool LOAD_FENCE = false;   // (stream core, in place: conv2 pair -1.0 us without it, gpurun_out/w18)
   static constexpr bool A_KMAJ = false, B_KMAJ = false, BIAS = false, RAW_ORDER = true;
   Grid g;             // {ceil(B / BM), 128 / BN, 100}
   const float* dz2;   // [B][9][9][64]
@@ -1721,6 +1726,8 @@ template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC, in
           int MF_ = 16>
 struct PConvWgrad {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  static constexpr bool LOAD_FENCE = false;   // (with the conv2 backward data's: conv2 pair 101.3 -> 99.8 us, w18)
+  // (XCD-grouped block order kept: hardware order measured conv2 / conv3 pairs +2.3 / +1.0 us, w19)
   static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
   static constexpr int MROWS = KS * KS * C, P = OH * OW, CHUNK = SC;
   Grid g;
