@@ -559,7 +559,9 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
 // weight-gradient chunk tiles 64 x 64 on 1 x 4 waves (each wave 64 rows x 16 channels): conv3 / conv2 pairs 73.0 -> 72.3 /
 // 102.2 -> 101.2 us in place against 2 x 2 (4 x 1: no change; gpurun_out/w14)
-using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4>;
+// conv3's offset table after the images (3 blocks per CU: pair 72.2 us; in the images' pads, 4 per CU: 76.2 us, held to 3:
+// 81 us - gpurun_out/w22, w23); conv2's in the pads (4 blocks per CU: pair 99.6 -> 96.8 us)
+using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4, 16, false>;
 using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4>;
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
@@ -658,10 +660,12 @@ static void launch(qlx_model* m, const P& p, const char* scope, double work, hip
   debug_sync(s, scope);
 }
 
+// blocks_per_cu > 0: the launch reserves 160 KB / blocks_per_cu of LDS per block, so at most that many blocks share a CU
 template <class P1, class P2, class S, class T = NoSide>
 static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side, const char* scope, double work, hipStream_t s,
-                        const T& tail = T{}) {
-  const size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS, T::LDS});
+                        const T& tail = T{}, int blocks_per_cu = 0) {
+  size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS, T::LDS});
+  if (blocks_per_cu > 0) lds = std::max(lds, (size_t)160 * 1024 / blocks_per_cu / 256 * 256);
   hipEvent_t ea = nullptr, eb = nullptr;
   if (m->prof) m->prof->ext(scope, work, &ea, &eb);
   hipExtLaunchKernelGGL((k_gemm32_pair<P1, P2, S, T>), dim3(side.blocks() + p1.g.blocks() + p2.g.blocks() + tail.blocks()), dim3(256),
@@ -854,7 +858,7 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
     PFc1WgradS Pw{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
     PFc1DgradS Pd{grid(B, PFc1DgradS::BM, 3136, PFc1DgradS::BN, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
     SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
-    launch_pair(m, Pw, Pd, S, "f32_fc1_bwd", 2.0 * 2.0 * B * 512 * 3136, s);
+    launch_pair(m, Pw, Pd, S, "f32_fc1_bwd", 2.0 * 2.0 * B * 512 * 3136, s);   // (3 blocks per CU: 72.8 vs 61.8 us, w23)
   }
 }
 

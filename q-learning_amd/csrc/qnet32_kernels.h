@@ -694,7 +694,7 @@ struct PairStreams {
 // and adds its row offset - no per-slab division or scalar offset arithmetic.  A thread stages 4 consecutive rows (a float4)
 // of one k; the 64 lanes of a wave instruction cover 4 consecutive k (16 lanes each): wave w stages k = 4 w + g and
 // 16 + 4 w + g.  (Measured slower and removed: the same offsets generated per slab on the scalar unit, 4 per wave load.)
-template <int T>
+template <int T, bool PADS = true>
 struct TableK4Stream {
   static_assert(T == 256, "table gather stream: four waves");
   using O = Opnd<64, true, 16>;
@@ -703,7 +703,14 @@ struct TableK4Stream {
   __amdgpu_buffer_rsrc_t rs;
   uint32_t vo;   // the lane's row-group offset
   int tid, g, k0;
-  const uint32_t* tbl;   // LDS: byte offset of each k of the tile's reduction (kOob past its end)
+  const uint32_t* tbl;   // LDS: byte offset of each k of the tile's reduction (kOob past its end), in the operand images' pads
+  // entry r of the table: 16-entry segment r / 16 in the pad columns 64 .. 79 of k-row (r / 16) % 32 of image r / 512 (the
+  // four 64-row KMAJ images - A and B, two buffers each - are contiguous, 2,560 floats each; no fragment read or slab store
+  // touches a pad), so the table costs no LDS and the launch keeps four blocks per CU
+  static constexpr int IMG = Opnd<64, true, 16>::FLOATS, PITCH = Opnd<64, true, 16>::PITCH;
+  static_assert(PITCH == 80, "table stream: 16 pad columns per k-row");
+  // (PADS = false: the table follows the four images, entry r at 4 IMG + r - the launch then needs EXTRA_LDS)
+  __host__ __device__ static int slot(int r) { return PADS ? (r >> 9) * IMG + ((r >> 4) & 31) * PITCH + 64 + (r & 15) : 4 * IMG + r; }
   __device__ void init(const void* base, uint32_t bytes, int tid_, uint32_t row_off) {
     rs = buf_rsrc(base, bytes);
     tid = tid_;
@@ -713,7 +720,7 @@ struct TableK4Stream {
   }
   __device__ void load(int kbase, Regs& rg) const {
 #pragma unroll
-    for (int i = 0; i < N; ++i) rg[i] = buf_ld4(rs, vo + tbl[kbase + k0 + 16 * i + g], 0u);
+    for (int i = 0; i < N; ++i) rg[i] = buf_ld4(rs, vo + tbl[slot(kbase + k0 + 16 * i + g)], 0u);
   }
   __device__ void store(float* t, const Regs& rg) const {
 #pragma unroll
@@ -721,11 +728,17 @@ struct TableK4Stream {
   }
 };
 
-// a policy's extra LDS after the operand buffers (EXTRA_LDS bytes; the streams' prepare(ptr) fills it per tile)
+// a policy's LDS beyond its operand images (EXTRA_LDS bytes, after them)
 template <class P, class = void>
 struct ExtraLdsOf : std::integral_constant<size_t, 0> {};
 template <class P>
 struct ExtraLdsOf<P, std::void_t<decltype(P::EXTRA_LDS)>> : std::integral_constant<size_t, P::EXTRA_LDS> {};
+
+// streams with a per-tile prepare(lds, ns) (tables written into LDS before the slab loop)
+template <class S, class = void>
+struct HasPrepare : std::false_type {};
+template <class S>
+struct HasPrepare<S, std::void_t<decltype(std::declval<S&>().prepare((float*)nullptr, 0))>> : std::true_type {};
 
 template <class P>
 constexpr size_t gemm_lds_bytes() {
@@ -771,8 +784,8 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
   float* Bs1 = Bs0 + OB::FLOATS;
-  if constexpr (ExtraLdsOf<P>::value > 0) {   // the streams' per-tile LDS tables, complete before the first slab load
-    st.prepare(Bs1 + OB::FLOATS, ns);
+  if constexpr (HasPrepare<St>::value) {   // the streams' per-tile LDS tables, complete before the first slab load
+    st.prepare(lds, ns);
     __syncthreads();
   }
   Regs x0, x1;
@@ -1723,7 +1736,7 @@ using PConv2DgradS = PConv2DgradT<64, 32, 4, 1>;
 // conv2 / conv3 weight gradient over sample chunk z (samples [z SC, min(B, (z + 1) SC))): rows m = (kh, kw, c),
 // cols oc, r = (b, oh, ow) ascending; partial slab[z][M + 1][OC] (row M = bias partial)
 template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
-          int MF_ = 16>
+          int MF_ = 16, bool TPADS = true>
 struct PConvWgrad {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool LOAD_FENCE = false;   // (with the conv2 backward data's: conv2 pair 101.3 -> 99.8 us, w18)
@@ -1764,23 +1777,23 @@ struct PConvWgrad {
   static constexpr int T = WM_ * WN_ * 64;
   static constexpr int KMAX = (SC * P + BK - 1) / BK * BK;   // table entries: the chunk's r, padded to whole slabs
   struct StreamsImpl {
-    TableK4Stream<T> a;
+    TableK4Stream<T, TPADS> a;
     AffineStream<BN_, true, T, true> b;
     int z, rows;
     struct Regs {
-      typename TableK4Stream<T>::Regs a;
+      typename TableK4Stream<T, TPADS>::Regs a;
       typename AffineStream<BN_, true, T, true>::Regs b;
     };
     // the chunk's r -> byte offset of its im2col row base in `in` (kOob past the chunk)
-    __device__ void prepare(float* ext, int ns) {
-      uint32_t* t = reinterpret_cast<uint32_t*>(ext);
+    __device__ void prepare(float* lds, int ns) {
+      uint32_t* t = reinterpret_cast<uint32_t*>(lds);
       for (int r = a.tid; r < ns * BK; r += T) {
         uint32_t o = kOob;
         if (r < rows) {
           const int bl = r / P, pp = r - bl * P, oh = pp / OW, ow = pp - oh * OW;
           o = (uint32_t)((((z * SC + bl) * H + oh * S) * W + ow * S) * C) * 4u;
         }
-        t[r] = o;
+        t[TableK4Stream<T, TPADS>::slot(r)] = o;
       }
       a.tbl = t;
     }
@@ -1799,7 +1812,8 @@ struct PConvWgrad {
   // one path: the weight-gradient tiles then issue no per-slab address arithmetic)
   static constexpr bool STREAMED = BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4;
   using Streams = std::conditional_t<STREAMED, StreamsImpl, void>;
-  static constexpr size_t EXTRA_LDS = STREAMED ? (size_t)KMAX * 4 : 0;
+  static_assert(!TPADS || KMAX <= 4 * 32 * 16, "weight-gradient chunk: the offset table lives in the four images' pads");
+  static constexpr size_t EXTRA_LDS = STREAMED && !TPADS ? (size_t)KMAX * 4 : 0;
   template <class ST = Streams>
   __device__ ST streams(int z, int row0, int col0, int tid) const {
     ST st;
@@ -1822,7 +1836,8 @@ struct PConvWgrad {
 struct SideFc2 {
   static constexpr int BLOCKS = 33;   // 512 rows of a4^T + the ones row
   __host__ __device__ int blocks() const { return BLOCKS; }
-  static constexpr int HB = 512;      // samples per LDS pass (40 KB; 256 measured slower: 73.4 vs 71.2 us per fc1 backward)
+  static constexpr int HB = 512;      // samples per LDS pass (40 KB; 256 measured slower: 73.4 vs 71.2 us per fc1 backward,
+                                      // 61.9 vs 61.7 us on the stream core, gpurun_out/w23)
   static constexpr size_t LDS = (size_t)HB * 20 * sizeof(float);
   const float* a4;
   const uint8_t* act;
