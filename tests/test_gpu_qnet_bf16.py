@@ -2,11 +2,13 @@
 weights) vs the fp32 oracle.  The fp32 path (the reference's arithmetic) is bit-exact: tests/test_gpu_qnet32.py.
 
 Stated tolerances (bf16 operands carry 8 significant bits):
-  Q values / activations : max|gpu - ref| <= 3e-2 * max|ref| (+ tiny absolute floor)
-  kernel exactness       : gradients within 1e-2 relative L2 of tests/bf16_reference.py, which
+  Q values               : max|gpu - ref| <= 1.5e-2 * max|ref| (+ tiny absolute floor; measured <= 8.1e-3)
+  activations a1..a4     : max|gpu - ref| <= 3e-2 * max|ref|
+  kernel exactness       : gradients within 2e-3 relative L2 of tests/bf16_reference.py (measured <= 4.3e-4), which
                            rounds exactly where the product stores bf16 (weights, a1..a4, dz1..dz4)
-  gradients vs fp32      : relative L2 error <= 0.15 per variable and cosine >= 0.99 (bf16
-                           activation gradients compound through 3 layers: conv1 is the worst, ~0.1)
+  gradients vs fp32      : relative L2 error <= 0.13 per variable and cosine >= 0.992 (measured <= 0.115 / >= 0.9938:
+                           bf16 activation gradients compound through 3 layers)
+(round 4: tightened from Q 3e-2, exactness 1e-2, gradients 0.15 / 0.99 to the measured levels with margin)
   post-Adam weights      : |w_gpu - w_ref| <= 2e-3 * max|w0| (the step is ~lr = 2.5e-4 per element)
   loss                   : relative error <= 3e-2
 Initial weights (GlorotUniform from the build's Philox stream) are bit-identical.
@@ -77,7 +79,8 @@ def test_forward_parity(B, kind):
     x = env_states(B) if kind == "env" else rand_states(B, B, sparse=kind == "sparse")
     q, a = m.q_values(x)
     qr, acts = ref.forward(x, acts=True)
-    assert close(q, qr, 3e-2), (np.abs(q - qr).max(), np.abs(qr).max())
+    print(f"B={B} {kind}: Q err / max|Q| {np.abs(q - qr).max() / np.abs(qr).max():.2e}")
+    assert close(q, qr, 1.5e-2), (np.abs(q - qr).max(), np.abs(qr).max())
     # argmax agrees wherever the oracle's top-2 margin exceeds the tolerance
     srt = np.sort(qr, axis=1)
     margin = srt[:, -1] - srt[:, -2]
@@ -95,7 +98,7 @@ def test_batch_max_q_and_predict_action():
     x = env_states(32)
     mx = m.batch_predict_max_future_reward(x)
     qr = ref.forward(x)
-    assert close(mx, qr.max(axis=1), 3e-2)
+    assert close(mx, qr.max(axis=1), 1.5e-2)
     a = m.predict_action(x[0])
     assert a in (0, 1, 2)
 
@@ -119,7 +122,7 @@ def test_train_step_parity(B):
         g, ge = grads[v].ravel().astype(np.float64), grads_e[v].ravel()
         rel = np.linalg.norm(g - ge) / (np.linalg.norm(ge) + 1e-30)
         report.append(f"var{v}: emu rel {rel:.2e}")
-        assert rel <= 1e-2, "; ".join(report)
+        assert rel <= 2e-3, "; ".join(report)
     # (2) precision gap to the fp32 oracle (stated tolerance, module docstring)
     loss_r, grads_r, norms_r = ref.train(x, a, y)
     assert abs(loss - loss_r) <= 3e-2 * abs(loss_r)
@@ -128,7 +131,7 @@ def test_train_step_parity(B):
         rel = np.linalg.norm(g - gr) / (np.linalg.norm(gr) + 1e-30)
         cos = g @ gr / (np.linalg.norm(g) * np.linalg.norm(gr) + 1e-30)
         report.append(f"var{v}: fp32 rel {rel:.2e} cos {cos:.5f}")
-        assert rel <= 0.15 and cos >= 0.99, "; ".join(report)
+        assert rel <= 0.13 and cos >= 0.992, "; ".join(report)
         assert abs(norms[v] - norms_r[v]) <= 0.15 * norms_r[v]
     print("\n".join(report))
     # Adam's first step is lr * g/|g| (m/sqrt(v) at t = 1): weights move by exactly +-lr where the gradient
@@ -197,7 +200,7 @@ def test_large_batch_forward_paths_agree():
     assert d.max() <= 1e-2 * top and d.mean() <= 1e-4 * top, (d.max(), d.mean(), top)
     sl = slice(4000, 4064)
     qr = O.QNet(seed=3).forward(x[sl])
-    assert close(q_big[sl], qr, 3e-2)
+    assert close(q_big[sl], qr, 1.5e-2)
     srt = np.sort(q_chunks, axis=1)
     sure = srt[:, -1] - srt[:, -2] > 2e-2 * top
     assert np.array_equal(a_big[sure], np.argmax(q_chunks, axis=1)[sure])
