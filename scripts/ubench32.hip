@@ -511,6 +511,12 @@ int main(int argc, char** argv) {
            PConv2DgradPx<64, 128, 2, 2>{Grid{(B + 63) / 64, 1, 100}, dz2, W1, a1, dz1, B}, f2);
       run2("conv2 W64x64 Dpx64x32", Wg2{grid(512, 64, 64, 64, z), a1, dz2, slab, B},
            PConv2DgradPx<64, 32, 2, 2>{Grid{(B + 63) / 64, 4, 100}, dz2, W1, a1, dz1, B}, f2);
+      run2("conv2 W64x64 Dpx128x64", Wg2{grid(512, 64, 64, 64, z), a1, dz2, slab, B},
+           PConv2DgradPx<128, 64, 2, 2>{Grid{(B + 127) / 128, 2, 100}, dz2, W1, a1, dz1, B}, f2);
+      run2("conv3 W64x64 Dpx128x64", Wg3{grid(576, 64, 64, 64, z), a2, dz3, slab, B},
+           PConv3DgradPx<128, 64, 2, 2>{Grid{(B + 127) / 128, 1, 81}, dz3, W2, a2, dz2, B}, f3);
+      run2("fc1 W64x64 D128x64", PFc1WgradT<64, 64, 2, 2>{grid(3136, 64, 512, 64, 1), a3, dz4, gw, gw, B},
+           PFc1DgradT<128, 64, 2, 2>{grid(B, 128, 3136, 64, 1), dz4, W3, a3, dz3, B}, ff);
       run2("conv2 W64x32 Dpx64x64", Wg2{grid(512, 64, 64, 32, z), a1, dz2, slab, B},
            PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, W1, a1, dz1, B}, f2);
     }
