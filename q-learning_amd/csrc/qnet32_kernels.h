@@ -2239,7 +2239,8 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
     stage();
     __syncthreads();
     if (bl + 1 < nb) prefetch(b0 + bl + 1);
-#pragma unroll 10   // (2 / 4 / 10 / 20 / 25 / 50: 74.0 / 74.5 / 68.5 / 69.2 / 69.5 / 69.3 us at B = 1024, max-ILP scheduling)
+#pragma unroll 10   // (2 / 4 / 10 / 20 / 25 / 50: 74.0 / 74.5 / 68.5 / 69.2 / 69.5 / 69.3 us at B = 1024, max-ILP scheduling;
+                    // with the zero-step skip, round 4: 5 / 10 / 20 / 25: 44.0 / 43.0 / 49.0 / 49.3 us, gpurun_out/w29)
     for (int rs = 0; rs < 100; ++rs) {
       const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
       const float bv = dzs[r * 16 + l15];
