@@ -559,8 +559,8 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
 // weight-gradient chunk tiles 64 x 64 on 1 x 4 waves (each wave 64 rows x 16 channels): conv3 / conv2 pairs 73.0 -> 72.3 /
 // 102.2 -> 101.2 us in place against 2 x 2 (4 x 1: no change; gpurun_out/w14)
-// conv3's offset table after the images (3 blocks per CU: pair 72.2 us; in the images' pads, 4 per CU: 76.2 us, held to 3:
-// 81 us - gpurun_out/w22, w23); conv2's in the pads (4 blocks per CU: pair 99.6 -> 96.8 us)
+// conv3's offset table after the images (3 blocks per CU: pair 72.1 us; in the images' pads, 4 per CU: 76.1 us, held to 3
+// by a 44 KB LDS request: 73.1 us - gpurun_out/w22, w31); conv2's in the pads (4 blocks per CU: pair 99.6 -> 96.8 us)
 using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4, 16, false>;
 using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4>;
 
