@@ -660,12 +660,10 @@ static void launch(qlx_model* m, const P& p, const char* scope, double work, hip
   debug_sync(s, scope);
 }
 
-// blocks_per_cu > 0: the launch reserves 160 KB / blocks_per_cu of LDS per block, so at most that many blocks share a CU
 template <class P1, class P2, class S, class T = NoSide>
 static void launch_pair(qlx_model* m, const P1& p1, const P2& p2, const S& side, const char* scope, double work, hipStream_t s,
-                        const T& tail = T{}, int blocks_per_cu = 0) {
-  size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS, T::LDS});
-  if (blocks_per_cu > 0) lds = std::max(lds, (size_t)160 * 1024 / blocks_per_cu / 256 * 256);
+                        const T& tail = T{}) {
+  const size_t lds = std::max({gemm_lds_bytes<P1>(), gemm_lds_bytes<P2>(), S::LDS, T::LDS});
   hipEvent_t ea = nullptr, eb = nullptr;
   if (m->prof) m->prof->ext(scope, work, &ea, &eb);
   hipExtLaunchKernelGGL((k_gemm32_pair<P1, P2, S, T>), dim3(side.blocks() + p1.g.blocks() + p2.g.blocks() + tail.blocks()), dim3(256),
