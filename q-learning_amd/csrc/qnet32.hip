@@ -44,7 +44,7 @@ static int64_t voff(int v) {
 // the dz4 epilogue read them from there.  Row pitch 514 floats: a fragment read's 32-lane group (16 rows x 2 k) hits 32
 // distinct banks (ds_read_b32: 32 banks, (address / 4) mod 32); rows are 8-byte aligned, so stores / epilogue reads are b64.
 constexpr int kHeadPitch = 514;
-template <int MODE>
+template <int MODE, int HS = 16>   // HS samples per block (<= 16: rows past HS are MFMA padding)
 __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
   __shared__ f32x4 part[4][16];
   __shared__ float gsh[16];
@@ -53,16 +53,16 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
   __shared__ __attribute__((aligned(16))) float w4s[512 * 3];
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int s0 = blockIdx.x * 16;
+  const int s0 = blockIdx.x * HS;
   const int j = lane & 15, g = lane >> 4, n = lane & 15;
   const int b = s0 + j;
-  const bool valid = b < A.B;
+  const bool valid = j < HS && b < A.B;
   {   // stage: 16 rows x 128 float4 of a4 (8 per thread; rows past B read row s0) and W4's 384 float4
     f32x4 xr[8], wr[2];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int f = threadIdx.x + 256 * r, jj = f >> 7, k4 = f & 127;
-      xr[r] = ld4(A.a4f + (size_t)(s0 + jj < A.B ? s0 + jj : s0) * 512 + 4 * k4);
+      xr[r] = ld4(A.a4f + (size_t)(jj < HS && s0 + jj < A.B ? s0 + jj : s0) * 512 + 4 * k4);
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int f = threadIdx.x + 256 * r, jj = f >> 7, k = 4 * (f & 127), bb = s0 + jj;
-      if (bb < A.B) {
+      if (jj < HS && bb < A.B) {
         const f32x2* xp = reinterpret_cast<const f32x2*>(xs + jj * kHeadPitch + k);
         const f32x2 x01 = xp[0], x23 = xp[1];
         const float xa[4] = {x01[0], x01[1], x23[0], x23[1]};
@@ -822,12 +822,15 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
 }
 
 void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s) {
+  // the training head on 4 samples per block (MFMA rows 4..15 padding): 256 blocks at B = 1024 instead of 64, 8.7 -> 7.9 us
+  // (8 per block: 8.1 us; gpurun_out/w32); the chunk-size heads keep 16
+  constexpr int kHs3 = 4;
   const dim3 g((B + 15) / 16), blk(256);   // 16 samples per block
   switch (mode) {
     case 0: hipLaunchKernelGGL(k_head32<0>, g, blk, 0, s, a); break;
     case 1: hipLaunchKernelGGL(k_head32<1>, g, blk, 0, s, a); break;
     case 2: hipLaunchKernelGGL(k_head32<2>, g, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL(k_head32<3>, g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_head32<3, kHs3>), dim3((B + kHs3 - 1) / kHs3), blk, 0, s, a); break;
   }
   QLX_HIP(hipGetLastError());
   debug_sync(s, "k_head32");
