@@ -219,8 +219,10 @@ __global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
 // Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
 // [16 q, 16 q + 16)), S_q = chain over its chunks in order, dW = chain over q of S_q (each chain t = 0; t = t + x).
 // Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order, the last row of each the bias.
-// Block = 64 consecutive outputs x 16 group lanes (one wave per lane, 256-byte rows per load): wave g chains groups
-// g, g + 16, .. (16 partial loads in flight each); the group sums meet in LDS and wave 0 chains them.
+// Block = 16 waves = 16 / W slices of 64 consecutive outputs, W waves per slice (W = wv[L], the power of two >= the
+// segment's group count, at most 16; 256-byte rows per load): wave g of a slice chains groups g, g + W, .. (16 partial
+// loads in flight each); the group sums meet in LDS and the slice's wave 0 chains them in q order.  (One slice per block
+// left 12 of 16 waves idle at 64 chunks - conv2 / conv3 at B = 1024 - and held the CUs' wave slots.)
 constexpr int kWGroup = 16;
 constexpr int kWGroupsMax = 128;   // chunks <= 2,048 (conv1 at the largest fp32 batch, 8,192)
 struct WRed {
@@ -228,9 +230,17 @@ struct WRed {
   int nz[3];
   int count[3];   // (M + 1) * OC; segments 0 and 1 are multiples of 64
   int oc[3];
+  int wv[3];      // waves per 64-output slice
+  int nb[3];      // blocks of the segment
   float* gw[3];   // W gradient
   float* gb[3];   // b gradient
 };
+__host__ __device__ inline int wred_waves(int nz) {
+  const int ng = (nz + kWGroup - 1) / kWGroup;
+  int w = 1;
+  while (w < ng && w < 16) w *= 2;
+  return w;
+}
 // Blocks [nred, ..) of the launch (update schedule 2, qnet.h): clip-norm segment partials of segments seg0 .. seg0 + nseg
 // - the dense variables', final since the fc1 backward - four 256-thread groups per block, one k_norm32 block's
 // arithmetic each.
@@ -248,28 +258,29 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred
     if (tl == 0 && live) N.partial[sg] = __fadd_rn(__fadd_rn(__fadd_rn(gs[grp * 4], gs[grp * 4 + 1]), gs[grp * 4 + 2]), gs[grp * 4 + 3]);
     return;
   }
-  const int o = threadIdx.x & 63, g0 = threadIdx.x >> 6;
-  int e = blockIdx.x * 64;
-  int L = 0;
-  while (L < 3 && e >= R.count[L]) { e -= R.count[L]; ++L; }
+  int b = blockIdx.x, L = 0;
+  while (L < 3 && b >= R.nb[L]) { b -= R.nb[L]; ++L; }
   if (L >= 3) return;   // block-uniform
+  const int W = R.wv[L], o = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = wave / W, g0 = wave - sub * W;
+  const int e = (b * (16 / W) + sub) * 64;
   const bool live = e + o < R.count[L];
   const size_t stride = (size_t)R.count[L];
   const int nz = R.nz[L], ng = (nz + kWGroup - 1) / kWGroup;
-  const float* p = R.slab[L] + e + (live ? o : 0);
-  for (int q = g0; q < ng; q += 16) {
+  const float* p = R.slab[L] + (live ? e + o : 0);
+  float* gsub = gs + sub * ng * 64;   // (16 / W) * ng <= kWGroupsMax slices of 64
+  for (int q = g0; q < ng; q += W) {
     float v[kWGroup];
 #pragma unroll
     for (int j = 0; j < kWGroup; ++j) v[j] = q * kWGroup + j < nz ? p[(size_t)(q * kWGroup + j) * stride] : 0.0f;
     float t = 0.0f;
 #pragma unroll
     for (int j = 0; j < kWGroup; ++j) t = __fadd_rn(t, v[j]);   // + 0 past the last chunk leaves t unchanged
-    gs[q * 64 + o] = t;
+    gsub[q * 64 + o] = t;
   }
   __syncthreads();
   if (g0 != 0 || !live) return;
   float t = 0.0f;
-  for (int q = 0; q < ng; ++q) t = __fadd_rn(t, gs[q * 64 + o]);
+  for (int q = 0; q < ng; ++q) t = __fadd_rn(t, gsub[q * 64 + o]);
   const int oc = R.oc[L], m = (e + o) / oc, n = (e + o) - m * oc;
   const int M = R.count[L] / oc - 1;
   if (m == M) R.gb[L][n] = t;
@@ -939,10 +950,15 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     R.slab[0] = w.fslab3; R.nz[0] = z3; R.count[0] = 577 * 64; R.oc[0] = 64; R.gw[0] = G + voff(4); R.gb[0] = G + voff(5);
     R.slab[1] = w.fslab2; R.nz[1] = z2; R.count[1] = 513 * 64; R.oc[1] = 64; R.gw[1] = G + voff(2); R.gb[1] = G + voff(3);
     R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
-    const int total = R.count[0] + R.count[1] + R.count[2];
     QLX_CHECK(std::max({z1, z2, z3}) <= kWGroup * kWGroupsMax, QLX_E_INVALID, "too many weight-gradient chunks");
+    int nred = 0;
+    for (int L = 0; L < 3; ++L) {
+      R.wv[L] = wred_waves(R.nz[L]);
+      const int per = 64 * (16 / R.wv[L]);
+      R.nb[L] = (R.count[L] + per - 1) / per;
+      nred += R.nb[L];
+    }
     // the scheduled update: + the dense variables' clip-norm segment partials (4 per block)
-    const int nred = (total + 63) / 64;
     const int dseg = m->f32_update_scheduled ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
     hipLaunchKernelGGL(k_wreduce32, dim3(nred + (dseg + 3) / 4), dim3(1024), 0, s, R, N, nred, N.seg_first[6], dseg);
     QLX_HIP(hipGetLastError());

@@ -764,7 +764,6 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   using OA = Opnd<P::BM, P::A_KMAJ, MF>;
   using OB = Opnd<P::BN, P::B_KMAJ, MF>;
   using Acc = f32x4;
-  constexpr int T = P::WM * P::WN * 64;
   constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
   static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
   using St = typename P::Streams;

@@ -6,8 +6,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-q}
 rm -rf "$OUT" && mkdir -p "$OUT"
-K=${2:+-k "$2"}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K > "$OUT/gputest.log" 2>&1 || exit 1
+K=()
+[ -n "$2" ] && K=(-k "$2")
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > "$OUT/gputest.log" 2>&1 || exit 1
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
 timeout -k 10 500 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
 exit 0
