@@ -83,6 +83,12 @@ def parse():
     ap.add_argument("--dense-steps", type=int, default=5,
                     help="fp32: timed vector steps of a learner built with the exact zero skips off (QLX_F32_BG=0 "
                          "QLX_F32_C1_SKIP=0: every conv1 step and conv2 / conv3 row computed; 0 = skip)")
+    ap.add_argument("--refwork-steps", type=int, default=5,
+                    help="fp32: timed vector steps doing the reference's work - the target net per sampled batch AND the "
+                         "exact zero skips off (QLX_TARGET_CACHE=0 QLX_F32_BG=0 QLX_F32_C1_SKIP=0; 0 = skip)")
+    ap.add_argument("--dp1-steps", type=int, default=5,
+                    help="one GPU: timed vector steps of the data-parallel update path on a single-rank RCCL communicator "
+                         "(bucketed all-reduce + the DP update tail; the cost C4 pays per rank besides the link; 0 = skip)")
     ap.add_argument("--sparsity-steps", type=int, default=8,
                     help="fp32: untimed vector steps after the timed window, each reporting the fractions of conv work "
                          "the skips left out (qlx_learner_frame_sparsity)")
@@ -217,7 +223,7 @@ def rate(work, us, div):
 class Run:
     """One learner measured on the steady-state workload."""
 
-    def __init__(self, args, ctl, precision, steps, warmup, flags, sparsity_steps=0):
+    def __init__(self, args, ctl, precision, steps, warmup, flags, sparsity_steps=0, dp1=False):
         import qlx
         self.args, self.ctl, self.precision = args, ctl, precision
         N, B = args.envs, args.batch
@@ -232,6 +238,8 @@ class Run:
             if ctl.world > 1:
                 uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
                 L.dist_init(ctl.world, ctl.rank, uid)
+            elif dp1:   # a single-rank communicator: the data-parallel update path on one GPU
+                L.dist_init(1, 0, qlx.dist_unique_id())
             self.rccl_world = L.comm_size()   # read back from the communicator (ncclCommCount)
             # steady state: replay at capacity and past the pure-random phase, whatever --warmup is
             prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
@@ -469,6 +477,20 @@ def control_check(ctl):
         print(json.dumps(out), flush=True)
 
 
+def run_with_env(env, *a, **kw):
+    """A Run with some QLX_* switches set while its learner is built (the switches are read per model / learner)."""
+    prev = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Run(*a, **kw)
+    finally:
+        for k, v in prev.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
 def main():
     args = parse()
     if args.no_target_memo:
@@ -488,29 +510,21 @@ def main():
     nomemo = None
     if args.nomemo_steps > 0 and "target_memo" in head.comps:
         # the reference's per-batch target work (same values, tests/test_gpu_learner.py), measured in this run
-        prev = os.environ.get("QLX_TARGET_CACHE")
-        os.environ["QLX_TARGET_CACHE"] = "0"
-        try:
-            nomemo = Run(args, ctl, args.precision, args.nomemo_steps, 1, flags)
-        finally:
-            if prev is None:
-                del os.environ["QLX_TARGET_CACHE"]
-            else:
-                os.environ["QLX_TARGET_CACHE"] = prev
+        nomemo = run_with_env({"QLX_TARGET_CACHE": "0"}, args, ctl, args.precision, args.nomemo_steps, 1, flags)
         assert "target_memo" not in nomemo.comps
     dense = None
     if f32 and args.dense_steps > 0:
         # the same loop on a learner built with the exact zero skips off (every conv1 step, every conv2 / conv3 row)
-        prev = {k: os.environ.get(k) for k in ("QLX_F32_BG", "QLX_F32_C1_SKIP")}
-        os.environ.update({"QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"})
-        try:
-            dense = Run(args, ctl, "fp32", args.dense_steps, 1, flags)
-        finally:
-            for k, v in prev.items():
-                if v is None:
-                    del os.environ[k]
-                else:
-                    os.environ[k] = v
+        dense = run_with_env({"QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"}, args, ctl, "fp32", args.dense_steps, 1, flags)
+    refwork = None
+    if f32 and args.refwork_steps > 0 and not args.no_target_memo:
+        # the reference's whole work: the target forward per sampled batch and every dense conv step / row
+        refwork = run_with_env({"QLX_TARGET_CACHE": "0", "QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"}, args, ctl, "fp32",
+                               args.refwork_steps, 1, flags)
+        assert "target_memo" not in refwork.comps
+    dp1 = None
+    if ctl.world == 1 and args.dp1_steps > 0:
+        dp1 = Run(args, ctl, args.precision, args.dp1_steps, 1, flags, dp1=True)
     other = "bf16" if args.precision == "fp32" else "fp32"
     beside = Run(args, ctl, other, args.beside_steps, 1, flags) if args.beside_steps > 0 else None
     # the measured window is the steady-state loop: greedy acting and episode ends inside it
@@ -579,6 +593,32 @@ def main():
             "note": "fp32 with the exact zero skips off (QLX_F32_BG=0 QLX_F32_C1_SKIP=0, a learner built so in this run): "
                     "every conv1 MFMA step and every conv2 / conv3 row computed - the rate on frames without black "
                     "background; bit-identical results (tests/test_gpu_qnet32_paths.py)"}
+    if refwork is not None:
+        line["value_reference_work"] = round(refwork.value(), 1)
+        line["reference_work"] = {
+            "value": round(refwork.value(), 1), "unit": "env-steps/s", "steps": refwork.steps,
+            "ms_per_step": round(refwork.dt / refwork.steps * 1e3, 3),
+            "grad_updates_per_sec": round(refwork.updates / refwork.dt, 2),
+            "note": "fp32 doing the reference's whole work: the frozen target net evaluated per sampled batch (no memo) AND the "
+                    "exact zero skips off (QLX_TARGET_CACHE=0 QLX_F32_BG=0 QLX_F32_C1_SKIP=0, a learner built so in this "
+                    "run); identical results"}
+    if dp1 is not None:
+        def per_update(run, names):
+            return {n: round(run.comps[n]["avg_us"], 2) for n in names if n in run.comps}
+        tail_plain = ("f32_wgrad_reduce", "f32_adam") if f32 else ("wgrad_reduce", "adam")
+        tail_dp = ("allreduce_dense", "f32_norms", "allreduce_conv", "f32_wgrad_reduce", "f32_adam") if f32 else \
+            ("allreduce_dense", "allreduce_conv", "wgrad_reduce", "norms", "adam")
+        line["value_dp_single_rank"] = round(dp1.value(), 1)
+        line["dp_single_rank"] = {
+            "value": round(dp1.value(), 1), "unit": "env-steps/s", "steps": dp1.steps,
+            "ms_per_step": round(dp1.dt / dp1.steps * 1e3, 3), "vs_plain": round(dp1.value() / head.value(), 4),
+            "rccl_world": dp1.rccl_world,
+            "per_update_us_event_timed": {"dp": per_update(dp1, tail_dp), "plain": per_update(head, tail_plain)},
+            "note": "the same workload with the learner on a single-rank RCCL communicator (qlx_learner_dist_init(1, 0)): "
+                    "the data-parallel update path - dense bucket all-reduced on the communicator stream beside the conv "
+                    "backward, its clip-norm partials after it there, conv bucket all-reduced on the learner stream, the "
+                    "k_update32 tail - whose per-rank cost C4 pays besides the xGMI transfer; bit-identical to the plain "
+                    "path at world 1 (tests/test_gpu_learner.py)"}
     if head.sparsity is not None:
         line["skipped_fractions"] = head.sparsity
     if beside is not None:
@@ -586,6 +626,9 @@ def main():
             "value": round(beside.value(), 1), "unit": "env-steps/s", "steps": beside.steps,
             "ms_per_step": round(beside.dt / beside.steps * 1e3, 3),
             "grad_updates_per_sec": round(beside.updates / beside.dt, 2), "roofline": beside.roofline(),
+            "mfma_per_layer": beside.report()["mfma_per_layer"],
+            "components_event_timed": {k: {"avg_us": round(v["avg_us"], 2), "launches_per_step": round(v["launches_per_step"], 2)}
+                                       for k, v in sorted(beside.comps.items(), key=lambda kv: -kv[1]["total_us_per_step"])},
             "note": "bf16 MFMA operands, fp32 accumulation and master weights: the labelled fast path, not the reference's "
                     "arithmetic; its tolerance contract vs the fp32 oracle (DESIGN.md §6, tests/test_gpu_qnet_bf16.py): Q "
                     "<= 1.5e-2 and activations <= 3e-2 max|ref|, loss <= 3e-2 relative, per-variable gradients relative "

@@ -186,7 +186,9 @@ typedef struct qlx_params { /* Parameter (self_driving_tf_q_learner.rs:20-67) + 
   char checkpoint_file[256];   /* write_checkpoint target of those events and of solved() (empty = not written) */
   float episode_reward_goal;   /* goal solved() tests (Environment::episode_reward_goal_mean, prelude.rs); NaN (the
                                   qlx_params_default value) = the env's own (Breakout: bricks - 1,
-                                  breakout_environment.rs:203-206); any other value, 0 included, mocks it */
+                                  breakout_environment.rs:203-206); any other value, 0 included, mocks it.
+                                  ABI semantics change in round 4: 0 used to select the env's goal; a zero-filled
+                                  struct now mocks a goal of 0 (qlx_learner_create warns on stderr) */
 } qlx_params;
 
 #define QLX_PREC_F32 0u
@@ -241,7 +243,8 @@ int32_t qlx_learner_last(qlx_learner* l, uint8_t* actions, float* rewards, uint8
 int32_t qlx_learner_priorities(qlx_learner* l, float* is_weights, float* leaves, float* per_max);
 /* Frame sparsity of the last vector step (diagnostic, not on the hot path; synchronises): the fractions of the fp32
  * conv work the exact zero skips leave out, in the kernels' own units - out[0..3] over the step's sampled training
- * states (NaN when the step ran no update), out[4..7] over the acting frames, each {conv1 forward all-zero steps,
+ * states (NaN when the step ran no update), out[4..7] over the current acting frames (the observations the next
+ * vector step acts on: after this step's env step and resets), each {conv1 forward all-zero steps,
  * conv1 weight-gradient all-zero steps, conv2 background rows, conv3 background rows}. */
 int32_t qlx_learner_frame_sparsity(qlx_learner* l, double* out);
 /* Learning statistics (learning_update_log, self_driving_tf_q_learner.rs:235-273): per-action counts over the

@@ -24,6 +24,7 @@ void generate_distinct_random_ids(uint64_t seed, uint32_t update_idx, uint32_t r
 }
 
 float det_powf(float xf, float yf) {
+  if (std::isnan(yf)) return NAN;   // a NaN exponent: NaN on both sides (no rint of NaN below)
   if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : (yf < 0.0f ? INFINITY : 1.0f)) : NAN;
   if (std::isinf(xf)) return yf > 0.0f ? INFINITY : (yf < 0.0f ? 0.0f : 1.0f);
   int e = 0;

@@ -1,0 +1,300 @@
+// bf16 GEMM core of the bf16 fast path (round 5): the dense layer fc1 (3136 <-> 512) forward, backward data and weight
+// gradient (qnet.hip), replacing the register-staged 128 x 128 core of gemm_kernels.h.
+//
+//   C[m][n] = sum_k A(m, k) B(n, k), fp32 accumulation on v_mfma_f32_16x16x32_bf16 (16 cycles per MFMA per SIMD).
+//   Operands in global memory: row-major  [rows][ld], k contiguous   (KM = false)
+//                              k-major    [K][ld], rows contiguous  (KM = true)
+//   fc1 forward  : A = a3 [B][ld] row-major          B = W3 [3136][512] k-major (the Keras [in][out] layout)
+//   fc1 dgrad    : A = dz4 [B][512] row-major        B = W3 [3136][512] row-major (n = in, k = out)
+//   fc1 wgrad    : A = a3 [B][ld] k-major (k = b)    B = dz4 [B][512] k-major; a3's pitch ld > 3136 holds a column of
+//                  ones at 3136, so output row 3136 is db3 (the bias gradient rides along as one more row of dW3)
+//
+// Why this shape (MI355X_MICROARCH.md §LDS, cdna_hip_programming.md §5):
+// - operands reach LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`, 1 KB per wave instruction): no VGPR staging and no
+//   ds_write pass (ds_write_b128 moves ~79 B/clk per CU, which is what bounded the old core's k-steps), and the buffer
+//   descriptor's range check turns rows / k-rows past the operand into zeros (ragged M, N and K need no branches);
+// - a 3-stage LDS ring, BK = 32: k-step t + 2 is in flight while t is multiplied; one raw s_barrier per k-step and a
+//   counted `s_waitcnt vmcnt` (never __syncthreads, whose fence would drain the DMA in flight);
+// - MFMA fragments come from LDS conflict-free: row-major images [rows][32] (64-byte rows) read with ds_read_b128 under
+//   the chunk XOR swz_r(r) = ((r >> 3) & 1) * 2; k-major images [32][rows] read with two ds_read_b64_tr_b16 per fragment
+//   (the transpose on read) under the chunk XOR of k-row kr: s128(kr) = 2 ((kr & 3) | ((kr & 8) >> 1)) for 128-row
+//   images, s64(kr) = 2 (((kr >> 1) & 1) | ((kr >> 3) & 1) << 1) for 64-row ones.  The DMA writes each wave
+//   instruction's 1 KB linearly, so the permutation is applied on the SOURCE address (each lane fetches the chunk that
+//   belongs at its linear LDS slot; the permutation stays inside one row / k-row, so coalescing is unchanged) and the
+//   same XOR on the read (cdna_hip_programming.md §5.4 rule 21).  scripts/bgemm_banks.py checks both layouts;
+// - the MFMA computes C^T (B fragment as the A operand), so each lane ends with 4 consecutive n of one m: the epilogues
+//   of gemm_kernels.h (Epi4*) move 16 bytes (fp32) or 8 bytes (bf16) per access.
+// Requirements (host-checked): row-major operands have K % 32 == 0; every split's k range is a multiple of 32 but the last.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gemm_kernels.h"
+#include "qnet_kernels.h"
+
+namespace qlx {
+namespace qn {
+
+struct BOp {
+  const bf16* p;
+  int ld;     // elements between rows (row-major) or k-rows (k-major)
+  int rows;   // valid rows (M for A, N for B)
+};
+
+template <int BM_, int BN_, int WM_, int WN_, bool AK_, bool BKM_>
+struct BGemmCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NW = WM_ * WN_, T = NW * 64;
+  static constexpr int BK = 32, S = 3;
+  static constexpr bool AK = AK_, BKM = BKM_;
+  static constexpr int TM = BM / WM, TN = BN / WN;   // wave tile
+  static constexpr int FM = TM / 16, FN = TN / 16;   // 16 x 16 MFMA tiles per wave
+  static constexpr int ABYTES = BM * BK * 2, BBYTES = BN * BK * 2, STAGE = ABYTES + BBYTES;
+  static constexpr size_t LDS = (size_t)S * STAGE;
+  static constexpr int LA = ABYTES / 1024, LB = BBYTES / 1024;   // 1 KB DMA instructions per stage and operand
+  static constexpr int LPA = LA / NW, LPB = LB / NW;              // per wave
+  static_assert(LA % NW == 0 && LB % NW == 0, "every wave issues the same DMA count per operand");
+  static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile of whole 16 x 16 MFMA tiles");
+  static_assert(!AK || BM == 64 || BM == 128, "k-major images are 64 or 128 rows");
+  static_assert(!BKM || BN == 64 || BN == 128, "k-major images are 64 or 128 rows");
+};
+
+template <class Epi>
+struct BGemmProblem {
+  BOp A, B;
+  int M, N, K, kps;   // kps: k per split (a multiple of 32)
+  int ones_m;         // kSq epilogues: the output row whose square sum goes to its own partial (a bias row), or -1
+  int tiles_m, tiles_n, splits;
+  int n_fastest;      // tile order: n fastest (the tiles of one m-panel adjacent) or m fastest
+  Epi epi;
+  __host__ __device__ int tiles() const { return tiles_m * tiles_n * splits; }
+};
+
+// chunk XOR of row-major (64-byte-row) images and of k-major images by their row count
+__device__ __forceinline__ int bswz_r(int r) { return ((r >> 3) & 1) * 2; }
+template <int BR>
+__device__ __forceinline__ int bswz_k(int kr) {
+  if constexpr (BR == 128) return 2 * ((kr & 3) | ((kr & 8) >> 1));
+  else return 2 * (((kr >> 1) & 1) | (((kr >> 3) & 1) << 1));
+}
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+// One operand's DMA and fragment addressing inside a tile.  Instruction j of this wave covers image bytes
+// [1024 (wave + NW j), + 1024).
+template <bool KM, int BR, int NW, int LP>
+struct BStage {
+  uint32_t voff[LP];   // per-lane source byte offsets (k0 = 0); kOobOffset for rows past the operand
+  int first;           // this wave's first instruction index
+  __device__ void init(const BOp& o, int row0, int wave, int lane) {
+    first = wave;
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      const int ii = wave + NW * j;
+      if constexpr (!KM) {   // 16 rows of 64 bytes per instruction
+        const int r = ii * 16 + (lane >> 2), gc = (lane & 3) ^ bswz_r(r);
+        voff[j] = row0 + r < o.rows ? (uint32_t)(((row0 + r) * o.ld + 8 * gc) * 2) : (uint32_t)kOobOffset;
+      } else {   // 1024 / (2 BR) k-rows per instruction
+        constexpr int CPR = BR / 8;   // 16-byte chunks per k-row
+        const int kr = ii * (64 / CPR) + lane / CPR, gc = (lane % CPR) ^ bswz_k<BR>(kr);
+        const int row = row0 + 8 * gc;
+        voff[j] = row < o.rows ? (uint32_t)((kr * o.ld + row) * 2) : (uint32_t)kOobOffset;
+      }
+    }
+  }
+  // issue this wave's DMA of k-step k0 into the operand image at img (LDS byte address of the image)
+  __device__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t soff, char* img) const {
+#pragma unroll
+    for (int j = 0; j < LP; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)(img + 1024 * (first + NW * j)), 16, voff[j], soff, 0, 0);
+  }
+};
+
+// fragment read addresses (byte offsets inside an operand image) for fragment f of a wave whose rows start at r0
+template <bool KM, int BR>
+__device__ __forceinline__ int bfrag_off(int r0, int f, int lane) {
+  const int rb = r0 + 16 * f;
+  if constexpr (!KM) {
+    const int r = rb + (lane & 15);
+    return r * 64 + 16 * ((lane >> 4) ^ bswz_r(r));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, kr = 8 * g + q;
+    const int c = (rb >> 3) + (p >> 1);
+    return kr * (BR * 2) + 16 * (c ^ bswz_k<BR>(kr)) + 8 * (p & 1);
+  }
+}
+
+// The fragment reads are inline asm: the compiler's wait-count pass makes every LDS read it can see wait for all LDS-DMA in
+// flight (s_waitcnt vmcnt(0) before the first ds_read of each k-step - measured in the .s of this core), which would
+// drain the ring each step.  The asm reads are invisible to it, so the kernel counts lgkmcnt itself (bfrag_wait) and
+// fences the MFMAs behind each wait with a scheduling barrier (cdna_hip_programming.md §5.4 rule 18).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <bool KM>
+constexpr int bfrag_insts() { return KM ? 2 : 1; }   // LDS instructions per fragment
+// addr: the fragment's lane address inside the operand image (VGPR); OFF: the image's byte offset in LDS (immediate)
+template <bool KM, int BR, int OFF>
+__device__ __forceinline__ bf16x8 bfrag_read(uint32_t addr) {
+  static_assert(OFF + 4 * BR * 2 < 65536, "ds offset field");
+  if constexpr (!KM) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return __builtin_bit_cast(bf16x8, r);
+  } else {
+    u32x2 v0, v1;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v0) : "v"(addr), "n"(OFF));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(addr), "n"(OFF + 4 * BR * 2));
+    return __builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]});
+  }
+}
+template <int N>
+__device__ __forceinline__ void bfrag_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_impl(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F f) { static_for_impl<0, N>(f); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One output tile (m-panel, n-panel, k split) of problem P; lds = the block's dynamic LDS (C::LDS bytes).
+template <class C, class Epi>
+__device__ __forceinline__ void bgemm_tile(const BGemmProblem<Epi>& P, int tile, char* lds) {
+  const int mn = tile % (P.tiles_m * P.tiles_n), bz = tile / (P.tiles_m * P.tiles_n);
+  const int bx = P.n_fastest ? mn / P.tiles_n : mn % P.tiles_m;
+  const int by = P.n_fastest ? mn % P.tiles_n : mn / P.tiles_m;
+  const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
+  const int wm = wave / C::WN, wn = wave - wm * C::WN;
+  const int m0 = bx * C::BM, n0 = by * C::BN;
+  const int kb = bz * P.kps, ke = min(P.K, kb + P.kps);
+  const int nk = (ke - kb + C::BK - 1) / C::BK;
+  // descriptor ranges: row-major operands [rows][ld], k-major ones [K][ld] (k-rows past K read zeros)
+  const __amdgpu_buffer_rsrc_t rA =
+      make_rsrc(P.A.p, (uint32_t)((C::AK ? P.K : P.A.rows) * P.A.ld * 2));
+  const __amdgpu_buffer_rsrc_t rB =
+      make_rsrc(P.B.p, (uint32_t)((C::BKM ? P.K : P.B.rows) * P.B.ld * 2));
+  BStage<C::AK, C::BM, C::NW, C::LPA> sa;
+  BStage<C::BKM, C::BN, C::NW, C::LPB> sb;
+  sa.init(P.A, m0, wave, lane);
+  sb.init(P.B, n0, wave, lane);
+  const uint32_t stepA = C::AK ? (uint32_t)(C::BK * P.A.ld * 2) : (uint32_t)(C::BK * 2);
+  const uint32_t stepB = C::BKM ? (uint32_t)(C::BK * P.B.ld * 2) : (uint32_t)(C::BK * 2);
+  const uint32_t baseA = C::AK ? (uint32_t)(kb * P.A.ld * 2) : (uint32_t)(kb * 2);
+  const uint32_t baseB = C::BKM ? (uint32_t)(kb * P.B.ld * 2) : (uint32_t)(kb * 2);
+  auto issue = [&](int t, int stage) {
+    char* st = lds + stage * C::STAGE;
+    sa.issue(rA, baseA + (uint32_t)t * stepA, st);
+    sb.issue(rB, baseB + (uint32_t)t * stepB, st + C::ABYTES);
+  };
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  uint32_t offA[C::FM], offB[C::FN];
+#pragma unroll
+  for (int f = 0; f < C::FM; ++f) offA[f] = lds_base + bfrag_off<C::AK, C::BM>(wm * C::TM, f, lane);
+#pragma unroll
+  for (int f = 0; f < C::FN; ++f) offB[f] = lds_base + bfrag_off<C::BKM, C::BN>(wn * C::TN, f, lane);
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  constexpr int LPW = C::LPA + C::LPB;
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  auto step = [&](auto stage_c, int t) {
+    constexpr int stage = decltype(stage_c)::value;
+    // k-step t has landed (this wave's part; t + 1 may stay in flight), then every wave's part (barrier).  The barrier
+    // also retires every wave's reads of step t - 1, whose stage the DMA of step t + 2 overwrites next.
+    if (t + 1 < nk) wait_vm<LPW>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) issue(t + 2, (stage + 2) % 3);
+    bf16x8 fa[C::FM], fb[C::FN];
+#pragma unroll
+    for (int f = 0; f < C::FM; ++f) fa[f] = bfrag_read<C::AK, C::BM, stage * C::STAGE>(offA[f]);
+#pragma unroll
+    for (int f = 0; f < C::FN; ++f) fb[f] = bfrag_read<C::BKM, C::BN, stage * C::STAGE + C::ABYTES>(offB[f]);
+    // column j of MFMAs waits for the A fragments and B_0 .. B_j (the reads retire in issue order); the last wait is
+    // lgkmcnt(0), so this step's LDS reads are complete before the next barrier releases the DMA that reuses the stage
+    constexpr int IB = bfrag_insts<C::BKM>();
+    static_assert(C::FM * bfrag_insts<C::AK>() + C::FN * IB <= 15, "lgkmcnt counts to 15");
+    auto col = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      bfrag_wait<(C::FN - 1 - j) * IB>();
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    };
+    static_for<C::FN>(col);
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  int t = 0;
+  for (; t + 3 <= nk; t += 3) {
+    step(S0{}, t);
+    step(S1{}, t + 1);
+    step(S2{}, t + 2);
+  }
+  if (t < nk) {
+    step(S0{}, t);
+    if (t + 1 < nk) step(S1{}, t + 1);
+  }
+  // C^T fragments: lane & 15 = m, registers = 4 consecutive n starting at 4 (lane >> 4)
+  const Epi& epi = P.epi;
+  float sq_main = 0.0f, sq_ones = 0.0f;
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) {
+    const int m = m0 + wm * C::TM + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+      const int n = n0 + wn * C::TN + 16 * j + 4 * (lane >> 4);
+      if (m < P.M && n < P.N) {
+        epi(m, n, acc[i][j], bz);
+        if constexpr (Epi::kSq) {
+          const float q = sq4(acc[i][j]);
+          if (m == P.ones_m) sq_ones = __fadd_rn(sq_ones, q);
+          else sq_main = __fadd_rn(sq_main, q);
+        }
+      }
+    }
+  }
+  if constexpr (Epi::kSq) {
+    if (epi.sq) {   // fixed-order block reduction: xor butterfly per wave, then the waves in order
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        sq_main += __shfl_xor(sq_main, off);
+        sq_ones += __shfl_xor(sq_ones, off);
+      }
+      float* red = reinterpret_cast<float*>(lds);
+      __syncthreads();   // every wave is past its last LDS read of the k loop
+      if (lane == 0) { red[2 * wave] = sq_main; red[2 * wave + 1] = sq_ones; }
+      __syncthreads();
+      if (tid == 0) {
+        float a = red[0], b = red[1];
+        for (int w = 1; w < C::NW; ++w) { a += red[2 * w]; b += red[2 * w + 1]; }
+        epi.sq[tile] = a;
+        epi.sq[P.tiles() + tile] = b;
+      }
+    }
+  }
+}
+
+template <class C, class Epi>
+__global__ __launch_bounds__(C::T, 2) void k_bgemm(BGemmProblem<Epi> P, int remap) {
+  extern __shared__ __attribute__((aligned(16))) char bg_lds[];
+  const int t = remap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  if (t < P.tiles()) bgemm_tile<C>(P, t, bg_lds);
+}
+
+}  // namespace qn
+}  // namespace qlx

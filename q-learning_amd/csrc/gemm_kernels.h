@@ -129,15 +129,16 @@ struct Epi4BiasRelu {   // out[m][n] = relu(v + bias[n]) as bf16
   }
 };
 
-struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16
+struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16 (act rows act_ld apart)
   static constexpr bool kSq = false;
   bf16* out;
   const bf16* act;
   int ldo;
+  int act_ld;
   __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int) const {
     const size_t i = (size_t)m * ldo + n;
     typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-    const bf16x4v a = *reinterpret_cast<const bf16x4v*>(act + i);
+    const bf16x4v a = *reinterpret_cast<const bf16x4v*>(act + (size_t)m * act_ld + n);
     *reinterpret_cast<uint2*>(out + i) = pack4((float)a[0] > 0.0f ? v[0] : 0.0f, (float)a[1] > 0.0f ? v[1] : 0.0f,
                                                (float)a[2] > 0.0f ? v[2] : 0.0f, (float)a[3] > 0.0f ? v[3] : 0.0f);
   }

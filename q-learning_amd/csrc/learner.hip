@@ -401,6 +401,9 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
     // communicator stream as soon as the fc1 backward produced it, overlapping the conv backward; the conv bucket
     // follows on the learner stream once the dense reduction is done (so the two collectives of the communicator
     // never run at the same time and keep one order on every rank).  Adam then sees both.
+    // fp32: the dense variables' clip-norm partials of the reduced bucket follow it on the communicator stream (they read
+    // the dense gradient only), so the update tail on the learner stream is the conv all-reduce + k_update32
+    scale = 1.0f / (float)L->world;
     model_backward_dense(on, (int)B, bact, L->d_targets + (size_t)u_local * B, L->d_losses + u_local, s, isw, td);
     QLX_HIP(hipEventRecord(L->ev_dense, s));
     QLX_HIP(hipStreamWaitEvent(L->comm_stream, L->ev_dense, 0));
@@ -411,6 +414,7 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
                                            ncclFloat, ncclSum, L->comm, L->comm_stream);
       QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     }
+    if (on->f32) model_norms(on, L->comm_stream, scale);
     QLX_HIP(hipEventRecord(L->ev_reduced, L->comm_stream));
     model_backward_conv(on, tab_s, (int)B, s);
     QLX_HIP(hipStreamWaitEvent(s, L->ev_reduced, 0));
@@ -419,7 +423,10 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
       const ncclResult_t r = ncclAllReduce(on->d_grads, on->d_grads, (size_t)off_dense, ncclFloat, ncclSum, L->comm, s);
       QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     }
-    scale = 1.0f / (float)L->world;
+    if (!on->f32) model_norms(on, s, scale);
+    model_adam(on, s, scale);
+    L->update_count += 1;
+    return;
   }
   model_norms(on, s, scale);
   model_adam(on, s, scale);
@@ -573,8 +580,14 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
     QLX_CHECK(p->qnet_precision == QLX_PREC_F32 || p->qnet_precision == QLX_PREC_BF16, QLX_E_INVALID, "unknown qnet_precision");
     QLX_CHECK(p->qnet_precision == QLX_PREC_BF16 || p->batch_size <= (uint32_t)kF32FwdChunk, QLX_E_INVALID,
               "fp32 batch_size above the forward chunk");
-    QLX_CHECK(!(p->flags & QLX_LEARNER_PER) || (p->per_alpha >= 0.0f && p->per_beta >= 0.0f && p->per_eps > 0.0f),
-              QLX_E_INVALID, "prioritized replay needs alpha >= 0, beta >= 0, eps > 0");
+    QLX_CHECK(!(p->flags & QLX_LEARNER_PER) || (std::isfinite(p->per_alpha) && std::isfinite(p->per_beta) && std::isfinite(p->per_eps) &&
+                                                 p->per_alpha >= 0.0f && p->per_beta >= 0.0f && p->per_eps > 0.0f),
+              QLX_E_INVALID, "prioritized replay needs finite alpha >= 0, beta >= 0, eps > 0");
+    // ABI note (round 4): NaN, not 0, selects the env's own goal.  A caller that zero-fills the struct instead of starting
+    // from qlx_params_default would mock a goal of 0, which any Breakout episode reaches: say so once.
+    if (p->episode_reward_goal == 0.0f)
+      std::fprintf(stderr, "qlx_learner_create: episode_reward_goal is 0 - a mocked goal of 0 (NaN selects the env's own goal; "
+                           "start from qlx_params_default)\n");
     current_device_checked(device);
     auto* L = new qlx_learner;
     try {   // a failure part-way releases what was built
@@ -854,7 +867,8 @@ int32_t qlx_learner_priorities(qlx_learner* L, float* is_weights, float* leaves,
 }
 
 // Frame sparsity of the last vector step (diagnostic; synchronises): out[0..3] over its sampled training states (NaN when
-// it ran no update), out[4..7] over the acting frames, each {conv1 forward zero steps, conv1 weight-gradient zero steps,
+// it ran no update), out[4..7] over the current acting frames (the observations the NEXT vector step acts on: the table
+// after this step's env step and resets), each {conv1 forward zero steps, conv1 weight-gradient zero steps,
 // conv2 background rows, conv3 background rows} as fractions (qnet32.hip k_frame_sparsity)
 int32_t qlx_learner_frame_sparsity(qlx_learner* L, double* out) {
   return guard([&] {

@@ -38,6 +38,7 @@ constexpr uint32_t kTreeChunk = 2048;
 // final rounding (within one float ulp of the correctly rounded powf; tests/test_oracle_per.py).
 __device__ __forceinline__ float per_powf(float xf, float yf) {
 #pragma clang fp contract(off)
+  if (__builtin_isnan(yf)) return __builtin_nanf("");   // a NaN exponent: NaN on both sides (no rint of NaN below)
   if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : (yf < 0.0f ? __builtin_inff() : 1.0f)) : __builtin_nanf("");
   if (__builtin_isinf(xf)) return yf > 0.0f ? __builtin_inff() : (yf < 0.0f ? 0.0f : 1.0f);
   int e;

@@ -98,6 +98,10 @@ struct qlx_model {
   // partials as extra blocks of the weight-gradient reduction launch, then every variable's clip_by_norm + Adam in one
   // launch (k_update32) - the update's tail is two launches.  Set by the backward, consumed by model_norms / model_adam.
   bool f32_update_scheduled = false;
+  // data parallel (an all-reduce between the backward and the update): model_norms wrote the dense variables' norm
+  // partials of the reduced gradient x f32_partials_scale; model_adam then runs the same k_update32 tail
+  bool f32_dense_partials = false;
+  float f32_partials_scale = 1.0f;
   // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
   // sample's result does not depend on the batch it is evaluated in (the learner's target net)
   bool fc1_single = false;

@@ -20,6 +20,7 @@
 #include "qnet_kernels.h"
 #include "trunk_kernels.h"
 #include "gemm_kernels.h"
+#include "bgemm.h"
 #include "profiler.h"
 
 namespace qlx {
@@ -260,13 +261,15 @@ struct Fc2WgradArgs {
 };
 constexpr int kFc2WgradBlocks = 65;
 
-__device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, float* red /* LDS [4][24] */) {
+template <int NT>
+__device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, float* red /* LDS [NT / 64][24] + 24 */) {
+  constexpr int NWV = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float s[24];
 #pragma unroll
   for (int i = 0; i < 24; ++i) s[i] = 0.0f;
   if (j == 64) {
-    for (int b = tid; b < A.B; b += 256) {
+    for (int b = tid; b < A.B; b += NT) {
       const int a = A.actions[b];
       const float g = A.gs[b];
       s[0] += a == 0 ? g : 0.0f;
@@ -276,7 +279,7 @@ __device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, fl
     }
   } else {
     const int k0 = j * 8;
-    for (int b = tid; b < A.B; b += 256) {
+    for (int b = tid; b < A.B; b += NT) {
       const bf16x8 x = ld8(A.a4 + (size_t)b * 512 + k0);
       const int a = A.actions[b];
       const float g = A.gs[b];
@@ -299,36 +302,59 @@ __device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, fl
   __syncthreads();
   float t = 0.0f;
   if (tid < 24) {
-    t = ((red[tid] + red[24 + tid]) + red[48 + tid]) + red[72 + tid];
+    t = red[tid];
+    for (int w = 1; w < NWV; ++w) t += red[24 * w + tid];   // the wave sums in order
     if (j == 64) {
       if (tid < 3) A.g_b4[tid] = t;
       else if (tid == 3) *A.loss = t / (float)A.B;
     } else {
       A.g_w4[j * 24 + tid] = t;   // [k][a] with k = 8 j + tid / 3
     }
-    red[96 + tid] = (j < 64 || tid < 3) ? t * t : 0.0f;
+    red[24 * NWV + tid] = (j < 64 || tid < 3) ? t * t : 0.0f;
   }
   __syncthreads();
   if (tid == 0) {
     float q = 0.0f;
-    for (int i = 0; i < 24; ++i) q += red[96 + i];
+    for (int i = 0; i < 24; ++i) q += red[24 * NWV + i];
     if (j < 64) A.sq_w4[j] = q;
     else A.sq_b4[0] = q;
   }
 }
 
-// fc1 backward (dW3 + db3 tiles, then dz3 tiles) and the dense-3 weight gradient in one launch; block b runs
-// unit map[b] (pair tile < tiles, then fc2 wgrad blocks; -1 = idle), see fc1_bwd_map
+// fc1 on the bf16 GEMM core (bgemm.h): the forward at the training batch in kFc1Split k splits (fp32 slabs the head
+// reduces), at chunk batches (and for the target net, fc1_single) in one pass with bias + ReLU; the backward as one
+// launch of the weight gradient (dW3 | db3 = a3^T dz4, 3137 x 512 x B), the backward data (dz3 = (dz4 W3^T) (a3 > 0),
+// B x 3136 x 512) and the dense-3 weight gradient blocks.
+using CfgFc1Fwd = BGemmCfg<128, 128, 2, 2, false, true>;   // A = a3 (k = feature), B = W3 [3136][512] k-major
+using CfgFc1Wg = BGemmCfg<128, 128, 2, 4, true, true>;     // A = a3 k-major (k = sample), B = dz4 k-major
+using CfgFc1Dg = BGemmCfg<128, 128, 2, 4, false, false>;   // A = dz4 (k = out), B = W3 (rows = in, k = out)
+static_assert(CfgFc1Wg::T == CfgFc1Dg::T && CfgFc1Wg::LDS == CfgFc1Dg::LDS, "one block shape for the backward launch");
+constexpr int kFc1BwdThreads = CfgFc1Wg::T;
+
+// block b runs unit map[b] (weight-gradient tile, backward-data tile, then fc2 wgrad blocks; -1 = idle), see fc1_bwd_map
 template <class E1, class E2>
-__global__ __launch_bounds__(256, 2) void k_fc1_bwd(GemmProblem<E1> Pw, GemmProblem<E2> Pd, Fc2WgradArgs F, const int* map) {
-  const int t = map[blockIdx.x], tg = Pw.tiles() + Pd.tiles();
+__global__ __launch_bounds__(kFc1BwdThreads, 4) void k_fc1_bwd(BGemmProblem<E1> Pw, BGemmProblem<E2> Pd, Fc2WgradArgs F,
+                                                               const int* map) {
+  extern __shared__ __attribute__((aligned(16))) char fc1_lds[];
+  const int t = map[blockIdx.x], tw = Pw.tiles(), tg = tw + Pd.tiles();
   if (t < 0) return;
-  if (t < tg) {
-    gemm_pair_block<true, true, E1, false, false, E2>(Pw, Pd, t);
-  } else {
-    extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-    fc2_wgrad_block(F, t - tg, reinterpret_cast<float*>(lds));
-  }
+  if (t < tw) bgemm_tile<CfgFc1Wg>(Pw, t, fc1_lds);
+  else if (t < tg) bgemm_tile<CfgFc1Dg>(Pd, t - tw, fc1_lds);
+  else fc2_wgrad_block<kFc1BwdThreads>(F, t - tg, reinterpret_cast<float*>(fc1_lds));
+}
+
+template <class Epi>
+static BGemmProblem<Epi> bproblem(BOp A, BOp Bo, int M, int N, int K, int splits, int bm, int bn, Epi e, int ones_m = -1) {
+  const int kps = ((K + splits - 1) / splits + 31) / 32 * 32;
+  return BGemmProblem<Epi>{A, Bo, M, N, K, kps, ones_m, (M + bm - 1) / bm, (N + bn - 1) / bn, (K + kps - 1) / kps, 0, e};
+}
+
+// a3's pad columns: 1 at 3136 (the ones row of the weight gradient), 0 at 3137 .. kA3Ld - 1
+__global__ void k_a3_pad(bf16* a3, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over B * 8
+  if (i >= B * 8) return;
+  const int b = i >> 3, c = 3136 + (i & 7);
+  a3[(size_t)b * kA3Ld + c] = (bf16)(c == 3136 ? 1.0f : 0.0f);
 }
 
 // Block -> unit table of k_fc1_bwd.  Blocks b and b + 8 share an XCD (round-robin dispatch), so the table gives
@@ -336,8 +362,8 @@ __global__ __launch_bounds__(256, 2) void k_fc1_bwd(GemmProblem<E1> Pw, GemmProb
 // the dz3 tiles of W3 panels {x + 4, x + 12, ..} (all batch panels each), then its share of the fc2 wgrad
 // blocks.  Every a3 / W3 panel is fetched into one L2 instead of up to eight, and both GEMMs (16 vs 8 k-steps
 // per tile) spread evenly over the XCDs.
-template <class E1, class E2>
-static void fc1_bwd_map(qlx_model* m, const GemmProblem<E1>& Pw, const GemmProblem<E2>& Pd, int extra, hipStream_t s) {
+template <class PW, class PD>
+static void fc1_bwd_map(qlx_model* m, const PW& Pw, const PD& Pd, int extra, hipStream_t s) {
   if (m->fc1bwd_map_B == Pd.M) return;
   std::vector<int> lists[8];
   auto tile_of = [](const auto& P, int mi, int nj) {
@@ -479,7 +505,7 @@ void model_workspace(qlx_model* m, int B) {
   auto take = [&](size_t bytes) { const size_t o = off; off = align_up(off + bytes, 256); return o; };
   const size_t o_frames = take((size_t)B * 4 * kFramePix);
   const size_t o_table = take((size_t)B * 4 * sizeof(void*));
-  const size_t o_a1 = take((size_t)B * 12800 * 2), o_a2 = take((size_t)B * 5184 * 2), o_a3 = take((size_t)B * 3136 * 2);
+  const size_t o_a1 = take((size_t)B * 12800 * 2), o_a2 = take((size_t)B * 5184 * 2), o_a3 = take((size_t)B * kA3Ld * 2);
   const size_t o_a4 = take((size_t)B * 512 * 2), o_q = take((size_t)B * 3 * 4);
   const size_t o_dz1 = take((size_t)B * 12800 * 2), o_dz2 = take((size_t)B * 5184 * 2), o_dz3 = take((size_t)B * 3136 * 2);
   const size_t o_dz4 = take((size_t)B * 512 * 2);
@@ -503,6 +529,8 @@ void model_workspace(qlx_model* m, int B) {
   w.slab = (float*)(base + o_slab);
   w.bslab = (float*)(base + o_bslab);
   w.loss = (float*)(base + o_loss);
+  hipLaunchKernelGGL(k_a3_pad, dim3((B * 8 + 255) / 256), dim3(256), 0, m->stream, w.a3, B);
+  QLX_HIP(hipGetLastError());
   m->ws_batch = B;
 }
 
@@ -527,22 +555,12 @@ static void set_lds_attr(Kern k, size_t bytes) {
   set_lds_limit((const void*)k, bytes);
 }
 
-template <class Epi>
-static GemmProblem<Epi> gemm_problem(bool row_major_operand, const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K,
-                                     int splits, Epi epi, int ones_m = -1, bool n_fastest = false, bool remap = false) {
-  const int kps = (K + splits - 1) / splits;
-  QLX_CHECK(!row_major_operand || (K % 64 == 0 && kps % 64 == 0), QLX_E_INVALID,
-            "k_gemm: row-major operands need K and K/splits multiples of 64");
-  return GemmProblem<Epi>{A, lda, Bm, ldb, M, N, K, kps, ones_m, (M + 127) / 128, (N + 127) / 128, splits, n_fastest ? 1 : 0,
-                          remap ? 1 : 0, epi};
-}
-
-template <bool AK, bool BK, class Epi>
-static void launch_gemm(const bf16* A, int lda, const bf16* Bm, int ldb, int M, int N, int K, int splits, Epi epi, hipStream_t s,
-                        int ones_m = -1, bool remap = false) {
-  set_lds_attr(k_gemm<AK, BK, Epi>, GemmCfg::LDS);
-  const GemmProblem<Epi> P = gemm_problem(!(AK && BK), A, lda, Bm, ldb, M, N, K, splits, epi, ones_m, false, remap);
-  hipLaunchKernelGGL((k_gemm<AK, BK, Epi>), dim3(xcd_grid(P.tiles())), dim3(256), GemmCfg::LDS, s, P);
+// XCD-grouped tile order (xcd_tile): each XCD runs a contiguous range of the tile order, so the operand panels its tiles
+// share are fetched into its own L2 once (for the split forward: about one k split per XCD)
+template <class C, class Epi>
+static void launch_bgemm(const BGemmProblem<Epi>& P, hipStream_t s) {
+  set_lds_attr(k_bgemm<C, Epi>, C::LDS);
+  hipLaunchKernelGGL((k_bgemm<C, Epi>), dim3(xcd_grid(P.tiles())), dim3(C::T), C::LDS, s, P, 1);
 }
 
 void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool store_acts) {
@@ -567,13 +585,14 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
   {  // fc1: M = B, N = 512, K = 3136.  Small batches split K into kFc1Split fp32 slabs (reduced with bias +
      // ReLU in fixed order) to fill the chip; from 64 M tiles on (B >= 8192) one pass with the epilogue fused
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
+    const BOp A{w.a3, kA3Ld, B}, W{m->wb3, 512, 512};
     if (B >= 64 * 128 || m->fc1_single) {
-      launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, 1, Epi4BiasRelu{w.a4, p + var_offset(7), 512}, s);
+      launch_bgemm<CfgFc1Fwd>(bproblem(A, W, B, 512, 3136, 1, 128, 128, Epi4BiasRelu{w.a4, p + var_offset(7), 512}), s);
       w.a4_splits = 0;
     } else {
-      // XCD-grouped order: each XCD works on one k split (its a3 / W3 slices land in that XCD's L2 once)
-      launch_gemm<false, true>(w.a3, 3136, m->wb3, 512, B, 512, 3136, kFc1Split, Epi4Slab{w.fc1slab, 512, (size_t)B * 512}, s, -1,
-                               true);
+      const auto P = bproblem(A, W, B, 512, 3136, kFc1Split, 128, 128, Epi4Slab{w.fc1slab, 512, (size_t)B * 512});
+      QLX_CHECK(P.splits == kFc1Split, QLX_E_STATE, "fc1 split count");
+      launch_bgemm<CfgFc1Fwd>(P, s);
       w.a4_splits = kFc1Split;   // bias + ReLU + the fixed-order sum happen in the fc2 head that follows
     }
   }
@@ -627,21 +646,21 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
   //   dz3 = (dz4 W3^T) * (a3 > 0)
   {
     ProfScope ps(m->prof, "fc1_bwd", s, 2.0 * 2.0 * B * 512 * 3136);
-    const auto Pd = gemm_problem(true, w.dz4, 512, m->wb3, 512, B, 3136, 512, 1, Epi4ReluMask{w.dz3, w.a3, 3136});
+    const auto Pd = bproblem(BOp{w.dz4, 512, B}, BOp{m->wb3, 512, 3136}, B, 3136, 512, 1, 128, 128,
+                             Epi4ReluMask{w.dz3, w.a3, 3136, kA3Ld});
     const Fc2WgradArgs F{w.a4, actions, w.gs, w.hs, B, G + var_offset(8), G + var_offset(9), loss_dev,
                          m->d_sqf + sq_first(8), m->d_sqf + sq_first(9)};
     auto launch = [&](const auto& Pw, auto kern) {
       QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
       fc1_bwd_map(m, Pw, Pd, kFc2WgradBlocks, s);
-      // one block per CU (LDS request above half the CU's 160 KB): a 16-k-step dW3 tile sharing its CU with a
-      // second block lost more than the co-resident block gained (measured 28.3 -> 27.2 us per launch)
-      constexpr size_t lds_req = GemmCfg::LDS + 2048;
-      static_assert(2 * lds_req > 160 * 1024, "k_fc1_bwd: one block per CU");
+      constexpr size_t lds_req = CfgFc1Wg::LDS;
+      static_assert(lds_req >= (kFc1BwdThreads / 64 + 1) * 24 * sizeof(float), "fc2 wgrad block scratch");
       set_lds_attr(kern, lds_req);
-      hipLaunchKernelGGL(kern, dim3(m->fc1bwd_grid), dim3(256), lds_req, s, Pw, Pd, F, (const int*)m->d_fc1bwd_map);
+      hipLaunchKernelGGL(kern, dim3(m->fc1bwd_grid), dim3(kFc1BwdThreads), lds_req, s, Pw, Pd, F, (const int*)m->d_fc1bwd_map);
     };
-    launch(gemm_problem(false, w.a3, 3136, w.dz4, 512, 3137, 512, B, 1,
-                        Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136),
+    // dW3 rows 0..3135 and db3 as row 3136 (a3's ones column), written straight into the flat gradient (b3 follows W3)
+    launch(bproblem(BOp{w.a3, kA3Ld, 3137}, BOp{w.dz4, 512, 512}, 3137, 512, B, 1, 128, 128,
+                    Epi4StoreF32{G + var_offset(6), 512, m->d_sqf + sq_first(6)}, 3136),
            k_fc1_bwd<Epi4StoreF32, Epi4ReluMask>);
   }
   QLX_HIP(hipGetLastError());
@@ -992,7 +1011,10 @@ int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
     const bf16* src = layer == 1 ? m->w.a1 : layer == 2 ? m->w.a2 : layer == 3 ? m->w.a3 : m->w.a4;
     const size_t count = per[layer] * (size_t)m->last_batch;
     std::vector<uint16_t> tmp(count);
-    QLX_HIP(hipMemcpy(tmp.data(), src, count * 2, hipMemcpyDeviceToHost));
+    if (layer == 3)   // rows kA3Ld apart
+      QLX_HIP(hipMemcpy2D(tmp.data(), 3136 * 2, src, (size_t)kA3Ld * 2, 3136 * 2, (size_t)m->last_batch, hipMemcpyDeviceToHost));
+    else
+      QLX_HIP(hipMemcpy(tmp.data(), src, count * 2, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < count; ++i) {
       const uint32_t b = (uint32_t)tmp[i] << 16;
       std::memcpy(&out[i], &b, 4);

@@ -160,9 +160,9 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
 
 // clip_by_norm sums of squares: segment j of variable v = elements [j S, min(n_v, (j + 1) S)), S = kNormSeg = 2048;
 // thread t chains t = fmaf(x, x, t) over its elements j S + 4 t .. + 3, then j S + 1024 + 4 t .. + 3 (x = g * scale);
-// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  Norm_v from its partials in k_adam32.
+// wave xor butterfly (32, 16, .., 1); then ((w0 + w1) + w2) + w3 -> partial j.  Norm_v from its partials in k_update32.
 // (Measured and reverted: the last block to finish - a device-scope counter - reducing the partials to the ten norms, so
-// Adam loads ten values: Adam 16.3 -> 12.5 us, but the per-block release fence took k_norm32 6.2 -> 24.6 us.)
+// Adam loads ten values: Adam 16.3 -> 12.5 us, but the per-block release fence took the norm launch 6.2 -> 24.6 us.)
 constexpr int kNormSeg = 2048;
 constexpr int kNormSegMax = 832;   // partials per variable (13 per lane; W3 has 784)
 struct NormArgs {
@@ -201,21 +201,6 @@ __device__ __forceinline__ float norm32_lane(const float* gall, const int64_t* o
   return t;
 }
 
-// one 256-thread block = one segment partial: ((w0 + w1) + w2) + w3 of its four waves (wsum: 4 floats of LDS)
-__device__ __forceinline__ void norm32_block(const NormArgs& A, int blk, float* wsum) {
-  int v = 0;
-  while (v < kNumVars - 1 && blk >= A.seg_first[v + 1]) ++v;
-  const float t = norm32_lane(A.g, A.off, A.scale, v, blk - A.seg_first[v], threadIdx.x);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) A.partial[blk] = __fadd_rn(__fadd_rn(__fadd_rn(wsum[0], wsum[1]), wsum[2]), wsum[3]);
-}
-
-__global__ __launch_bounds__(256) void k_norm32(NormArgs A) {
-  __shared__ float wsum[4];
-  norm32_block(A, blockIdx.x, wsum);
-}
-
 // Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
 // [16 q, 16 q + 16)), S_q = chain over its chunks in order, dW = chain over q of S_q (each chain t = 0; t = t + x).
 // Segment 0 conv3 [577][64], 1 conv2 [513][64], 2 conv1 [257][32], rows in HWIO order, the last row of each the bias.
@@ -242,8 +227,8 @@ __host__ __device__ inline int wred_waves(int nz) {
   return w;
 }
 // Blocks [nred, ..) of the launch (update schedule 2, qnet.h): clip-norm segment partials of segments seg0 .. seg0 + nseg
-// - the dense variables', final since the fc1 backward - four 256-thread groups per block, one k_norm32 block's
-// arithmetic each.
+// - the dense variables', final since the fc1 backward - four 256-thread groups per block, one segment's
+// arithmetic each (norm32_lane, then ((w0 + w1) + w2) + w3).
 __global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred, int seg0, int nseg) {
   __shared__ float gs[kWGroupsMax * 64];
   if ((int)blockIdx.x >= nred) {
@@ -347,51 +332,8 @@ __device__ __forceinline__ void norms_prologue(const Adam32Args& A, int lane, fl
   }
 }
 
-// One float4 group (16-byte accesses) per thread: the grid covers count / 4 groups plus the tail group (elements past the
-// last full group, finished element by element).  Every variable but the last starts at a multiple of 4, so a group never
-// straddles two variables.  The group's g / w / m / v loads are issued first; wave 0 then loads all the clip-norm
-// partials (13 per lane for W3, one for each smaller variable: one memory round) and finishes the ten norms while the
-// element loads are in flight.
-__global__ __launch_bounds__(256) void k_adam32(Adam32Args A) {
-  __shared__ float nrm[kNumVars];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t count = A.off[kNumVars], n4 = count / 4;
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, i0 = q * 4;
-  f32x4 g = zero4(), w = zero4(), m = zero4(), v = zero4();
-  if (q < n4) {
-    g = ld4(A.g + i0);
-    w = ld4(A.w + i0);
-    m = ld4(A.m + i0);
-    v = ld4(A.v + i0);
-  }
-  if (wave == 0) norms_prologue<0>(A, lane, nrm, blockIdx.x == 0);
-  __syncthreads();
-  if (q < n4) {
-    const float denom = fmaxf(nrm[var_of(A, i0)], A.clipnorm);
-    f32x4 o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float mk = m[k], vk = v[k];
-      o[k] = adam32_elem(g[k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[k]);
-      m[k] = mk;
-      v[k] = vk;
-    }
-    *reinterpret_cast<f32x4*>(A.w + i0) = o;
-    *reinterpret_cast<f32x4*>(A.m + i0) = m;
-    *reinterpret_cast<f32x4*>(A.v + i0) = v;
-  } else if (q == n4) {
-    for (int64_t i = i0; i < count; ++i) {
-      const float denom = fmaxf(nrm[var_of(A, i)], A.clipnorm);
-      float mi = A.m[i], vi = A.v[i];
-      A.w[i] = adam32_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mi, vi, A.w[i]);
-      A.m[i] = mi;
-      A.v[i] = vi;
-    }
-  }
-}
-
 // The dense variables' blocks of k_update32: clip_by_norm + Adam of W3, b3, W4, b4 (95 % of the update's Adam bytes)
-// from their norm partials.  Same arithmetic as k_adam32 on those elements.
+// from their norm partials.  Explicit roundings in the oracle's order (adam32_elem).
 struct AdamDense {
   static constexpr size_t LDS = 64;
   Adam32Args A;
@@ -474,7 +416,7 @@ struct AdamDense {
 
 // clip_by_norm + Adam of the six conv variables (W0 .. b2, 78K elements) in one launch of independent 1024-thread blocks:
 // block = (variable v, chunk c of 4,096 elements).  Each block finishes v's norm itself - every gradient element of v
-// loaded at once (four 256-thread groups, group q taking segments q, q + 4, .., each with one k_norm32 block's
+// loaded at once (four 256-thread groups, group q taking segments q, q + 4, .., each with one segment's
 // arithmetic), then the partials and the final chain in LDS - and updates its chunk (one float4 per thread).  The
 // re-read of v per chunk (<= 147 KB, from L2) buys a launch with one memory round per phase.
 constexpr int kConvAdamChunk = 4096;
@@ -966,34 +908,38 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   }
 }
 
+// Data parallel (an all-reduce sits between the backward and the update, so the reduction launch could not take the dense
+// partials): the dense variables' clip-norm segment partials of the reduced gradient x scale, as k_wreduce32's extra
+// blocks compute them at world 1 (the same blocks, no chunk sums).  Only the dense gradient is read, so a caller may run it
+// as soon as the dense bucket is reduced (learner.hip: on the communicator stream, beside the conv backward).
 void f32_norms(qlx_model* m, hipStream_t s, float scale) {
   if (m->f32_update_scheduled) return;   // the backward scheduled them (f32_backward_conv)
-  ProfScope ps(m->prof, "f32_norms", s, 4.0 * kNumParams);
-  const NormArgs A = norm_args(m, scale);
-  hipLaunchKernelGGL(k_norm32, dim3(A.seg_first[kNumVars]), dim3(256), 0, s, A);
+  ProfScope ps(m->prof, "f32_norms", s, 4.0 * (kNumParams - kVarOffsetDense));
+  const NormArgs N = norm_args(m, scale);
+  const int dseg = N.seg_first[kNumVars] - N.seg_first[6];
+  const WRed R{};   // no chunk-sum blocks (nred = 0)
+  hipLaunchKernelGGL(k_wreduce32, dim3((dseg + 3) / 4), dim3(1024), 0, s, R, N, 0, N.seg_first[6], dseg);
   QLX_HIP(hipGetLastError());
-  debug_sync(s, "k_norm32");
+  debug_sync(s, "k_wreduce32 (dense norm partials)");
+  m->f32_dense_partials = true;
+  m->f32_partials_scale = scale;
 }
 
+// clip_by_norm + Adam of every variable in one launch (k_update32): the conv blocks finish their variable's norm from the
+// (scaled) gradient, the dense blocks from the partials of the reduction launch (world 1) or of f32_norms (data parallel).
+// One tail for both, so a rank's update is the single-GPU update of its reduced gradient (bit-identical at world 1).
 void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const int64_t t = m->iterations + 1;
   const Adam32Args a = adam_args(m, scale);
-  if (m->f32_update_scheduled) {   // every variable in one launch; the dense norm partials came with the reduction
-    QLX_CHECK(scale == 1.0f, QLX_E_STATE, "scheduled fp32 update with a gradient scale");
-    ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
-    const int nconv = conv_adam_blocks(), ndense = (int)((kNumParams - kVarOffsetDense) / 4 / 2048 + 1);   // 2 groups / thread
-    hipLaunchKernelGGL(k_update32, dim3(nconv + ndense), dim3(1024), 0, s, a, norm_args(m, 1.0f), nconv, ndense);
-    QLX_HIP(hipGetLastError());
-    debug_sync(s, "k_update32");
-    m->f32_update_scheduled = false;
-    m->iterations = t;
-    return;
-  }
+  QLX_CHECK(m->f32_update_scheduled ? scale == 1.0f : (m->f32_dense_partials && scale == m->f32_partials_scale), QLX_E_STATE,
+            "fp32 update without the dense norm partials of this gradient scale (model_norms first)");
   ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
-  const int64_t groups = kNumParams / 4 + 1;   // float4 groups + the tail group: one per thread
-  hipLaunchKernelGGL(k_adam32, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, a);
+  const int nconv = conv_adam_blocks(), ndense = (int)((kNumParams - kVarOffsetDense) / 4 / 2048 + 1);   // 2 groups / thread
+  hipLaunchKernelGGL(k_update32, dim3(nconv + ndense), dim3(1024), 0, s, a, norm_args(m, scale), nconv, ndense);
   QLX_HIP(hipGetLastError());
-  debug_sync(s, "k_adam32");
+  debug_sync(s, "k_update32");
+  m->f32_update_scheduled = false;
+  m->f32_dense_partials = false;
   m->iterations = t;
 }
 

@@ -1812,6 +1812,9 @@ struct PConvWgrad {
   static constexpr bool STREAMED = BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4;
   using Streams = std::conditional_t<STREAMED, StreamsImpl, void>;
   static_assert(!TPADS || KMAX <= 4 * 32 * 16, "weight-gradient chunk: the offset table lives in the four images' pads");
+  // TableK4Stream::slot() places the table in the pad columns 64..79 of four 64-row KMAJ images (A and B, two buffers):
+  // a B tile of another width would put it into B's live data
+  static_assert(!STREAMED || !TPADS || BN_ == 64, "streamed weight-gradient tiles with the table in the pads need BN = 64");
   static constexpr size_t EXTRA_LDS = STREAMED && !TPADS ? (size_t)KMAX * 4 : 0;
   template <class ST = Streams>
   __device__ ST streams(int z, int row0, int col0, int tid) const {

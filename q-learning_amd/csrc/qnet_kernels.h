@@ -19,6 +19,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// bf16 a3 row pitch: columns 0..3135 the flattened conv3 output, column 3136 = 1.0 and 3137..3143 = 0 (written once per
+// workspace, k_a3_pad), so the fc1 weight gradient a3^T dz4 over 3137 rows yields db3 as its last row (bgemm.h)
+constexpr int kA3Ld = 3144;
+
 // wave index as a scalar: keeps wave-derived loop bounds and branches uniform (SCC, not EXEC masks)
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
     lds_barrier();   // previous sample's conv phases are done with X / A2 (and the pointer slots)
     frames_stage_slots<kXW>(X, pf);
     if (threadIdx.x < 4) sptr[threadIdx.x] = pnext;
-    if (b != (int)blockIdx.x) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)(b - gridDim.x) * 3136);
+    if (b != (int)blockIdx.x) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)(b - gridDim.x) * kA3Ld);
     lds_barrier();
     mark(0);
     frames_prefetch_slots(sptr, b + (int)gridDim.x < B, pf);
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
   }
   lds_barrier();
   const int last = (int)blockIdx.x + ((B - 1 - (int)blockIdx.x) / (int)gridDim.x) * (int)gridDim.x;
-  if ((int)blockIdx.x < B) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)last * 3136);
+  if ((int)blockIdx.x < B) lds_copy_out<49, 64, kA3S>(A3, a3 + (size_t)last * kA3Ld);
 }
 
 // conv1 weight gradient: per block fp32 partial dW[256 (s2d k)][32] followed by the bias partial db[32] in

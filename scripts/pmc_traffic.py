@@ -29,7 +29,7 @@ SCOPES = {
         "f32_conv3_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<9, 9",
         "f32_conv2_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<20, 20",
         "f32_conv1_wgrad": "k_conv1_wgrad32",
-        "f32_norms": "k_norm32",
+        "f32_norms": "k_wreduce32",
         "f32_head": "k_head32<3>",
         "f32_wgrad_reduce": "k_wreduce32",
         "f32_adam": "k_update32",   # update schedule 2 (default): every variable's clip_by_norm + Adam in one launch
