@@ -538,7 +538,8 @@ class SelfDrivingQLearner(_LearningStats):
     def frame_sparsity(self):
         """Fractions of the fp32 conv work the exact zero skips leave out in the last vector step (diagnostic):
         {"train": [...], "act": [...]}, each [conv1 fwd zero steps, conv1 wgrad zero steps, conv2 bg rows, conv3 bg rows]
-        (train: the step's sampled states, NaN without an update; act: the acting frames)."""
+        (train: the step's sampled states, NaN without an update; act: the current acting frames - the observations the
+        next vector step acts on, after this step's env step and resets)."""
         out = np.zeros(8, np.float64)
         _check(lib().qlx_learner_frame_sparsity(self.h, _p(out)))
         return {"train": out[:4].tolist(), "act": out[4:].tolist()}
