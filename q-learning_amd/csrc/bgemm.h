@@ -42,10 +42,13 @@ struct BOp {
   int rows;   // valid rows (M for A, N for B)
 };
 
-template <int BM_, int BN_, int WM_, int WN_, bool AK_, bool BKM_>
+// DBG_ (development timing only, scripts/ubench_bgemm.hip): 1 = no MFMAs, 2 = no DMA in the k loop, 3 = DMA and barriers
+// only, 4 = no k loop (prologue DMA + epilogue), 5 = no epilogue stores
+template <int BM_, int BN_, int WM_, int WN_, bool AK_, bool BKM_, int S_ = 3, int DBG_ = 0>
 struct BGemmCfg {
+  static constexpr int DBG = DBG_;
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NW = WM_ * WN_, T = NW * 64;
-  static constexpr int BK = 32, S = 3;
+  static constexpr int BK = 32, S = S_;   // S LDS stages: S - 1 k-steps in flight ahead of the one multiplied
   static constexpr bool AK = AK_, BKM = BKM_;
   static constexpr int TM = BM / WM, TN = BN / WN;   // wave tile
   static constexpr int FM = TM / 16, FN = TN / 16;   // 16 x 16 MFMA tiles per wave
@@ -57,6 +60,7 @@ struct BGemmCfg {
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile of whole 16 x 16 MFMA tiles");
   static_assert(!AK || BM == 64 || BM == 128, "k-major images are 64 or 128 rows");
   static_assert(!BKM || BN == 64 || BN == 128, "k-major images are 64 or 128 rows");
+  static_assert(S >= 2 && S <= 8 && (S - 1) * (LPA + LPB) <= 63, "vmcnt counts to 63");
 };
 
 template <class Epi>
@@ -132,18 +136,34 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 template <bool KM>
 constexpr int bfrag_insts() { return KM ? 2 : 1; }   // LDS instructions per fragment
+// one LDS read at addr + OFF (OFF an immediate; the ds offset field is 16 bits, so 64 KB moves into the address)
+template <int OFF>
+__device__ __forceinline__ u32x4 ds_b128(uint32_t addr) {
+  if constexpr (OFF >= 65536) {
+    return ds_b128<OFF - 65536>(addr + 65536u);
+  } else {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+  }
+}
+template <int OFF>
+__device__ __forceinline__ u32x2 ds_tr16(uint32_t addr) {
+  if constexpr (OFF >= 65536) {
+    return ds_tr16<OFF - 65536>(addr + 65536u);
+  } else {
+    u32x2 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+  }
+}
 // addr: the fragment's lane address inside the operand image (VGPR); OFF: the image's byte offset in LDS (immediate)
 template <bool KM, int BR, int OFF>
 __device__ __forceinline__ bf16x8 bfrag_read(uint32_t addr) {
-  static_assert(OFF + 4 * BR * 2 < 65536, "ds offset field");
   if constexpr (!KM) {
-    u32x4 r;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(bf16x8, ds_b128<OFF>(addr));
   } else {
-    u32x2 v0, v1;
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v0) : "v"(addr), "n"(OFF));
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(addr), "n"(OFF + 4 * BR * 2));
+    const u32x2 v0 = ds_tr16<OFF>(addr), v1 = ds_tr16<OFF + 4 * BR * 2>(addr);
     return __builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]});
   }
 }
@@ -166,6 +186,16 @@ __device__ __forceinline__ void static_for(F f) { static_for_impl<0, N>(f); }
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(L * n) for a wave-uniform n in [0, NMAX]
+template <int L, int NMAX>
+__device__ __forceinline__ void wait_vm_n(int n) {
+  if constexpr (NMAX <= 0) {
+    wait_vm<0>();
+  } else {
+    if (n >= NMAX) wait_vm<L * NMAX>();
+    else wait_vm_n<L, NMAX - 1>(n);
+  }
 }
 
 // One output tile (m-panel, n-panel, k split) of problem P; lds = the block's dynamic LDS (C::LDS bytes).
@@ -209,64 +239,100 @@ __device__ __forceinline__ void bgemm_tile(const BGemmProblem<Epi>& P, int tile,
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int LPW = C::LPA + C::LPB;
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  auto step = [&](auto stage_c, int t) {
-    constexpr int stage = decltype(stage_c)::value;
-    // k-step t has landed (this wave's part; t + 1 may stay in flight), then every wave's part (barrier).  The barrier
-    // also retires every wave's reads of step t - 1, whose stage the DMA of step t + 2 overwrites next.
-    if (t + 1 < nk) wait_vm<LPW>();
-    else wait_vm<0>();
+  constexpr int S = C::S;
+  static_assert(S >= 3, "the fragment prefetch reads stage t + 1 while stage t + 2 .. t + S - 1 land");
+  // Fragments of step t + 1 are read while the MFMAs of step t run (two register sets, fr[t % 2]): the LDS latency hides
+  // behind the matrix pipe instead of sitting between the barrier and the MFMAs.
+  bf16x8 fa[2][C::FM], fb[2][C::FN];
+  auto read_frags = [&](auto stage_c, auto par_c) {
+    constexpr int stage = decltype(stage_c)::value, par = decltype(par_c)::value;
+#pragma unroll
+    for (int f = 0; f < C::FM; ++f) fa[par][f] = bfrag_read<C::AK, C::BM, stage * C::STAGE>(offA[f]);
+#pragma unroll
+    for (int f = 0; f < C::FN; ++f) fb[par][f] = bfrag_read<C::BKM, C::BN, stage * C::STAGE + C::ABYTES>(offB[f]);
+  };
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s, s);
+  if (nk > 0) {
+    wait_vm_n<LPW, S - 2>(min(S - 2, nk - 1));
     __builtin_amdgcn_s_barrier();
-    if (t + 2 < nk) issue(t + 2, (stage + 2) % 3);
-    bf16x8 fa[C::FM], fb[C::FN];
-#pragma unroll
-    for (int f = 0; f < C::FM; ++f) fa[f] = bfrag_read<C::AK, C::BM, stage * C::STAGE>(offA[f]);
-#pragma unroll
-    for (int f = 0; f < C::FN; ++f) fb[f] = bfrag_read<C::BKM, C::BN, stage * C::STAGE + C::ABYTES>(offB[f]);
-    // column j of MFMAs waits for the A fragments and B_0 .. B_j (the reads retire in issue order); the last wait is
-    // lgkmcnt(0), so this step's LDS reads are complete before the next barrier releases the DMA that reuses the stage
-    constexpr int IB = bfrag_insts<C::BKM>();
-    static_assert(C::FM * bfrag_insts<C::AK>() + C::FN * IB <= 15, "lgkmcnt counts to 15");
+    if constexpr (C::DBG != 3) read_frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  }
+  auto step = [&](auto u_c, int t) {
+    constexpr int u = decltype(u_c)::value, stage = u % S, par = u % 2;
+    // k-step t + 1 has landed (this wave's part; t + 2 .. t + S - 2 may stay in flight), then every wave's part
+    // (barrier).  The barrier also retires every wave's reads of stage t - 1 (waited for before the MFMAs of step t - 1),
+    // which the DMA of step t + S - 1 overwrites next.
+    const bool more = t + 1 < nk;
+    if (more) {
+      wait_vm_n<LPW, S - 3>(min(S - 3, nk - 2 - t));
+      __builtin_amdgcn_s_barrier();
+      if (t + S - 1 < nk && C::DBG != 2) issue(t + S - 1, (stage + S - 1) % S);
+    }
+    if constexpr (C::DBG == 3) return;
+    bfrag_wait<0>();   // the fragments of step t (read during step t - 1)
     auto col = [&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      bfrag_wait<(C::FN - 1 - j) * IB>();
 #pragma unroll
-      for (int i = 0; i < C::FM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < C::FM; ++i) {
+        if constexpr (C::DBG == 1) acc[i][j][0] += (float)fb[par][j][0] * (float)fa[par][i][0];
+        else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[par][j], fa[par][i], acc[i][j], 0, 0, 0);
+      }
+      if constexpr (j == 0) {   // the next step's reads go out behind the first column of MFMAs
+        if (more) read_frags(std::integral_constant<int, (stage + 1) % S>{}, std::integral_constant<int, par ^ 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+      }
     };
     static_for<C::FN>(col);
   };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  using S2 = std::integral_constant<int, 2>;
-  int t = 0;
-  for (; t + 3 <= nk; t += 3) {
-    step(S0{}, t);
-    step(S1{}, t + 1);
-    step(S2{}, t + 2);
-  }
-  if (t < nk) {
-    step(S0{}, t);
-    if (t + 1 < nk) step(S1{}, t + 1);
-  }
-  // C^T fragments: lane & 15 = m, registers = 4 consecutive n starting at 4 (lane >> 4)
+  // the loop unrolled by U (a multiple of S and of 2), so every stage offset and register set is static
+  constexpr int U = S % 2 == 0 ? S : 2 * S;
+  int t = C::DBG == 4 ? nk : 0;
+  if constexpr (C::DBG == 4) wait_vm<0>();
+  for (; t + U <= nk; t += U) static_for<U>([&](auto uc) { step(uc, t + decltype(uc)::value); });
+  static_for<U - 1>([&](auto uc) {
+    if (t + decltype(uc)::value < nk) step(uc, t + decltype(uc)::value);
+  });
+  // Epilogue through LDS: the C^T fragments (lane & 15 = m, 4 consecutive n at 4 (lane >> 4)) are written to a per-wave
+  // [rows][TN + 4] fp32 image and read back along the rows, so each store instruction covers whole row segments
+  // (TN / 4 lanes per row: 256-byte fp32 / 128-byte bf16 runs) instead of 16 rows x 64 bytes.  Half the wave's rows at
+  // a time (LDS), every DMA landed and every k-loop read retired before the image reuses the ring.
   const Epi& epi = P.epi;
   float sq_main = 0.0f, sq_ones = 0.0f;
+  wait_vm<0>();
+  bfrag_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  constexpr int HR = C::TM / 2, PITCH = C::TN + 4, LPR = C::TN / 4, RPI = 64 / LPR;   // rows per half, lanes per row
+  static_assert((size_t)C::NW * HR * PITCH * 4 <= C::LDS, "epilogue image fits the ring");
+  float* img = reinterpret_cast<float*>(lds) + wave * HR * PITCH;
 #pragma unroll
-  for (int i = 0; i < C::FM; ++i) {
-    const int m = m0 + wm * C::TM + 16 * i + (lane & 15);
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-      const int n = n0 + wn * C::TN + 16 * j + 4 * (lane >> 4);
+    for (int i = 0; i < C::FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+        *reinterpret_cast<f32x4*>(img + (16 * i + (lane & 15)) * PITCH + 16 * j + 4 * (lane >> 4)) = acc[h * (C::FM / 2) + i][j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's image is written (the wave reads only its own)
+#pragma unroll
+    for (int it = 0; it < HR / RPI; ++it) {
+      const int r = it * RPI + lane / LPR, c = 4 * (lane % LPR);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * PITCH + c);
+      const int m = m0 + wm * C::TM + h * HR + r, n = n0 + wn * C::TN + c;
+      if constexpr (C::DBG == 5) {
+        asm volatile("" ::"v"(v));
+        continue;
+      }
       if (m < P.M && n < P.N) {
-        epi(m, n, acc[i][j], bz);
+        epi(m, n, v, bz);
         if constexpr (Epi::kSq) {
-          const float q = sq4(acc[i][j]);
+          const float q = sq4(v);
           if (m == P.ones_m) sq_ones = __fadd_rn(sq_ones, q);
           else sq_main = __fadd_rn(sq_main, q);
         }
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // the reads are done before the second half overwrites the image
   }
   if constexpr (Epi::kSq) {
     if (epi.sq) {   // fixed-order block reduction: xor butterfly per wave, then the waves in order
@@ -275,8 +341,8 @@ __device__ __forceinline__ void bgemm_tile(const BGemmProblem<Epi>& P, int tile,
         sq_main += __shfl_xor(sq_main, off);
         sq_ones += __shfl_xor(sq_ones, off);
       }
-      float* red = reinterpret_cast<float*>(lds);
-      __syncthreads();   // every wave is past its last LDS read of the k loop
+      float* red = reinterpret_cast<float*>(lds) + C::NW * HR * PITCH;
+      static_assert((size_t)C::NW * HR * PITCH * 4 + 2 * C::NW * 4 <= C::LDS, "sq scratch");
       if (lane == 0) { red[2 * wave] = sq_main; red[2 * wave + 1] = sq_ones; }
       __syncthreads();
       if (tid == 0) {

@@ -12,7 +12,7 @@ namespace qlx {
 constexpr int kNumVars = 10;
 constexpr int64_t kVarOffsetDense = 77984;   // flat offset of W3 (conv variables before it, dense ones after)
 constexpr int64_t kNumParams = 1685667;   // sum of the 10 Keras variables (variables.index shapes)
-constexpr int kFc1Split = 7;              // split-K of the 3136-deep dense layer (14 MFMA k-steps each)
+constexpr int kFc1Split = 4;              // bf16: split-K of the 3136-deep dense layer at training batches (25 / 23 k-steps)
 // conv weight-gradient partial slabs, one region per layer (conv3 and conv2 share a launch)
 constexpr size_t kSlabConv3 = 0, kSlabConv2 = (size_t)3200 * 1024, kSlabConv1 = (size_t)7424 * 1024;
 constexpr size_t kWgradSlabFloats = (size_t)9600 * 1024;

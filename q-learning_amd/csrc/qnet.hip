@@ -325,9 +325,13 @@ __device__ __forceinline__ void fc2_wgrad_block(const Fc2WgradArgs& A, int j, fl
 // reduces), at chunk batches (and for the target net, fc1_single) in one pass with bias + ReLU; the backward as one
 // launch of the weight gradient (dW3 | db3 = a3^T dz4, 3137 x 512 x B), the backward data (dz3 = (dz4 W3^T) (a3 > 0),
 // B x 3136 x 512) and the dense-3 weight gradient blocks.
-using CfgFc1Fwd = BGemmCfg<128, 128, 2, 2, false, true>;   // A = a3 (k = feature), B = W3 [3136][512] k-major
-using CfgFc1Wg = BGemmCfg<128, 128, 2, 4, true, true>;     // A = a3 k-major (k = sample), B = dz4 k-major
-using CfgFc1Dg = BGemmCfg<128, 128, 2, 4, false, false>;   // A = dz4 (k = out), B = W3 (rows = in, k = out)
+// tiles and ring depths from scripts/ubench_bgemm.hip (gpurun_out/a4): forward at B = 1024 on 128 x 64 tiles in 4 k splits
+// 8.7 us (128 x 128 in 7 splits: 9.6 us, and twice the slab bytes the head reads), backward data 9.1 us and weight
+// gradient 12.5 us on 8-wave 128 x 128 tiles with 4 stages
+using CfgFc1Fwd = BGemmCfg<128, 64, 2, 2, false, true, 4>;    // A = a3 (k = feature), B = W3 [3136][512] k-major
+using CfgFc1FwdBig = BGemmCfg<128, 128, 2, 4, false, true, 4>;   // chunk batches (one pass, bias + ReLU)
+using CfgFc1Wg = BGemmCfg<128, 128, 2, 4, true, true, 4>;     // A = a3 k-major (k = sample), B = dz4 k-major
+using CfgFc1Dg = BGemmCfg<128, 128, 2, 4, false, false, 4>;   // A = dz4 (k = out), B = W3 (rows = in, k = out)
 static_assert(CfgFc1Wg::T == CfgFc1Dg::T && CfgFc1Wg::LDS == CfgFc1Dg::LDS, "one block shape for the backward launch");
 constexpr int kFc1BwdThreads = CfgFc1Wg::T;
 
@@ -442,17 +446,43 @@ struct AdamArgs {
   PackPtrs pack;
 };
 
-// tf.clip_by_norm per variable + ResourceApplyAdam.  Every block first finishes the per-variable norms
-// from the k_sumsq partials (wave w reduces variables w, w+4, w+8: lane-strided sums + xor tree, the
-// same fixed order in every block).
+// flat offsets of the ten variables (kVarSize running sums); every variable but b4 starts at a multiple of 4
+__device__ constexpr int64_t kVarOff[kNumVars + 1] = {0, 8192, 8224, 40992, 41056, 77920, 77984, 1683616, 1684128, 1685664, 1685667};
+__device__ __forceinline__ int adam_var_of(int64_t i) {
+  int v = 0;
+#pragma unroll
+  for (int k = 1; k < kNumVars; ++k) v += i >= kVarOff[k] ? 1 : 0;
+  return v;
+}
+
+// the bf16 operand copies of float4 group i0 (4 consecutive parameters of one variable)
+__device__ __forceinline__ void pack_group(const PackPtrs& P, int64_t i0, int var, f32x4 w) {
+  if (var == 6) {   // W3: the Keras layout, 8-byte store
+    *reinterpret_cast<uint2*>(P.wb3 + (i0 - kVarOff[6])) = pack4(w[0], w[1], w[2], w[3]);
+  } else if (var == 0 || var == 2 || var == 4) {   // conv kernels: fragment-major scatter
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pack_one(P, i0 + k, w[k]);
+  }
+}
+
+// tf.clip_by_norm per variable + ResourceApplyAdam + the bf16 operand copies.  Two float4 groups per thread, all eight
+// loads issued before the norm prologue; every block first finishes the per-variable norms from the partials (wave w
+// reduces variables w, w+4, w+8: lane-strided sums + xor tree, the same fixed order in every block).  (Round 5: one
+// element per thread over 2048 blocks took 16.6 us per update; 16-byte groups per thread measured slower in round 1 -
+// then without the loads issued ahead of the prologue.)
+constexpr int kAdamGroups = 2;
 __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
-  __shared__ int64_t offs[kNumVars + 1];
   __shared__ float nrm[kNumVars];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (threadIdx.x == 0) {
-    int64_t o = 0;
-    for (int i = 0; i < kNumVars; ++i) { offs[i] = o; o += kVarSize[i]; }
-    offs[kNumVars] = o;
+  const int64_t n4 = A.count / 4, st = (int64_t)gridDim.x * blockDim.x, q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  f32x4 g[kAdamGroups], w[kAdamGroups], m[kAdamGroups], vs[kAdamGroups];
+#pragma unroll
+  for (int u = 0; u < kAdamGroups; ++u) {
+    const int64_t qq = q0 + u * st, i0 = (qq < n4 ? qq : 0) * 4;
+    g[u] = *reinterpret_cast<const f32x4*>(A.g + i0);
+    w[u] = *reinterpret_cast<const f32x4*>(A.w + i0);
+    m[u] = *reinterpret_cast<const f32x4*>(A.m + i0);
+    vs[u] = *reinterpret_cast<const f32x4*>(A.v + i0);
   }
   for (int v = wave; v < kNumVars; v += 4) {
     // all of a lane's partials are loaded before the first add (one memory latency, not one per partial),
@@ -475,17 +505,37 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     }
   }
   __syncthreads();
-  // one parameter per thread and grid-stride step (measured faster than 16-byte groups on this kernel)
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.count; i += (int64_t)gridDim.x * blockDim.x) {
-    int var = 0;
-    while (i >= offs[var + 1]) ++var;
-    const float denom = fmaxf(nrm[var], A.clipnorm);
-    float m = A.m[i], v = A.v[i];
-    const float w = adam_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, m, v, A.w[i]);
-    A.m[i] = m;
-    A.v[i] = v;
-    A.w[i] = w;
-    pack_one(A.pack, i, w);
+#pragma unroll
+  for (int u = 0; u < kAdamGroups; ++u) {
+    const int64_t qq = q0 + u * st;
+    if (qq < n4) {
+      const int64_t i0 = qq * 4;
+      const int var = adam_var_of(i0);
+      const float denom = fmaxf(nrm[var], A.clipnorm);
+      f32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float mk = m[u][k], vk = vs[u][k];
+        o[k] = adam_elem(g[u][k], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mk, vk, w[u][k]);
+        m[u][k] = mk;
+        vs[u][k] = vk;
+      }
+      *reinterpret_cast<f32x4*>(A.w + i0) = o;
+      *reinterpret_cast<f32x4*>(A.m + i0) = m[u];
+      *reinterpret_cast<f32x4*>(A.v + i0) = vs[u];
+      pack_group(A.pack, i0, var, o);
+    } else if (qq == n4) {   // the tail (b4's last elements), element by element
+      for (int64_t i = n4 * 4; i < A.count; ++i) {
+        const int var = adam_var_of(i);
+        const float denom = fmaxf(nrm[var], A.clipnorm);
+        float mi = A.m[i], vi = A.v[i];
+        const float wi = adam_elem(A.g[i], A.scale, A.clipnorm, denom, A.alpha, A.beta1, A.beta2, A.eps, mi, vi, A.w[i]);
+        A.m[i] = mi;
+        A.v[i] = vi;
+        A.w[i] = wi;
+        pack_one(A.pack, i, wi);
+      }
+    }
   }
 }
 
@@ -587,10 +637,11 @@ void model_forward_trunk(qlx_model* m, const uint8_t* const* table, int B, hipSt
     ProfScope ps(m->prof, "fc1_fwd", s, 2.0 * B * 512 * 3136);
     const BOp A{w.a3, kA3Ld, B}, W{m->wb3, 512, 512};
     if (B >= 64 * 128 || m->fc1_single) {
-      launch_bgemm<CfgFc1Fwd>(bproblem(A, W, B, 512, 3136, 1, 128, 128, Epi4BiasRelu{w.a4, p + var_offset(7), 512}), s);
+      launch_bgemm<CfgFc1FwdBig>(bproblem(A, W, B, 512, 3136, 1, CfgFc1FwdBig::BM, CfgFc1FwdBig::BN,
+                                          Epi4BiasRelu{w.a4, p + var_offset(7), 512}), s);
       w.a4_splits = 0;
     } else {
-      const auto P = bproblem(A, W, B, 512, 3136, kFc1Split, 128, 128, Epi4Slab{w.fc1slab, 512, (size_t)B * 512});
+      const auto P = bproblem(A, W, B, 512, 3136, kFc1Split, CfgFc1Fwd::BM, CfgFc1Fwd::BN, Epi4Slab{w.fc1slab, 512, (size_t)B * 512});
       QLX_CHECK(P.splits == kFc1Split, QLX_E_STATE, "fc1 split count");
       launch_bgemm<CfgFc1Fwd>(P, s);
       w.a4_splits = kFc1Split;   // bias + ReLU + the fixed-order sum happen in the fc2 head that follows
@@ -761,7 +812,8 @@ void model_adam(qlx_model* m, hipStream_t s, float scale) {
   a.beta1 = m->beta1; a.beta2 = m->beta2; a.eps = m->eps; a.clipnorm = m->clipnorm;
   a.pack = pack_ptrs(m);
   ProfScope ps(m->prof, "adam", s, 32.0 * kNumParams);
-  hipLaunchKernelGGL(k_adam, dim3(2048), dim3(256), 0, s, a);
+  const int64_t groups = kNumParams / 4 + 1;   // float4 groups + the tail group
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)((groups + 256 * kAdamGroups - 1) / (256 * kAdamGroups))), dim3(256), 0, s, a);
   QLX_HIP(hipGetLastError());
   m->iterations = t;
 }
