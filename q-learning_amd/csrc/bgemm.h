@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "gemm_kernels.h"
 #include "qnet_kernels.h"
@@ -44,9 +45,11 @@ struct BOp {
 
 // DBG_ (development timing only, scripts/ubench_bgemm.hip): 1 = no MFMAs, 2 = no DMA in the k loop, 3 = DMA and barriers
 // only, 4 = no k loop (prologue DMA + epilogue), 5 = no epilogue stores
-template <int BM_, int BN_, int WM_, int WN_, bool AK_, bool BKM_, int S_ = 3, int DBG_ = 0>
+// AG_: void, or the im2col geometry of a gathered A operand (ConvGather: A(m, k) = in[im2col row k][column m], k-major)
+template <int BM_, int BN_, int WM_, int WN_, bool AK_, bool BKM_, int S_ = 3, int DBG_ = 0, class AG_ = void>
 struct BGemmCfg {
   static constexpr int DBG = DBG_;
+  using AG = AG_;
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NW = WM_ * WN_, T = NW * 64;
   static constexpr int BK = 32, S = S_;   // S LDS stages: S - 1 k-steps in flight ahead of the one multiplied
   static constexpr bool AK = AK_, BKM = BKM_;
@@ -59,6 +62,7 @@ struct BGemmCfg {
   static_assert(LA % NW == 0 && LB % NW == 0, "every wave issues the same DMA count per operand");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile of whole 16 x 16 MFMA tiles");
   static_assert(!AK || BM == 64 || BM == 128, "k-major images are 64 or 128 rows");
+  static_assert(std::is_void<AG_>::value || (AK_ && BM_ == 128), "a gathered A operand is a 128-row k-major image");
   static_assert(!BKM || BN == 64 || BN == 128, "k-major images are 64 or 128 rows");
   static_assert(S >= 2 && S <= 8 && (S - 1) * (LPA + LPB) <= 63, "vmcnt counts to 63");
 };
@@ -84,14 +88,26 @@ __device__ __forceinline__ int bswz_k(int kr) {
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
-// One operand's DMA and fragment addressing inside a tile.  Instruction j of this wave covers image bytes
-// [1024 (wave + NW j), + 1024).
+// One operand's DMA inside a tile.  Instruction j of this wave covers image bytes [1024 (wave + NW j), + 1024).  The
+// descriptor of a k-major operand starts at the tile's first k-row and ends at its last (k-rows past the split read zeros,
+// so a split's k range need not be a multiple of BK); a row-major one spans the operand (rows past it read zeros).
 template <bool KM, int BR, int NW, int LP>
 struct BStage {
   uint32_t voff[LP];   // per-lane source byte offsets (k0 = 0); kOobOffset for rows past the operand
   int first;           // this wave's first instruction index
-  __device__ void init(const BOp& o, int row0, int wave, int lane) {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t base, step;   // soffset of k-step t = base + t * step
+  __device__ void init(const BOp& o, int row0, int kb, int ke, int wave, int lane) {
     first = wave;
+    if constexpr (KM) {
+      rs = make_rsrc(o.p + (size_t)kb * o.ld, (uint32_t)((ke - kb) * o.ld * 2));
+      base = 0;
+      step = (uint32_t)(32 * o.ld * 2);
+    } else {
+      rs = make_rsrc(o.p, (uint32_t)(o.rows * o.ld * 2));
+      base = (uint32_t)(kb * 2);
+      step = 64u;
+    }
 #pragma unroll
     for (int j = 0; j < LP; ++j) {
       const int ii = wave + NW * j;
@@ -106,12 +122,72 @@ struct BStage {
       }
     }
   }
-  // issue this wave's DMA of k-step k0 into the operand image at img (LDS byte address of the image)
-  __device__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t soff, char* img) const {
+  // issue this wave's DMA of k-step t into the operand image at img (LDS byte address of the image)
+  __device__ void issue(int t, char* img) const {
+    const uint32_t soff = base + (uint32_t)t * step;
 #pragma unroll
     for (int j = 0; j < LP; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)(img + 1024 * (first + NW * j)), 16, voff[j], soff, 0, 0);
   }
+};
+
+// im2col geometry of a conv weight gradient's gathered operand: input in [B][IH][IW][C] (bf16), reduction index
+// k = b * P + oh * OW + ow (P = OH * OW output positions per sample), row m = (kh * KS + kw) * C + c (the HWIO row of dW).
+// Element offset of (m, k) = kbase(k) + roff(m); 8 consecutive rows (one 16-byte chunk, 8 | C) are contiguous.
+template <int IH_, int IW_, int C_, int KS_, int S_, int OH_, int OW_>
+struct ConvGather {
+  static constexpr int IH = IH_, IW = IW_, C = C_, KS = KS_, S = S_, OH = OH_, OW = OW_, P = OH_ * OW_, M = KS_ * KS_ * C_;
+  static_assert(C % 8 == 0, "16-byte chunks of one tap");
+  __device__ static uint32_t kbase(int k) {
+    const int b = k / P, p = k - b * P, oh = p / OW, ow = p - oh * OW;
+    return (uint32_t)(((b * IH + oh * S) * IW + ow * S) * C);
+  }
+  __device__ static uint32_t roff(int m) {
+    const int tap = m / C, c = m - tap * C, kh = tap / KS, kw = tap - kh * KS;
+    return (uint32_t)((kh * IW + kw) * C + c);
+  }
+};
+
+// The gathered (im2col) A operand as a 128-row k-major image: lane chunk -> rows m0 + 8 gc .. + 7 of k-row kr, fetched from
+// in + kbase(k) + roff(m).  kbase is evaluated per k-step (a few VALU per DMA instruction); roff is fixed per lane.
+template <class G, int NW, int LP>
+struct BStageGather {
+  uint32_t roff[LP];
+  int kr[LP];
+  int first, kstart;
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ void init(const BOp& o, int row0, int kb, int ke, int wave, int lane) {
+    first = wave;
+    kstart = kb;
+    rs = make_rsrc(o.p, (uint32_t)((size_t)o.ld * 2));   // gathered operand: o.ld = elements of the whole input tensor
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      const int ii = wave + NW * j, k = ii * 4 + (lane >> 4), gc = (lane & 15) ^ bswz_k<128>(k);
+      const int m = row0 + 8 * gc;
+      kr[j] = k;
+      roff[j] = m < o.rows ? G::roff(m) : 0xFFFFFFFFu;
+    }
+  }
+  __device__ void issue(int t, char* img) const {
+    const int k0 = kstart + 32 * t;
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      const uint32_t v = roff[j] == 0xFFFFFFFFu ? (uint32_t)kOobOffset : (G::kbase(k0 + kr[j]) + roff[j]) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)(img + 1024 * (first + NW * j)), 16, v, 0, 0, 0);
+    }
+  }
+};
+
+template <class C, bool IS_A>
+struct BStageOf {
+  using type = BStage<IS_A ? C::AK : C::BKM, IS_A ? C::BM : C::BN, C::NW, IS_A ? C::LPA : C::LPB>;
+};
+template <class C>
+struct BStageA {
+  using type = std::conditional_t<std::is_void<typename C::AG>::value, typename BStageOf<C, true>::type,
+                                  BStageGather<std::conditional_t<std::is_void<typename C::AG>::value, ConvGather<1, 1, 8, 1, 1, 1, 1>,
+                                                                  typename C::AG>,
+                                               C::NW, C::LPA>>;
 };
 
 // fragment read addresses (byte offsets inside an operand image) for fragment f of a wave whose rows start at r0
@@ -209,23 +285,14 @@ __device__ __forceinline__ void bgemm_tile(const BGemmProblem<Epi>& P, int tile,
   const int m0 = bx * C::BM, n0 = by * C::BN;
   const int kb = bz * P.kps, ke = min(P.K, kb + P.kps);
   const int nk = (ke - kb + C::BK - 1) / C::BK;
-  // descriptor ranges: row-major operands [rows][ld], k-major ones [K][ld] (k-rows past K read zeros)
-  const __amdgpu_buffer_rsrc_t rA =
-      make_rsrc(P.A.p, (uint32_t)((C::AK ? P.K : P.A.rows) * P.A.ld * 2));
-  const __amdgpu_buffer_rsrc_t rB =
-      make_rsrc(P.B.p, (uint32_t)((C::BKM ? P.K : P.B.rows) * P.B.ld * 2));
-  BStage<C::AK, C::BM, C::NW, C::LPA> sa;
-  BStage<C::BKM, C::BN, C::NW, C::LPB> sb;
-  sa.init(P.A, m0, wave, lane);
-  sb.init(P.B, n0, wave, lane);
-  const uint32_t stepA = C::AK ? (uint32_t)(C::BK * P.A.ld * 2) : (uint32_t)(C::BK * 2);
-  const uint32_t stepB = C::BKM ? (uint32_t)(C::BK * P.B.ld * 2) : (uint32_t)(C::BK * 2);
-  const uint32_t baseA = C::AK ? (uint32_t)(kb * P.A.ld * 2) : (uint32_t)(kb * 2);
-  const uint32_t baseB = C::BKM ? (uint32_t)(kb * P.B.ld * 2) : (uint32_t)(kb * 2);
+  typename BStageA<C>::type sa;
+  typename BStageOf<C, false>::type sb;
+  sa.init(P.A, m0, kb, ke, wave, lane);
+  sb.init(P.B, n0, kb, ke, wave, lane);
   auto issue = [&](int t, int stage) {
     char* st = lds + stage * C::STAGE;
-    sa.issue(rA, baseA + (uint32_t)t * stepA, st);
-    sb.issue(rB, baseB + (uint32_t)t * stepB, st + C::ABYTES);
+    sa.issue(t, st);
+    sb.issue(t, st + C::ABYTES);
   };
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
   uint32_t offA[C::FM], offB[C::FN];

@@ -733,18 +733,19 @@ void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipSt
   // conv3 (3 tap groups of 3 taps) + conv2 (2 groups of 8 taps) weight gradients in one launch, then
   // conv1's; per-block fp32 partials of [dW | db] rows, reduced in fixed order by one grouped launch
   // straight into the flat gradient (each layer's b follows its W; conv1 goes s2d -> HWIO)
-  using CW3 = ConvWgradCfg<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>;
-  using CW2 = ConvWgradCfg<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>;
+  using CW3 = ConvWgradCfg<9, 9, 64, 3, 1, 7, 7, 3, 3, 2, kWg3Samples>;
+  using CW2 = ConvWgradCfg<20, 20, 32, 4, 2, 9, 9, 8, 2, 4, kWg2Samples>;
   static_assert(85 * CW3::ZS <= kSlabConv2 && kSlabConv2 + 128 * CW2::ZS <= kSlabConv1 &&
                     kSlabConv1 + 256 * (size_t)kConv1SlabStride <= kWgradSlabFloats,
                 "slab regions overlap");
-  auto chunking = [&](int groups, int& per) {
+  // about 256 blocks per layer; a chunk is a whole number of LDS rounds (ns samples each)
+  auto chunking = [&](int groups, int ns, int& per) {
     const int chunks = std::max(1, std::min(B, 256 / groups));
-    per = (B + chunks - 1) / chunks;
+    per = ((B + chunks - 1) / chunks + ns - 1) / ns * ns;
     return (B + per - 1) / per;
   };
   int per3 = 0, per2 = 0;
-  const int used3 = chunking(3, per3), used2 = chunking(2, per2);
+  const int used3 = chunking(3, kWg3Samples, per3), used2 = chunking(2, kWg2Samples, per2);
   {
     ProfScope ps(m->prof, "conv23_wgrad", s, 2.0 * B * (49.0 * 576 * 64 + 81.0 * 512 * 64));
     constexpr size_t lds = std::max(CW3::LDS, CW2::LDS);

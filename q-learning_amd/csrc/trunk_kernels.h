@@ -737,39 +737,43 @@ namespace qn {
 // KTW k-tiles (16 rows of dW each) x NTW of the four 16-column n-tiles.
 // Output: slab[chunk][TAPS*C*64 + 64] rows of [dW partial | db partial] (db from tap group 0 only).
 // Launched as k_conv23_wgrad (conv3 and conv2 blocks in one grid).
-template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW>
+template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW, int NS_ = 1>
 struct ConvWgradCfg {
+  static constexpr int NS = NS_;   // samples staged per LDS round (round 5: one sample per round left 2 m-steps of MFMA
+                                   // work (conv3) between each pair of barriers)
   static constexpr int M = OH * OW, MP = (M + 31) / 32 * 32;   // positions, padded to the 32-row m-step
   static constexpr int XS = C + (C == 32 ? 8 : 16);            // input row stride (bf16): 20 / 40 dwords
   static constexpr int DS = 64 + 16;                            // dz row stride: 40 dwords
   static constexpr int LX = IH * IW * XS, LD = MP * DS;
-  static constexpr size_t LDS = (size_t)(LX + LD) * 2;
+  static constexpr size_t LDS = (size_t)NS * (LX + LD) * 2;
   static constexpr int KTILES = TG * C / 16;                    // 16-row k tiles per block
   static_assert(4 % NTW == 0 && (KTILES / KTW) * (4 / NTW) == 8 && KTILES % KTW == 0,
                 "KTW k tiles x NTW n tiles per wave must cover the block's KTILES x 4 tiles with 8 waves");
   static constexpr int CHX = IH * IW * C / 8, CHD = M * 64 / 8;  // 16-byte chunks per sample
-  static constexpr int PF = (CHX + CHD + kTrunkThreads - 1) / kTrunkThreads;
+  static constexpr int PF = (NS * (CHX + CHD) + kTrunkThreads - 1) / kTrunkThreads;
   static constexpr int TAPS = KS * KS;
   static constexpr size_t ZS = (size_t)TAPS * C * 64 + 64;      // slab row
 };
 
-template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW>
+template <int IH, int IW, int C, int KS, int S, int OH, int OW, int TG, int KTW, int NTW, int NS>
 __device__ __forceinline__ void conv_wgrad_body(const bf16* __restrict__ in, const bf16* __restrict__ dz, int B, int per_chunk,
                                                 float* slab, int chunk, int tg) {
-  using Cf = ConvWgradCfg<IH, IW, C, KS, S, OH, OW, TG, KTW, NTW>;
+  using Cf = ConvWgradCfg<IH, IW, C, KS, S, OH, OW, TG, KTW, NTW, NS>;
   constexpr int M = Cf::M, MP = Cf::MP, XS = Cf::XS, DS = Cf::DS;
   constexpr int CHX = Cf::CHX, CHD = Cf::CHD, PF = Cf::PF;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  bf16* X = lds;
-  bf16* DZ = lds + Cf::LX;
+  bf16* X = lds;                   // NS images [IH * IW][XS]
+  bf16* DZ = lds + NS * Cf::LX;    // NS images [MP][DS]
   const int tid = threadIdx.x, wave = wave_id(), lane = tid & 63;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int b0 = chunk * per_chunk, b1 = min(B, b0 + per_chunk);
   // wave's tiles: k tiles kt0 .. kt0+KTW-1, n tiles nt0 .. nt0+NTW-1
   constexpr int NGROUPS = 4 / NTW;                  // waves sharing a k-tile set
   const int kt0 = (wave / NGROUPS) * KTW, nt0 = (wave % NGROUPS) * NTW;
-  for (int i = tid; i < (MP - M) * DS / 8; i += kTrunkThreads)   // zero dz pad rows once
-    *reinterpret_cast<uint4*>(DZ + M * DS + i * 8) = uint4{0, 0, 0, 0};
+  for (int i = tid; i < NS * (MP - M) * DS / 8; i += kTrunkThreads) {   // zero the dz pad rows once
+    const int s = i / ((MP - M) * DS / 8), r = i - s * ((MP - M) * DS / 8);
+    *reinterpret_cast<uint4*>(DZ + s * Cf::LD + M * DS + r * 8) = uint4{0, 0, 0, 0};
+  }
   f32x4 acc[KTW][NTW];
 #pragma unroll
   for (int a = 0; a < KTW; ++a)
@@ -782,35 +786,41 @@ __device__ __forceinline__ void conv_wgrad_body(const bf16* __restrict__ in, con
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   uint4 pf[PF];
+  // chunk c of a round: sample s = c / (CHX + CHD) of the round, then its input chunks, then its dz chunks
   auto prefetch = [&](int b) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
-      const int c = tid + u * kTrunkThreads;
+      const int c = tid + u * kTrunkThreads, s = c / (CHX + CHD), cc = c - s * (CHX + CHD);
       pf[u] = uint4{0, 0, 0, 0};
-      if (b < b1 && c < CHX + CHD)
-        pf[u] = __builtin_bit_cast(uint4, c < CHX ? *(gvec*)(in + (size_t)b * (IH * IW * C) + c * 8)
-                                                  : *(gvec*)(dz + (size_t)b * (M * 64) + (c - CHX) * 8));
+      if (b + s < b1 && s < NS)
+        pf[u] = __builtin_bit_cast(uint4, cc < CHX ? *(gvec*)(in + (size_t)(b + s) * (IH * IW * C) + cc * 8)
+                                                   : *(gvec*)(dz + (size_t)(b + s) * (M * 64) + (cc - CHX) * 8));
     }
   };
   auto tr = [](const bf16* pp) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pp)); };
   prefetch(b0);
-  for (int b = b0; b < b1; ++b) {
-    lds_barrier();   // previous sample's readers are done
+  for (int b = b0; b < b1; b += NS) {
+    lds_barrier();   // previous round's readers are done
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
-      const int c = tid + u * kTrunkThreads;
-      if (c < CHX) {
-        const int row = c / (C / 8), col = (c - row * (C / 8)) * 8;
-        *reinterpret_cast<uint4*>(X + row * XS + col) = pf[u];
-      } else if (c < CHX + CHD) {
-        const int cc = c - CHX, row = cc >> 3, col = (cc & 7) * 8;
-        *reinterpret_cast<uint4*>(DZ + row * DS + col) = pf[u];
+      const int c = tid + u * kTrunkThreads, s = c / (CHX + CHD), cc = c - s * (CHX + CHD);
+      if (s < NS) {   // samples past the chunk stage zeros (their dz rows contribute nothing)
+        if (cc < CHX) {
+          const int row = cc / (C / 8), col = (cc - row * (C / 8)) * 8;
+          *reinterpret_cast<uint4*>(X + s * Cf::LX + row * XS + col) = pf[u];
+        } else {
+          const int cd = cc - CHX, row = cd >> 3, col = (cd & 7) * 8;
+          *reinterpret_cast<uint4*>(DZ + s * Cf::LD + row * DS + col) = pf[u];
+        }
       }
     }
     lds_barrier();
-    prefetch(b + 1);
+    prefetch(b + NS);
 #pragma unroll 1
-    for (int m0 = 0; m0 < MP; m0 += 32) {
+    for (int sm = 0; sm < NS * MP; sm += 32) {
+      const int s = sm / MP, m0 = sm - s * MP;
+      const bf16* X = lds + s * Cf::LX;
+      const bf16* DZ = lds + NS * Cf::LX + s * Cf::LD;
       // this lane's two tr-read rows: m0 + 4g + q and m0 + 16 + 4g + q (clamped; their dz rows are zero)
       const int mA = min(m0 + 4 * g + q, M - 1), mB = min(m0 + 16 + 4 * g + q, M - 1);
       const int ohA = mA / OW, owA = mA - ohA * OW, ohB = mB / OW, owB = mB - ohB * OW;
@@ -834,7 +844,8 @@ __device__ __forceinline__ void conv_wgrad_body(const bf16* __restrict__ in, con
       }
     }
     if (tg == 0)
-      for (int m = brg; m < M; m += 8) bsum += (float)DZ[m * DS + bn];
+      for (int s = 0; s < NS; ++s)
+        for (int m = brg; m < M; m += 8) bsum += (float)DZ[s * Cf::LD + m * DS + bn];
   }
   // D tile (a, c): row k = (tg * KTILES + kt0 + a) * 16 + 4g + e, col n = (nt0 + c) * 16 + li
   float* out = slab + (size_t)chunk * Cf::ZS;
@@ -870,6 +881,9 @@ __device__ __forceinline__ bool wgrad_chunk_group(int t, int used, int& chunk, i
 }
 __host__ __device__ __forceinline__ int wgrad_blocks(int groups, int used) { return (used + 7) / 8 * 8 * groups; }
 
+// samples per LDS round (the chunk sizes are multiples of these, qnet.hip).  Measured at C3 (bf16, gpurun_out/a8): conv3 4 and
+// conv2 2 samples per round (95 KB of LDS) took the launch 25.8 -> 34.3 us; one sample per round is kept
+constexpr int kWg3Samples = 1, kWg2Samples = 1;
 // conv3 (blocks [0, wgrad_blocks(3, used3))) and conv2 (the rest) in one launch
 __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv23_wgrad(const bf16* __restrict__ a2, const bf16* __restrict__ dz3,
                                                                    int per3, int used3, float* slab3, const bf16* __restrict__ a1,
@@ -879,9 +893,9 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_conv23_wgrad(const bf16* _
   int chunk, group;
   if (t < n3) {
     if (wgrad_chunk_group<3>(t, used3, chunk, group))
-      conv_wgrad_body<9, 9, 64, 3, 1, 7, 7, 3, 3, 2>(a2, dz3, B, per3, slab3, chunk, group);
+      conv_wgrad_body<9, 9, 64, 3, 1, 7, 7, 3, 3, 2, kWg3Samples>(a2, dz3, B, per3, slab3, chunk, group);
   } else if (wgrad_chunk_group<2>(t - n3, used2, chunk, group)) {
-    conv_wgrad_body<20, 20, 32, 4, 2, 9, 9, 8, 2, 4>(a1, dz2, B, per2, slab2, chunk, group);
+    conv_wgrad_body<20, 20, 32, 4, 2, 9, 9, 8, 2, 4, kWg2Samples>(a1, dz2, B, per2, slab2, chunk, group);
   }
 }
 
