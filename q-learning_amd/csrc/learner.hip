@@ -522,6 +522,9 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
     debug_sync(s, "sample");
     learner_targets(L, U);
     for (uint32_t u = 0; u < U; ++u) learner_update(L, u);
+    // the last update's dense variables may still be in flight on the model's aux stream (qnet32.hip f32_dense_async): the
+    // vector step ends with every weight final on the learner stream (host reads, target sync, the next acting forward)
+    model_dense_join(L->online, s);
     if (L->per) {
       ProfScope ps(&L->prof, "priorities", s);
       per_launch_update(s, L->d_idx, L->prio.d_td, U * L->B, cap, start, L->p.per_alpha, L->p.per_eps, L->prio.d_owner,

@@ -102,6 +102,14 @@ struct qlx_model {
   // partials of the reduced gradient x f32_partials_scale; model_adam then runs the same k_update32 tail
   bool f32_dense_partials = false;
   float f32_partials_scale = 1.0f;
+  // dense-variable update beside the conv backward (QLX_F32_DENSE_OVERLAP, scheduled update only): the dense clip-norm
+  // partials + Adam run on f32_aux from the end of the fc1 backward; the next fc1 forward (and every host-visible sync of
+  // the model) joins it.  f32_dense_async: this update's dense part went to f32_aux (k_update32 then runs the conv blocks).
+  bool dense_overlap = false;
+  bool f32_dense_async = false;
+  bool dense_pending = false;
+  hipStream_t f32_aux = nullptr;
+  hipEvent_t ev_dense_ready = nullptr, ev_dense_done = nullptr;
   // bf16 forward: fc1 as one pass with the fused epilogue at every batch size (no batch-size-dependent split-K), so a
   // sample's result does not depend on the batch it is evaluated in (the learner's target net)
   bool fc1_single = false;
@@ -169,6 +177,10 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
 void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update);
 void f32_norms(qlx_model* m, hipStream_t s, float scale);
 void f32_adam(qlx_model* m, hipStream_t s, float scale);
+// the dense variables' norm partials + Adam of the update in flight on m->f32_aux (after the fc1 backward on s)
+void f32_dense_async(qlx_model* m, hipStream_t s);
+// stream s waits for a pending dense update (before anything reads W3 / b3 / W4 / b4 again)
+void model_dense_join(qlx_model* m, hipStream_t s);
 // fractions of a batch's fp32 conv work the exact skips leave out (qnet32.hip k_frame_sparsity; synchronises s):
 // out = {conv1 forward zero steps, conv1 weight-gradient zero steps, conv2 background rows, conv3 background rows}
 void frame_sparsity(const uint8_t* const* table, int n, double* out, hipStream_t s);

@@ -173,32 +173,47 @@ struct NormArgs {
   int64_t off[kNumVars + 1];
 };
 // thread tl (0 .. 255) of segment j of variable v (elements off[v] ..): its fmaf chain over its eight elements, then its
-// wave's xor butterfly (every lane ends with the wave sum); segments past the variable's end chain zeros
-__device__ __forceinline__ float norm32_lane(const float* gall, const int64_t* off, float scale, int v, int j, int tl) {
+// wave's xor butterfly (every lane ends with the wave sum); segments past the variable's end chain zeros.
+// The loads are split from the chain so a caller can put every segment's loads in flight before the first add: variables
+// whose length is a multiple of 4 (all but b4) read through a buffer descriptor spanning the variable, elements past its
+// end reading as zeros - no per-lane branch around the loads (round 5: the branchy form serialised the five segment
+// rounds of a conv update block).
+struct NormLd {
+  f32x4 x[2];
+};
+__device__ __forceinline__ NormLd norm32_load(const float* gall, const int64_t* off, int v, int j, int tl, bool live) {
   const int64_t n = off[v + 1] - off[v];
   const int64_t b = (int64_t)j * kNormSeg;
   const float* g = gall + off[v];   // variable offsets are multiples of 4 floats (16-byte loads)
-  f32x4 x[2];
+  NormLd L;
+  if (n % 4 == 0) {   // wave-uniform
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(g, live ? (uint32_t)(n * 4) : 0u);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) L.x[h] = buf_ld4(rs, (uint32_t)((b + 1024 * h + 4 * tl) * 4), 0);
+    return L;
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int64_t i = b + 1024 * h + 4 * tl;
-    if (i + 4 <= n) {
-      x[h] = ld4(g + i);
-    } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) x[h][k] = i + k < n ? g[i + k] : 0.0f;   // zeros leave the chain unchanged
-    }
+    for (int k = 0; k < 4; ++k) L.x[h][k] = live && i + k < n ? g[i + k] : 0.0f;   // zeros leave the chain unchanged
   }
+  return L;
+}
+__device__ __forceinline__ float norm32_chain(const NormLd& L, float scale) {
   float t = 0.0f;
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float y = __fmul_rn(x[h][k], scale);
+      const float y = __fmul_rn(L.x[h][k], scale);
       t = fmaf(y, y, t);
     }
   for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
   return t;
+}
+__device__ __forceinline__ float norm32_lane(const float* gall, const int64_t* off, float scale, int v, int j, int tl) {
+  return norm32_chain(norm32_load(gall, off, v, j, tl, true), scale);
 }
 
 // Conv weight gradients from the sample-chunk partials, two levels: the chunks in groups of kWGroup (group q = chunks
@@ -445,12 +460,13 @@ __device__ __forceinline__ void conv_adam_block(const Adam32Args& A, const NormA
     m = ld4(A.m + i0);
     vv = ld4(A.v + i0);
   }
+  // every segment's loads in flight at once, then the chains (segments past the variable: zeros, t = 0)
+  NormLd ld[kConvSegsPerGroup];
+#pragma unroll
+  for (int r = 0; r < kConvSegsPerGroup; ++r) ld[r] = norm32_load(N.g, N.off, v, grp + 4 * r, tl, grp + 4 * r < nseg);
   float t[kConvSegsPerGroup];
 #pragma unroll
-  for (int r = 0; r < kConvSegsPerGroup; ++r) {
-    const int j = grp + 4 * r;
-    t[r] = j < nseg ? norm32_lane(N.g, N.off, N.scale, v, j, tl) : 0.0f;
-  }
+  for (int r = 0; r < kConvSegsPerGroup; ++r) t[r] = grp + 4 * r < nseg ? norm32_chain(ld[r], N.scale) : 0.0f;
 #pragma unroll
   for (int r = 0; r < kConvSegsPerGroup; ++r)
     if ((tl & 63) == 0) wsum[r][grp][tl >> 6] = t[r];
@@ -746,12 +762,14 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       if (big) {
         // (64 x 32 list tiles here: conv2 / conv3 145 / 185 us against 139 / 181 us, gpurun_out/w10)
         run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<64, 64, 2, 2>{}, "f32_conv2_fwd_big", "f32_conv3_fwd_big");
+        model_dense_join(m, s);   // W3 / b3 of a dense update in flight on the aux stream
         launch(m, PFc1FwdB{grid(n, PFc1FwdB::BM, 512, PFc1FwdB::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
                2.0 * n * 3136 * 512, s);
       } else {
         // (on the stream core, in place: conv2 64 x 64 24.3 us against 27.9 us for 64 x 32 and 28.7 for 32 x 64; conv3 32 x 64
         // 27.6 us against 28.5 / 29.8 for 64 x 32 / 64 x 64 - gpurun_out/w10)
         run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<32, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        model_dense_join(m, s);
         launch(m, PFc1FwdS{grid(n, PFc1FwdS::BM, 512, PFc1FwdS::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);
       }
@@ -761,6 +779,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
              2.0 * n * 81 * 64 * 512, s);
       launch(m, PConv3Fwd{grid(n * 49, 64, 64, 64, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49}, "f32_conv3_fwd_big",
              2.0 * n * 49 * 64 * 576, s);
+      model_dense_join(m, s);
       launch(m, PFc1FwdB{grid(n, PFc1FwdB::BM, 512, PFc1FwdB::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd_big",
              2.0 * n * 3136 * 512, s);
     } else {
@@ -768,6 +787,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
                                       PConv2FwdS{grid(n * 81, 64, 64, 32, 1), w.fa1, p + voff(2), p + voff(3), w.fa2, n * 81});
       conv_fwd<PConv3Fwd, PConv3FwdR>(m, n * 49, w.fa2, p + voff(4), p + voff(5), w.fa3, "f32_conv3_fwd", 2.0 * n * 49 * 64 * 576, s,
                                       PConv3FwdS{grid(n * 49, 64, 64, 32, 1), w.fa2, p + voff(4), p + voff(5), w.fa3, n * 49});
+      model_dense_join(m, s);
       launch(m, PFc1FwdS{grid(n, PFc1FwdS::BM, 512, PFc1FwdS::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
              2.0 * n * 3136 * 512, s);
     }
@@ -901,7 +921,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
       nred += R.nb[L];
     }
     // the scheduled update: + the dense variables' clip-norm segment partials (4 per block)
-    const int dseg = m->f32_update_scheduled ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
+    const int dseg = m->f32_update_scheduled && !m->f32_dense_async ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
     hipLaunchKernelGGL(k_wreduce32, dim3(nred + (dseg + 3) / 4), dim3(1024), 0, s, R, N, nred, N.seg_first[6], dseg);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_wreduce32");
@@ -928,19 +948,55 @@ void f32_norms(qlx_model* m, hipStream_t s, float scale) {
 // clip_by_norm + Adam of every variable in one launch (k_update32): the conv blocks finish their variable's norm from the
 // (scaled) gradient, the dense blocks from the partials of the reduction launch (world 1) or of f32_norms (data parallel).
 // One tail for both, so a rank's update is the single-GPU update of its reduced gradient (bit-identical at world 1).
+constexpr int kDenseAdamBlocks = (int)((kNumParams - kVarOffsetDense) / 4 / 2048 + 1);   // 2 float4 groups per thread
+
 void f32_adam(qlx_model* m, hipStream_t s, float scale) {
   const int64_t t = m->iterations + 1;
   const Adam32Args a = adam_args(m, scale);
   QLX_CHECK(m->f32_update_scheduled ? scale == 1.0f : (m->f32_dense_partials && scale == m->f32_partials_scale), QLX_E_STATE,
             "fp32 update without the dense norm partials of this gradient scale (model_norms first)");
-  ProfScope ps(m->prof, "f32_adam", s, 28.0 * kNumParams);
-  const int nconv = conv_adam_blocks(), ndense = (int)((kNumParams - kVarOffsetDense) / 4 / 2048 + 1);   // 2 groups / thread
-  hipLaunchKernelGGL(k_update32, dim3(nconv + ndense), dim3(1024), 0, s, a, norm_args(m, scale), nconv, ndense);
+  const bool dense_here = !m->f32_dense_async;   // else the dense blocks run on f32_aux (f32_dense_async)
+  ProfScope ps(m->prof, "f32_adam", s, dense_here ? 28.0 * kNumParams : 28.0 * kVarOffsetDense);
+  const int nconv = conv_adam_blocks(), ndense = kDenseAdamBlocks;
+  hipLaunchKernelGGL(k_update32, dim3(nconv + (dense_here ? ndense : 0)), dim3(1024), 0, s, a, norm_args(m, scale), nconv, ndense);
   QLX_HIP(hipGetLastError());
   debug_sync(s, "k_update32");
   m->f32_update_scheduled = false;
   m->f32_dense_partials = false;
+  m->f32_dense_async = false;
   m->iterations = t;
+}
+
+// The dense variables (W3, b3, W4, b4: 95 % of the update's Adam bytes) are final after the fc1 backward and are next read
+// by the next forward's fc1: their clip-norm segment partials (k_wreduce32's dense blocks) and clip_by_norm + Adam
+// (k_update32's dense blocks) run on a second stream from there, beside the conv backward, the conv update and the next
+// forward's convs.  Same kernels and arithmetic as the one-stream tail, so the results are bit-identical.
+void f32_dense_async(qlx_model* m, hipStream_t s) {
+  if (!m->f32_aux) {
+    QLX_HIP(hipStreamCreateWithFlags(&m->f32_aux, hipStreamNonBlocking));
+    QLX_HIP(hipEventCreateWithFlags(&m->ev_dense_ready, hipEventDisableTiming));
+    QLX_HIP(hipEventCreateWithFlags(&m->ev_dense_done, hipEventDisableTiming));
+  }
+  hipStream_t a = m->f32_aux;
+  QLX_HIP(hipEventRecord(m->ev_dense_ready, s));
+  QLX_HIP(hipStreamWaitEvent(a, m->ev_dense_ready, 0));
+  ProfScope ps(m->prof, "f32_dense_update", a, 28.0 * (kNumParams - kVarOffsetDense));
+  const NormArgs N = norm_args(m, 1.0f);
+  const int dseg = N.seg_first[kNumVars] - N.seg_first[6];
+  const WRed R{};
+  hipLaunchKernelGGL(k_wreduce32, dim3((dseg + 3) / 4), dim3(1024), 0, a, R, N, 0, N.seg_first[6], dseg);
+  hipLaunchKernelGGL(k_update32, dim3(kDenseAdamBlocks), dim3(1024), 0, a, adam_args(m, 1.0f), N, 0, kDenseAdamBlocks);
+  QLX_HIP(hipGetLastError());
+  QLX_HIP(hipEventRecord(m->ev_dense_done, a));
+  debug_sync(a, "dense update (aux stream)");
+  m->f32_dense_async = true;
+  m->dense_pending = true;
+}
+
+void model_dense_join(qlx_model* m, hipStream_t s) {
+  if (!m->dense_pending) return;
+  QLX_HIP(hipStreamWaitEvent(s, m->ev_dense_done, 0));
+  m->dense_pending = false;
 }
 
 

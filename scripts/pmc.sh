@@ -5,8 +5,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-RE="${QLX_PMC_REGEX:-k_trunk|k_conv|k_gemm|k_fc1|k_adam|k_norm|k_slab|k_replay|k_env|k_sample|k_head|k_wreduce|k_slot}"
-ARGS="--steps 2 --warmup 1 --beside-steps 0 --nomemo-steps 0 --dense-steps 0 --sparsity-steps 0 --cpu-sample 0 --profile-steps 1 ${QLX_PMC_ARGS:-}"
+RE="${QLX_PMC_REGEX:-k_trunk|k_conv|k_gemm|k_bgemm|k_fc1|k_fc2|k_adam|k_update|k_slab|k_replay|k_env|k_sample|k_head|k_wreduce|k_slot}"
+ARGS="--steps 2 --warmup 1 --beside-steps 0 --nomemo-steps 0 --dense-steps 0 --refwork-steps 0 --dp1-steps 0 --sparsity-steps 0 --cpu-sample 0 --profile-steps 1 ${QLX_PMC_ARGS:-}"
 run() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-include-regex "$RE" --pmc "$@" --output-format csv -d gpurun_out/pmc/$name -o c -- \

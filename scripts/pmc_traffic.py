@@ -41,6 +41,9 @@ SCOPES = {
         "conv1_wgrad": "k_conv1_wgrad",
         "conv23_wgrad": "k_conv23_wgrad",
         "fc1_bwd": "k_fc1_bwd",
+        "fc1_fwd": "k_bgemm<qlx::qn::BGemmCfg<128, 64, 2, 2, false, true, 4",   # the training-batch forward (4 k splits)
+        "wgrad_reduce": "k_slab_reduce3",
+        "fc2_head": "k_fc2_train",
         "adam": "k_adam(",
     },
 }

@@ -40,6 +40,19 @@ __global__ void k_ref(const bf16* A, int lda, bool ak, const bf16* B, int ldb, b
   C[i] = s;
 }
 
+// reference conv weight gradient: dW[(kh KS + kw) C + c][n] = sum_b,oh,ow in[b][oh S + kh][ow S + kw][c] dz[b][oh][ow][n]
+__global__ void k_ref_conv(const bf16* in, const bf16* dz, int B, int IH, int IW, int C, int KS, int S, int OH, int OW, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, M = KS * KS * C;
+  if (i >= M * 64) return;
+  const int m = i / 64, n = i % 64, tap = m / C, c = m % C, kh = tap / KS, kw = tap % KS;
+  float s = 0.0f;
+  for (int b = 0; b < B; ++b)
+    for (int oh = 0; oh < OH; ++oh)
+      for (int ow = 0; ow < OW; ++ow)
+        s += (float)in[(((size_t)b * IH + oh * S + kh) * IW + ow * S + kw) * C + c] * (float)dz[(((size_t)b * OH + oh) * OW + ow) * 64 + n];
+  out[i] = s;
+}
+
 __global__ void k_fill(bf16* p, int64_t n, uint32_t seed, float lo, float hi, float zero_frac) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t h = (uint32_t)i * 2654435761u ^ seed;
@@ -235,6 +248,47 @@ int main(int argc, char** argv) {
     fwd(BGemmCfg<128, 128, 2, 2, false, true, 4>{}, 7, "fwd 128x128 S4 split7");
     fwd_big(BGemmCfg<128, 128, 2, 2, false, true, 4>{}, "fwd8192 128x128 S4");
     return 0;
+  }
+  {  // conv weight gradients on the gathered (im2col) operand: conv3 (a2 x dz3) and conv2 (a1 x dz2)
+    bf16 *a1, *a2, *dz2, *dz3;
+    CK(hipMalloc(&a1, (size_t)B * 12800 * 2));
+    CK(hipMalloc(&a2, (size_t)B * 5184 * 2));
+    CK(hipMalloc(&dz2, (size_t)B * 5184 * 2));
+    CK(hipMalloc(&dz3, (size_t)B * 3136 * 2));
+    k_fill<<<1024, 256>>>(a1, (int64_t)B * 12800, 5, 0.0f, 2.0f, 0.5f);
+    k_fill<<<1024, 256>>>(a2, (int64_t)B * 5184, 6, 0.0f, 2.0f, 0.5f);
+    k_fill<<<1024, 256>>>(dz2, (int64_t)B * 5184, 7, -1e-3f, 1e-3f, 0.5f);
+    k_fill<<<1024, 256>>>(dz3, (int64_t)B * 3136, 8, -1e-3f, 1e-3f, 0.3f);
+    CK(hipDeviceSynchronize());
+    auto conv = [&](auto cfg, const bf16* in, int inel, const bf16* dz, int P_, int M, int SC, int IH, int IW, int C_, int KS, int S_, int OH,
+                    int OW, const char* name) {
+      using C = decltype(cfg);
+      const int K = B * P_, kps = SC * P_;
+      BGemmProblem<Epi4Slab> Pr{BOp{in, inel, M}, BOp{dz, 64, 64}, M, 64, K, kps, -1, (M + C::BM - 1) / C::BM, 1,
+                                (K + kps - 1) / kps, 0, Epi4Slab{slab, 64, (size_t)M * 64}};
+      launch<C>(Pr, 0);
+      CK(hipDeviceSynchronize());
+      auto sl = get_f(slab, (size_t)Pr.splits * M * 64);
+      std::vector<float> got((size_t)M * 64, 0.0f);
+      for (int z = 0; z < Pr.splits; ++z)
+        for (size_t i = 0; i < got.size(); ++i) got[i] += sl[(size_t)z * M * 64 + i];
+      hipLaunchKernelGGL(k_ref_conv, dim3((M * 64 + 255) / 256), dim3(256), 0, 0, in, dz, B, IH, IW, C_, KS, S_, OH, OW, ref);
+      CK(hipDeviceSynchronize());
+      check(got, get_f(ref, (size_t)M * 64), name, 2e-3);
+      const float us = time_us([&] { launch<C>(Pr, 0); });
+      const float l2 = time_cold_us([&] { launch<C>(Pr, 0); }, (size_t)128 << 20);
+      const double f = 2.0 * K * M * 64;
+      std::printf("    %.2f us  %.1f TF  %.3f of peak (%d blocks, %d chunks); L2 flushed %.2f us\n", us, f / us * 1e-6,
+                  f / us * 1e-6 / peak, Pr.tiles(), Pr.splits, l2);
+    };
+    using G3 = ConvGather<9, 9, 64, 3, 1, 7, 7>;
+    using G2 = ConvGather<20, 20, 32, 4, 2, 9, 9>;
+    conv(BGemmCfg<128, 64, 2, 2, true, true, 4, 0, G3>{}, a2, B * 5184, dz3, 49, 576, 20, 9, 9, 64, 3, 1, 7, 7, "conv3 wgrad SC20 S4");
+    conv(BGemmCfg<128, 64, 2, 2, true, true, 6, 0, G3>{}, a2, B * 5184, dz3, 49, 576, 20, 9, 9, 64, 3, 1, 7, 7, "conv3 wgrad SC20 S6");
+    conv(BGemmCfg<128, 64, 2, 2, true, true, 4, 0, G3>{}, a2, B * 5184, dz3, 49, 576, 40, 9, 9, 64, 3, 1, 7, 7, "conv3 wgrad SC40 S4");
+    conv(BGemmCfg<128, 64, 2, 2, true, true, 4, 0, G2>{}, a1, B * 12800, dz2, 81, 512, 16, 20, 20, 32, 4, 2, 9, 9, "conv2 wgrad SC16 S4");
+    conv(BGemmCfg<128, 64, 2, 2, true, true, 6, 0, G2>{}, a1, B * 12800, dz2, 81, 512, 16, 20, 20, 32, 4, 2, 9, 9, "conv2 wgrad SC16 S6");
+    conv(BGemmCfg<128, 64, 2, 2, true, true, 4, 0, G2>{}, a1, B * 12800, dz2, 81, 512, 32, 20, 20, 32, 4, 2, 9, 9, "conv2 wgrad SC32 S4");
   }
   fwd(BGemmCfg<128, 64, 2, 2, false, true, 4>{}, 4, "fwd 128x64 S4 split4");
   fwd(BGemmCfg<128, 64, 2, 2, false, true, 6>{}, 4, "fwd 128x64 S6 split4");

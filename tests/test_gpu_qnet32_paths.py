@@ -2,7 +2,8 @@
 
 The switches kept in the product (they have reporting roles: the bench's dense-frame figure) are exact alternatives:
 the dense conv2 / conv3 forward without background rows (QLX_F32_BG=0) and conv1 issuing its all-zero frame steps
-(QLX_F32_C1_SKIP=0), alone and together; and the grid shapes of a part with few CUs (QLX_NUM_CUS=8: a CPX partition
+(QLX_F32_C1_SKIP=0), alone and together; the dense variables' update on the model's second stream beside the conv backward
+(QLX_F32_DENSE_OVERLAP=1) or on the learner stream (=0); and the grid shapes of a part with few CUs (QLX_NUM_CUS=8: a CPX partition
 of an MI300X / MI355X - conv1 then runs more than two blocks per CU so that no block holds more than 64 samples).
 Each must give the oracle's bits (oracle/qnet32_ref.cpp, the same chains as tests/test_gpu_qnet32.py): Q values and the
 conv2 / conv3 activations of a 1,024-sample forward, Q of a 3,000-sample (chunk-size kernels) forward, and one training
@@ -95,7 +96,8 @@ def case(tmp_path_factory):
 
 
 @pytest.mark.parametrize("env", [{}, {"QLX_F32_BG": "0"}, {"QLX_F32_C1_SKIP": "0"},
-                                 {"QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"}, {"QLX_NUM_CUS": "8"}],
+                                 {"QLX_F32_BG": "0", "QLX_F32_C1_SKIP": "0"}, {"QLX_NUM_CUS": "8"},
+                                 {"QLX_F32_DENSE_OVERLAP": "1"}, {"QLX_F32_DENSE_OVERLAP": "0"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "default")
 def test_path_bit_exact(case, env):
     d, inp, exp = case
