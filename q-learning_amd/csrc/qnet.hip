@@ -547,6 +547,7 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 void model_workspace(qlx_model* m, int B) {
   if (m->f32) { f32_workspace(m, B); return; }
   if (B <= m->ws_batch) return;
+  model_dense_join(m, m->stream);
   QLX_HIP(hipStreamSynchronize(m->stream));
   if (m->ws) (void)hipFree(m->ws);
   m->ws = nullptr;
@@ -672,6 +673,8 @@ Fc2Args fc2_args(qlx_model* m, int B) {
 void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint8_t* actions, const float* y, float* loss_dev,
                     hipStream_t s, const float* weights, float* td_abs, bool fuse_update) {
   model_backward_dense(m, B, actions, y, loss_dev, s, weights, td_abs);
+  // fp32, no all-reduce: the dense variables' update can leave the learner stream here (qnet32.hip f32_dense_async)
+  if (m->f32 && fuse_update && m->dense_overlap) f32_dense_async(m, s);
   model_backward_conv(m, table, B, s, fuse_update);
 }
 
@@ -828,6 +831,7 @@ void model_frame_table_from_host(qlx_model* m, const uint8_t* obs_host, int B) {
   hipLaunchKernelGGL(k_pack_obs, dim3((B * kFramePix + 255) / 256), dim3(256), 0, m->stream, d_obs, B, m->w.frames);
   hipLaunchKernelGGL(k_frame_table, dim3((B * 4 + 255) / 256), dim3(256), 0, m->stream, m->w.frames, B, m->w.table);
   QLX_HIP(hipGetLastError());
+  model_dense_join(m, m->stream);
   QLX_HIP(hipStreamSynchronize(m->stream));
   QLX_HIP(hipFree(d_obs));
 }
@@ -877,6 +881,8 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
     m->f32_bg_rows = !(bg && bg[0] == '0');
     const char* sk = std::getenv("QLX_F32_C1_SKIP");
     m->f32_c1_skip = (sk && sk[0] == '0') ? 0 : 1;
+    const char* dov = std::getenv("QLX_F32_DENSE_OVERLAP");
+    m->dense_overlap = dov && dov[0] == '1';
     try {   // a failure part-way releases what was built
       m->device = device;
       QLX_HIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
@@ -930,6 +936,7 @@ int32_t qlx_model_create(int32_t arch, uint64_t seed, int32_t device, qlx_model*
       QLX_HIP(hipMemset(m->d_v, 0, pb));
       QLX_HIP(hipMemset(m->d_grads, 0, pb));
       model_pack(m);
+      model_dense_join(m, m->stream);
       QLX_HIP(hipStreamSynchronize(m->stream));
     } catch (...) {
       qlx_model_destroy(m);
@@ -944,6 +951,12 @@ int32_t qlx_model_destroy(qlx_model* m) {
     if (!m) return;
     (void)hipSetDevice(m->device);
     (void)hipStreamSynchronize(m->stream);
+    if (m->f32_aux) {
+      (void)hipStreamSynchronize(m->f32_aux);
+      (void)hipStreamDestroy(m->f32_aux);
+      (void)hipEventDestroy(m->ev_dense_ready);
+      (void)hipEventDestroy(m->ev_dense_done);
+    }
     void* ptrs[] = {m->d_params, m->d_m, m->d_v, m->d_grads, m->wf0, m->wf1, m->wb1, m->wf2, m->wb2, m->wb3,
                     m->d_rbeg, m->d_rend, m->d_partial, m->d_var_first, m->d_norms, m->d_sqf, m->d_sqf_first, m->ws, m->d_fc1bwd_map,
                     m->w.fgrad};
@@ -957,6 +970,7 @@ int32_t qlx_model_get_var(qlx_model* m, int32_t var, int32_t which, float* out) 
   return guard([&] {
     QLX_CHECK(m && out && var >= 0 && var < kNumVars && which >= 0 && which <= 2, QLX_E_INVALID, "bad argument");
     QLX_HIP(hipSetDevice(m->device));
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
     const float* src = (which == 0 ? m->d_params : which == 1 ? m->d_m : m->d_v) + var_offset(var);
     QLX_HIP(hipMemcpy(out, src, kVarSize[var] * sizeof(float), hipMemcpyDeviceToHost));
@@ -967,10 +981,12 @@ int32_t qlx_model_set_var(qlx_model* m, int32_t var, int32_t which, const float*
   return guard([&] {
     QLX_CHECK(m && in && var >= 0 && var < kNumVars && which >= 0 && which <= 2, QLX_E_INVALID, "bad argument");
     QLX_HIP(hipSetDevice(m->device));
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
     float* dst = (which == 0 ? m->d_params : which == 1 ? m->d_m : m->d_v) + var_offset(var);
     QLX_HIP(hipMemcpy(dst, in, kVarSize[var] * sizeof(float), hipMemcpyHostToDevice));
-    if (which == 0) { model_pack(m); QLX_HIP(hipStreamSynchronize(m->stream)); }
+    if (which == 0) { model_pack(m); model_dense_join(m, m->stream);
+    QLX_HIP(hipStreamSynchronize(m->stream)); }
   });
 }
 
@@ -998,6 +1014,7 @@ int32_t qlx_model_predict(qlx_model* m, const uint8_t* obs, uint32_t n, float* q
     launch_fc2(1, a, (int)n, m->stream);
     if (q_out) QLX_HIP(hipMemcpyAsync(q_out, m->w.q, n * 3 * sizeof(float), hipMemcpyDeviceToHost, m->stream));
     if (actions) QLX_HIP(hipMemcpyAsync(actions, m->w.argmax, n, hipMemcpyDeviceToHost, m->stream));
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
   });
 }
@@ -1015,6 +1032,7 @@ int32_t qlx_model_batch_max_q(qlx_model* m, const uint8_t* obs, uint32_t n, floa
     a.rewards = m->w.rew; a.dones = m->w.done; a.gamma = 1.0f; a.y_out = m->w.y;
     launch_fc2(2, a, (int)n, m->stream);
     QLX_HIP(hipMemcpyAsync(out, m->w.y, n * sizeof(float), hipMemcpyDeviceToHost, m->stream));
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
   });
 }
@@ -1034,6 +1052,7 @@ int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions
     if (grads_out) QLX_HIP(hipMemcpyAsync(grads_out, m->d_grads, kNumParams * 4, hipMemcpyDeviceToHost, s));
     model_norms(m, s, 1.0f);
     model_adam(m, s, 1.0f);
+    model_dense_join(m, s);   // the dense norms / weights of an update on the aux stream
     if (norms_out) QLX_HIP(hipMemcpyAsync(norms_out, m->d_norms, kNumVars * 4, hipMemcpyDeviceToHost, s));
     if (loss_out) QLX_HIP(hipMemcpyAsync(loss_out, m->w.loss, 4, hipMemcpyDeviceToHost, s));
     QLX_HIP(hipStreamSynchronize(s));
@@ -1046,7 +1065,8 @@ int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
     QLX_HIP(hipSetDevice(m->device));
     if (m->f32) {   // a1..a3 of the last forward chunk (the whole batch up to kF32FwdChunk samples), a4 of all
       QLX_CHECK(layer == 4 || m->last_batch <= m->w.fchunk, QLX_E_STATE, "activations of a chunked forward");
-      QLX_HIP(hipStreamSynchronize(m->stream));
+      model_dense_join(m, m->stream);
+    QLX_HIP(hipStreamSynchronize(m->stream));
       const size_t per[5] = {0, 12800, 5184, 3136, 512};
       const float* src = layer == 1 ? m->w.fa1 : layer == 2 ? m->w.fa2 : layer == 3 ? m->w.fa3 : m->w.fa4;
       QLX_HIP(hipMemcpy(out, src, per[layer] * (size_t)m->last_batch * 4, hipMemcpyDeviceToHost));
@@ -1059,6 +1079,7 @@ int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
       QLX_HIP(hipGetLastError());
       m->w.a4_splits = 0;
     }
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
     const size_t per[5] = {0, 12800, 5184, 3136, 512};
     const bf16* src = layer == 1 ? m->w.a1 : layer == 2 ? m->w.a2 : layer == 3 ? m->w.a3 : m->w.a4;
@@ -1078,6 +1099,7 @@ int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
 int32_t qlx_model_write_checkpoint(qlx_model* m, const char* path) {
   return guard([&] {
     QLX_CHECK(m && path, QLX_E_INVALID, "bad argument");
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
     std::vector<float> buf(kNumParams * 3);
     QLX_HIP(hipMemcpy(buf.data(), m->d_params, kNumParams * 4, hipMemcpyDeviceToHost));
@@ -1101,12 +1123,14 @@ int32_t qlx_model_load_tf(qlx_model* m, const char* prefix) {
     int64_t it = 0;
     load_keras_bundle(prefix, 5, kVarSize, w, mm, vv, &it);
     QLX_HIP(hipSetDevice(m->device));
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
     QLX_HIP(hipMemcpy(m->d_params, w.data(), kNumParams * 4, hipMemcpyHostToDevice));
     QLX_HIP(hipMemcpy(m->d_m, mm.data(), kNumParams * 4, hipMemcpyHostToDevice));
     QLX_HIP(hipMemcpy(m->d_v, vv.data(), kNumParams * 4, hipMemcpyHostToDevice));
     m->iterations = it;
     model_pack(m);
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
   });
 }
@@ -1124,12 +1148,14 @@ int32_t qlx_model_read_checkpoint(qlx_model* m, const char* path) {
     std::fclose(f);
     QLX_CHECK(ok, QLX_E_IO, "not a qlx checkpoint");
     QLX_HIP(hipSetDevice(m->device));
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
     QLX_HIP(hipMemcpy(m->d_params, buf.data(), kNumParams * 4, hipMemcpyHostToDevice));
     QLX_HIP(hipMemcpy(m->d_m, buf.data() + kNumParams, kNumParams * 4, hipMemcpyHostToDevice));
     QLX_HIP(hipMemcpy(m->d_v, buf.data() + 2 * kNumParams, kNumParams * 4, hipMemcpyHostToDevice));
     m->iterations = hdr[1];
     model_pack(m);
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
   });
 }
@@ -1137,6 +1163,7 @@ int32_t qlx_model_read_checkpoint(qlx_model* m, const char* path) {
 int32_t qlx_model_sync(qlx_model* m) {
   return guard([&] {
     QLX_CHECK(m, QLX_E_INVALID, "null model");
+    model_dense_join(m, m->stream);
     QLX_HIP(hipStreamSynchronize(m->stream));
   });
 }
