@@ -985,8 +985,10 @@ int32_t qlx_model_set_var(qlx_model* m, int32_t var, int32_t which, const float*
     QLX_HIP(hipStreamSynchronize(m->stream));
     float* dst = (which == 0 ? m->d_params : which == 1 ? m->d_m : m->d_v) + var_offset(var);
     QLX_HIP(hipMemcpy(dst, in, kVarSize[var] * sizeof(float), hipMemcpyHostToDevice));
-    if (which == 0) { model_pack(m); model_dense_join(m, m->stream);
-    QLX_HIP(hipStreamSynchronize(m->stream)); }
+    if (which == 0) {
+      model_pack(m);
+      QLX_HIP(hipStreamSynchronize(m->stream));
+    }
   });
 }
 
@@ -996,6 +998,8 @@ int32_t qlx_model_copy_weights(qlx_model* dst, const qlx_model* src) {
   return guard([&] {
     QLX_CHECK(dst && src, QLX_E_INVALID, "null model");
     QLX_HIP(hipSetDevice(dst->device));
+    model_dense_join(const_cast<qlx_model*>(src), src->stream);   // src's weights complete, dst's not still being written
+    model_dense_join(dst, dst->stream);
     QLX_HIP(hipStreamSynchronize(src->stream));
     QLX_HIP(hipMemcpyAsync(dst->d_params, src->d_params, kNumParams * sizeof(float), hipMemcpyDeviceToDevice, dst->stream));
     model_pack(dst);
@@ -1066,7 +1070,7 @@ int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
     if (m->f32) {   // a1..a3 of the last forward chunk (the whole batch up to kF32FwdChunk samples), a4 of all
       QLX_CHECK(layer == 4 || m->last_batch <= m->w.fchunk, QLX_E_STATE, "activations of a chunked forward");
       model_dense_join(m, m->stream);
-    QLX_HIP(hipStreamSynchronize(m->stream));
+      QLX_HIP(hipStreamSynchronize(m->stream));
       const size_t per[5] = {0, 12800, 5184, 3136, 512};
       const float* src = layer == 1 ? m->w.fa1 : layer == 2 ? m->w.fa2 : layer == 3 ? m->w.fa3 : m->w.fa4;
       QLX_HIP(hipMemcpy(out, src, per[layer] * (size_t)m->last_batch * 4, hipMemcpyDeviceToHost));
