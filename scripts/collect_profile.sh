@@ -8,6 +8,7 @@ name=$1
 src=gpurun_out/$name
 dst=profiles/$name
 mkdir -p "$dst"
+find "$src" -name '*.csv.gz' -exec gunzip -f {} +
 cp "$src/bench.json" "$src/bench.err" "$src/gputest.log" "$src/smoke.log" "$dst/"
 cp "$(ls $src/stats/*kernel_stats.csv | head -1)" "$dst/kernel_stats.csv"
 cp "$(ls $src/stats_bf16/*kernel_stats.csv | head -1)" "$dst/kernel_stats_bf16.csv"

@@ -30,5 +30,7 @@ rm -rf "$OUT/pmc_bf16" && mv gpurun_out/pmc "$OUT/pmc_bf16"
 python3 scripts/pmc_traffic.py "$OUT/pmc_bf16" bf16 > "$OUT/pmc_traffic_bf16.log" 2>&1
 timeout -k 10 200 ./scripts/ubench_bgemm > "$OUT/ubench_bgemm.txt" 2>&1 || exit 1
 timeout -k 10 200 python3 -c "import bench, json; print(json.dumps(bench.cpu_baseline(10000)))" > "$OUT/cpu_full.json" 2>&1 || exit 1
+# the per-dispatch counter tables exceed what gpurun copies back (64 MiB): compressed here, gunzip before collect_profile.sh
+find "$OUT" -name '*.csv' -size +512k -exec gzip -f {} +
 fi
 exit 0
