@@ -35,8 +35,9 @@ SCOPES = {
         "f32_adam": "k_update32",   # update schedule 2 (default): every variable's clip_by_norm + Adam in one launch
     },
     "bf16": {
-        "trunk_fwd": "k_trunk_fwd<true>",
-        "trunk_fwd_nostore": "k_trunk_fwd<false>",
+        # rocprofv3 leaves these names mangled: k_trunk_fwd<store = true, ...> (training batches) / <false, ...>
+        "trunk_fwd": "k_trunk_fwdILb1E",
+        "trunk_fwd_nostore": "k_trunk_fwdILb0E",
         "trunk_bwd_data": "k_trunk_bwd_data",
         "conv1_wgrad": "k_conv1_wgrad",
         "conv23_wgrad": "k_conv23_wgrad",
