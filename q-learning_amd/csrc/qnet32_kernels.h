@@ -2192,6 +2192,10 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 // step.  Per sample the frames (row layout) and dz1's channel half sit in LDS (54,016 B) while the next sample's are in
 // flight in registers.
 constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
+#ifndef QLX_C1W_AHEAD
+#define QLX_C1W_AHEAD 1   // samples whose frames + dz1 are in flight in registers (1 or 2)
+#endif
+static_assert(QLX_C1W_AHEAD == 1 || QLX_C1W_AHEAD == 2, "conv1 weight gradient: 1 or 2 samples ahead");
 constexpr int kC1WgradThreads = 256;
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
                                                                        float* slab, int skip) {
@@ -2205,8 +2209,9 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
   const int nb = min(QLX_F32_WGRAD_CHUNK_CONV1, B - b0);
   // this lane's A row rho = l15: kh = 2 w + rho / 8, h = (rho / 4) % 2, c = rho % 4; dword of (x = 4 oh + kh, y / 4 = ow + h)
   const int ao = (l15 & 3) * kC1SlotDw + (2 * wave + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
-  uint4 pf[14];
-  auto prefetch = [&](int b) {
+  // (QLX_C1W_AHEAD = 2: two register sets, the samples two ahead in flight; the chunk loop is unrolled so each set is static)
+  uint4 pf[QLX_C1W_AHEAD][14];
+  auto prefetch = [&](int b, uint4 (&pf)[14]) {
     const C1Ptrs f = c1_ptrs(table, b);
     const uint64_t zp = (uint64_t)(gbyte*)q32_zero4;
     const uint64_t dzb = (uint64_t)(dz1 + (size_t)b * 400 * 32 + hh * 16);
@@ -2223,7 +2228,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
       pf[j] = uint4{v.x, v.y, v.z, v.w};
     }
   };
-  auto stage = [&]() {
+  auto stage = [&](const uint4 (&pf)[14]) {
 #pragma unroll
     for (int j = 0; j < 14; ++j) {
       const int q = tid + 256 * j;
@@ -2235,12 +2240,15 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = zero4();
   float bsum = 0.0f;   // lane (oc, q): chain Cq of its B-operand values
-  prefetch(b0);
-  for (int bl = 0; bl < nb; ++bl) {
+  prefetch(b0, pf[0]);
+  if (QLX_C1W_AHEAD > 1 && nb > 1) prefetch(b0 + 1, pf[QLX_C1W_AHEAD - 1]);
+#pragma unroll
+  for (int bl = 0; bl < QLX_F32_WGRAD_CHUNK_CONV1; ++bl) {
+    if (bl >= nb) break;
     __syncthreads();   // the previous sample's LDS reads are done
-    stage();
+    stage(pf[bl % QLX_C1W_AHEAD]);
     __syncthreads();
-    if (bl + 1 < nb) prefetch(b0 + bl + 1);
+    if (bl + QLX_C1W_AHEAD < nb) prefetch(b0 + bl + QLX_C1W_AHEAD, pf[bl % QLX_C1W_AHEAD]);
 #pragma unroll 10   // (2 / 4 / 10 / 20 / 25 / 50: 74.0 / 74.5 / 68.5 / 69.2 / 69.5 / 69.3 us at B = 1024, max-ILP scheduling;
                     // with the zero-step skip, round 4: 5 / 10 / 20 / 25: 44.0 / 43.0 / 49.0 / 49.3 us, gpurun_out/w29)
     for (int rs = 0; rs < 100; ++rs) {

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Parity + A/B of one build variant (development tool): the fp32 GPU tests against abvar/$1/libqlx.so, then bench.py
+# with the main build and with the variant (one JSON line each in gpurun_out/ab/).  Every GPU step has its own time
+# limit; the first failure ends the script.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+v=$1
+mkdir -p gpurun_out/ab
+QLX_LIB_PATH=abvar/$v/libqlx.so timeout -k 10 400 python -u -m pytest tests/test_gpu_qnet32.py tests/test_gpu_qnet32_paths.py \
+  -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/$v.test.log 2>&1 || exit 1
+export AB_ARGS="--steps 10 --beside-steps 0 --nomemo-steps 0 --dense-steps 0 --refwork-steps 0 --dp1-steps 0 --sparsity-steps 0"
+bash scripts/ab_bench.sh "base:" "$v:QLX_LIB_PATH=abvar/$v/libqlx.so" "base2:" "${v}_2:QLX_LIB_PATH=abvar/$v/libqlx.so"
