@@ -2196,6 +2196,9 @@ constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 h
 #define QLX_C1W_AHEAD 1   // samples whose frames + dz1 are in flight in registers (1 or 2)
 #endif
 static_assert(QLX_C1W_AHEAD == 1 || QLX_C1W_AHEAD == 2, "conv1 weight gradient: 1 or 2 samples ahead");
+#ifndef QLX_C1W_PIPE
+#define QLX_C1W_PIPE 5   // steps per software-pipelined operand group (0: the per-step loop)
+#endif
 constexpr int kC1WgradThreads = 256;
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
                                                                        float* slab, int skip) {
@@ -2249,6 +2252,44 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
     stage(pf[bl % QLX_C1W_AHEAD]);
     __syncthreads();
     if (bl + QLX_C1W_AHEAD < nb) prefetch(b0 + bl + QLX_C1W_AHEAD, pf[bl % QLX_C1W_AHEAD]);
+#if QLX_C1W_PIPE
+    // Operand groups of GS steps, software-pipelined: the next group's LDS reads are issued before this group's ballots and
+    // MFMAs, and a group's ballots are all taken before its first branch, so no branch merge waits for a read in flight.  (In
+    // the per-step form the compiler waits lgkmcnt(0) at every step's branch merge - one LDS round trip per step, 100 per
+    // sample.)  Same MFMAs on the same operands in the same order: bit-identical slabs.
+    constexpr int GS = QLX_C1W_PIPE, NG = 100 / GS;
+    static_assert(NG % 2 == 0 && NG * GS == 100 && 2 * GS <= 15, "conv1 weight gradient: operand groups");
+    float bA[GS], bB[GS];
+    uint32_t xA[GS], xB[GS];
+    auto rd = [&](int grp, float (&bv)[GS], uint32_t (&px)[GS]) {
+#pragma unroll
+      for (int j = 0; j < GS; ++j) {
+        const int r = 4 * (grp * GS + j) + g, oh = r / 20, ow = r - oh * 20;
+        bv[j] = dzs[r * 16 + l15];
+        px[j] = c1w[ao + 84 * oh + ow];
+      }
+    };
+    auto run = [&](const float (&bv)[GS], const uint32_t (&px)[GS]) {
+      bool nz[GS];
+#pragma unroll
+      for (int j = 0; j < GS; ++j) nz[j] = !skip || __builtin_amdgcn_ballot_w64(px[j] != 0u) != 0;   // wave-uniform
+#pragma unroll
+      for (int j = 0; j < GS; ++j) {
+        // all 64 x 4 frame values 0: the step adds +-0 (see the forward)
+        if (nz[j])
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px[j], t), bv[j], acc[t], 0, 0, 0);
+        bsum = __fadd_rn(bsum, bv[j]);   // (every wave; wave 0's is stored)
+      }
+    };
+    rd(0, bA, xA);
+    for (int grp = 0; grp < NG; grp += 2) {
+      rd(grp + 1, bB, xB);
+      run(bA, xA);
+      if (grp + 2 < NG) rd(grp + 2, bA, xA);
+      run(bB, xB);
+    }
+#else
 #pragma unroll 10   // (2 / 4 / 10 / 20 / 25 / 50: 74.0 / 74.5 / 68.5 / 69.2 / 69.5 / 69.3 us at B = 1024, max-ILP scheduling;
                     // with the zero-step skip, round 4: 5 / 10 / 20 / 25: 44.0 / 43.0 / 49.0 / 49.3 us, gpurun_out/w29)
     for (int rs = 0; rs < 100; ++rs) {
@@ -2262,6 +2303,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
         for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px, t), bv, acc[t], 0, 0, 0);
       if (wave == 0) bsum = __fadd_rn(bsum, bv);
     }
+#endif
   }
   float* out = slab + (size_t)z * 257 * 32;
   const int oc = hh * 16 + l15;
