@@ -1906,6 +1906,9 @@ struct SideFc2 {
 // LDS frame layout (rows): slot c, image row x, dword y / 4 holds pixels (x, y .. y + 3) at dword c * 1776 + x * 21 + y / 4.
 // Rows of 21 dwords make 16 consecutive output positions (oh, ow) hit 16 consecutive banks (84 = 20 mod 64 dwords per
 // oh step), and the slot stride 1,776 = 48 mod 64 puts the four slots (the MFMA lane groups) on disjoint bank ranges.
+#ifndef QLX_C1F_NZFIRST
+#define QLX_C1F_NZFIRST 1   // conv1 forward: a tile's zero-step masks before the next tile's operand reads (0: interleaved)
+#endif
 constexpr int kC1SlotDw = 1776;                 // 84 rows x 21 dwords + 12 (bank skew)
 constexpr int kC1Frames = 4 * kC1SlotDw * 4;    // 28,416 B of one sample's frames in LDS
 constexpr int kC1Chunks = 4 * kFramePix / 16;   // 1,764 s2d uint4 chunks in HBM
@@ -2162,6 +2165,20 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
         uint32_t d[16];
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq) d[kq] = dn[kq];
+#if QLX_C1F_NZFIRST
+        // the tile's 16 step masks are taken before the next tile's LDS reads are issued, so no branch merge of the MFMA
+        // chain waits for those reads (the compiler otherwise puts lgkmcnt(0) at the merges)
+        bool nz[16];
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) nz[kq] = !skip || __builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0;   // wave-uniform
+        if (j + 1 < nt) tile_dwords(j + 1, dn);
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq)
+          if (nz[kq])
+#pragma unroll
+            for (int kw = 0; kw < 4; ++kw) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[kq], kw), wf[kq * 4 + kw], acc, 0, 0, 0);
+#else
         if (j + 1 < nt) tile_dwords(j + 1, dn);
         f32x4 acc = zero4();
 #pragma unroll
@@ -2169,6 +2186,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
           if (!skip || __builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0)   // wave-uniform
 #pragma unroll
             for (int kw = 0; kw < 4; ++kw) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[kq], kw), wf[kq * 4 + kw], acc, 0, 0, 0);
+#endif
         const int t = rp + 2 * j, r0 = (4 * (t / 5) + g) * 20 + 4 * (t % 5);   // rows (oh, ow .. ow + 3) of the patch
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[i] + bias);
@@ -2258,7 +2276,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
     // the per-step form the compiler waits lgkmcnt(0) at every step's branch merge - one LDS round trip per step, 100 per
     // sample.)  Same MFMAs on the same operands in the same order: bit-identical slabs.
     constexpr int GS = QLX_C1W_PIPE, NG = 100 / GS;
-    static_assert(NG % 2 == 0 && NG * GS == 100 && 2 * GS <= 15, "conv1 weight gradient: operand groups");
+    static_assert(NG % 2 == 0 && NG * GS == 100, "conv1 weight gradient: operand groups");
     float bA[GS], bB[GS];
     uint32_t xA[GS], xB[GS];
     auto rd = [&](int grp, float (&bv)[GS], uint32_t (&px)[GS]) {
