@@ -2170,7 +2170,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
         // chain waits for those reads (the compiler otherwise puts lgkmcnt(0) at the merges)
         bool nz[16];
 #pragma unroll
-        for (int kq = 0; kq < 16; ++kq) nz[kq] = !skip || __builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0;   // wave-uniform
+        for (int kq = 0; kq < 16; ++kq) nz[kq] = (__builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0) | (skip == 0);   // wave-uniform, no branch
         if (j + 1 < nt) tile_dwords(j + 1, dn);
         f32x4 acc = zero4();
 #pragma unroll
@@ -2290,7 +2290,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
     auto run = [&](const float (&bv)[GS], const uint32_t (&px)[GS]) {
       bool nz[GS];
 #pragma unroll
-      for (int j = 0; j < GS; ++j) nz[j] = !skip || __builtin_amdgcn_ballot_w64(px[j] != 0u) != 0;   // wave-uniform
+      for (int j = 0; j < GS; ++j) nz[j] = (__builtin_amdgcn_ballot_w64(px[j] != 0u) != 0) | (skip == 0);   // wave-uniform, no branch
 #pragma unroll
       for (int j = 0; j < GS; ++j) {
         // all 64 x 4 frame values 0: the step adds +-0 (see the forward)
