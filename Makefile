@@ -42,9 +42,12 @@ $(OUT)/obj/qnet.o: $(SRC)/qnet.hip $(HDRS) | $(OUT)/obj
 # Q-net objects: the backend's max-ILP scheduling strategy (measured at C3: fp32 195.5K -> 196.2K env-steps/s, every GEMM
 # layer equal or faster; max-memory-clause 191.0K, iterative-ilp 196.6K; bf16 745.7K -> 749.3K)
 Q32SCHED := -mllvm --amdgpu-sched-strategy=max-ilp
+# fp32 Q-net: MFMA accumulators in VGPRs (the AGPR form rotated the pair GEMMs' accumulators through v_accvgpr moves every
+# slab - VALU time the fp32 MFMAs cannot overlap; measured: conv2 / conv3 pairs 96.4 / 72.1 -> 95.9 / 71.2 us)
+Q32VFORM := -mllvm -amdgpu-mfma-vgpr-form=1
 
 $(OUT)/obj/qnet32.o: $(SRC)/qnet32.hip $(HDRS) | $(OUT)/obj
-	$(HIPCC) $(HIPFLAGS) $(STRICT) $(Q32SCHED) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(STRICT) $(Q32SCHED) $(Q32VFORM) -c $< -o $@
 
 $(OUT)/obj/learner.o: $(SRC)/learner.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) $(STRICT) -c $< -o $@
