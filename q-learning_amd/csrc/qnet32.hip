@@ -754,8 +754,9 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
         using P2 = decltype(t2);
         using P3 = decltype(t3);
         // (the list tiles start at row tile 1; row tile 0, the constant row, is ConstRows' work: its blocks return)
-        launch_list(m, P2{lgrid(cap2, P2::BM, P2::BN), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, nullptr}, cr,
-                    sc2, 2.0 * n * 81 * 64 * 512, s);
+        P2 p2{lgrid(cap2, P2::BM, P2::BN), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, nullptr};
+        p2.pre_batched = big;
+        launch_list(m, p2, cr, sc2, 2.0 * n * 81 * 64 * 512, s);
         launch_list(m, P3{lgrid(cap3, P3::BM, P3::BN), w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride, c2, nullptr},
                     s23, sc3, 2.0 * n * 49 * 64 * 576, s);
       };

@@ -1014,17 +1014,36 @@ struct PConvFwdL {
   const unsigned long long* cnt;   // this layer's counter of region 0 (region x at x * 2 * kCntStride)
   const float* cx;   // constant input row [C]
   float* cbuf;       // constant output row [OC]
+  // the epilogue rows' entries batched per call (entries()) or row by row, per launch: measured at C3, batched: conv3
+  // 28.0 -> 27.5 us, the 8,192-sample conv2 / conv3 passes 137 / 180 -> 128 / 171 us, but the B = 1024 conv2 23.9 -> 25.6 us
+  // (that launch sets it false)
+  bool pre_batched = true;
   struct ACtx { int off[NA]; uint32_t m[NA]; };   // input offset (-1: no row), taps read from cx
-  struct Pre { float b; int o[4]; };
+  struct Pre { float b; int o[4]; };   // o: the rows' raw list entries
+
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return KS * KS * C / BK; }
   __device__ int count(int x) const { return (int)(cnt[x * 2 * kCntStride] >> 32); }
   // list entry of a GEMM row: >= 0 a row (SEL: with its constant-tap mask << 20), -1 none, -2 the constant row
-  __device__ int entry(int row) const {
-    const int tm = row / BM;
-    if (tm == 0) return row == 0 ? -2 : -1;
-    const int x = (tm - 1) % kListSlots, lr = ((tm - 1) / kListSlots) * BM + row % BM;
-    return lr < count(x) ? list[x * cap + lr] : -1;
+  // List entries of N rows of one row tile (the callers' rows all lie in one tile, so the tile index is read as
+  // wave-uniform): one scalar branch for the constant-row tile, the region counter as a scalar load, and the N entry loads -
+  // unconditional, at clamped addresses - all in flight at once.  (Row by row with a per-lane tile index the compiler put
+  // each row's loads behind an exec-masked branch and a vmcnt(0): one memory round trip per row in the tile prologue.)
+  template <int N>
+  __device__ void entries(const int (&row)[N], int (&out)[N]) const {
+    const int tm = __builtin_amdgcn_readfirstlane(row[0] / BM);
+    if (tm == 0) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) out[i] = row[i] == 0 ? -2 : -1;
+      return;
+    }
+    const int x = (tm - 1) % kListSlots, base = ((tm - 1) / kListSlots) * BM;
+    const int n = count(x);
+    int v[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = list[x * cap + min(base + row[i] % BM, cap - 1)];
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = base + row[i] % BM < n ? v[i] : -1;
   }
   __device__ bool active(int, int row0) const {   // (row tile 0 only where the constant row has somewhere to go)
     const int tm = row0 / BM;
@@ -1032,11 +1051,17 @@ struct PConvFwdL {
   }
   __device__ ACtx a_ctx(int, int row0, int tid) const {
     ACtx c;
+    int rows[NA], raws[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int r, k;
       OA::coord(tid + i * T, r, k);
-      const int raw = entry(row0 + r), e = raw >= 0 ? raw & 0xFFFFF : raw;
+      rows[i] = row0 + r;
+    }
+    entries(rows, raws);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int raw = raws[i], e = raw >= 0 ? raw & 0xFFFFF : raw;
       const int b = e / R, p = e - b * R, oh = p / OW, ow = p - oh * OW;
       c.off[i] = e >= 0 ? ((b * H + oh * S) * W + ow * S) * C : -1;
       c.m[i] = e == -2 ? 0xFFFFFFFFu : (SEL && raw >= 0 ? (uint32_t)raw >> 20 : 0u);
@@ -1054,17 +1079,24 @@ struct PConvFwdL {
   __device__ Pre epi_pre(int, int row, int col) const {
     Pre q;
     q.b = bias[col];
+    if (!pre_batched) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int raw = entry(row + r);
-      q.o[r] = raw >= 0 ? (raw & 0xFFFFF) * OC : raw;
+      const int tm = (row + r) / BM;
+      if (tm == 0) { q.o[r] = row + r == 0 ? -2 : -1; continue; }
+      const int x = (tm - 1) % kListSlots, lr = ((tm - 1) / kListSlots) * BM + (row + r) % BM;
+      q.o[r] = lr < count(x) ? list[x * cap + lr] : -1;
+    }
+    } else {
+    const int rows[4] = {row, row + 1, row + 2, row + 3};
+    entries(rows, q.o);   // raw entries: decoded in the epilogue, so nothing waits for these loads before the slab loop
     }
     return q;
   }
   __device__ void epi_post(int, int, int col, f32x4 v, const Pre& q) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if (q.o[r] >= 0) out[(size_t)q.o[r] + col] = relu(v[r] + q.b);
+      if (q.o[r] >= 0) out[(size_t)(q.o[r] & 0xFFFFF) * OC + col] = relu(v[r] + q.b);
       else if (q.o[r] == -2) cbuf[col] = relu(v[r] + q.b);
     }
   }
@@ -1119,11 +1151,19 @@ struct PConvFwdL {
     const char* base = SEL && (const char*)cx < lo ? (const char*)cx : lo;
     const uint32_t in_off = (uint32_t)(lo - base), cx_off = SEL ? (uint32_t)((const char*)cx - base) : 0u;
     st.ra = buf_rsrc(base, 0x7FFFFFF0u);   // (row offsets are bounded by the list entries: b * R + p of this chunk)
+    int rows[NA], raws[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int r = 0, k = 0;
       OA::coord(tid + i * T, r, k);
-      const int raw = entry(row0 + r), e = raw >= 0 ? raw & 0xFFFFF : -1;
+      rows[i] = row0 + r;
+    }
+    entries(rows, raws);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      int r = 0, k = 0;
+      OA::coord(tid + i * T, r, k);
+      const int raw = raws[i], e = raw >= 0 ? raw & 0xFFFFF : -1;
       const int bb = e / R, pp = e - bb * R, oh = pp / OW, ow = pp - oh * OW;
       st.vo[i] = e >= 0 ? in_off + (uint32_t)(((bb * H + oh * S) * W + ow * S) * C + k) * 4u : kOob;
       st.cxo[i] = cx_off + (uint32_t)k * 4u;
