@@ -57,6 +57,25 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
   const int j = lane & 15, g = lane >> 4, n = lane & 15;
   const int b = s0 + j;
   const bool valid = j < HS && b < A.B;
+  // the per-sample operands of the head's tail, loaded with the stage (one memory round instead of a second one after the
+  // MFMA chain): MODE 3 action, target and IS weight; MODE 2 reward, done and the double-DQN selector's q
+  const bool tail = wave == 0 && g == 0 && valid;
+  const int bt = tail ? b : 0;
+  int t_act = 0;
+  float t_y = 0.0f, t_w = 1.0f, t_r = 0.0f, t_qs[3] = {0.0f, 0.0f, 0.0f};
+  bool t_done = false;
+  if (tail) {
+    if (MODE == 3) {
+      t_act = A.actions[bt];
+      t_y = A.y[bt];
+      if (A.weights) t_w = A.weights[bt];
+    } else if (MODE == 2) {
+      t_r = A.rewards[bt];
+      t_done = A.dones[bt] != 0;
+      if (A.q_select)
+        for (int r = 0; r < 3; ++r) t_qs[r] = A.q_select[bt * 3 + r];
+    }
+  }
   {   // stage: 16 rows x 128 float4 of a4 (8 per thread; rows past B read row s0) and W4's 384 float4
     f32x4 xr[8], wr[2];
 #pragma unroll
@@ -111,24 +130,23 @@ __global__ __launch_bounds__(256) void k_head32(Fc2Args A) {
     } else if (MODE == 2) {
       float mx;
       if (A.q_select) {
-        const float* qs = A.q_select + b * 3;
         int best = 0;
-        float bv = qs[0];
-        if (qs[1] > bv) { best = 1; bv = qs[1]; }
-        if (qs[2] > bv) best = 2;
+        float bv = t_qs[0];
+        if (t_qs[1] > bv) { best = 1; bv = t_qs[1]; }
+        if (t_qs[2] > bv) best = 2;
         mx = best == 0 ? q0 : (best == 1 ? q1 : q2);
       } else {
         mx = fmaxf(fmaxf(q0, q1), q2);
       }
-      const float r = A.rewards[b];
+      const float r = t_r;
       // add_arrays(reward, array_mul(max_future, gamma)) (self_driving_tf_q_learner.rs:189-199,298-315): two roundings
-      A.y_out[b] = A.dones[b] ? r : __fadd_rn(r, __fmul_rn(mx, A.gamma));
+      A.y_out[b] = t_done ? r : __fadd_rn(r, __fmul_rn(mx, A.gamma));
     } else if (MODE == 3) {
-      const int a = A.actions[b];
+      const int a = t_act;
       const float qa = a == 0 ? q0 : (a == 1 ? q1 : q2);
-      const float e = __fsub_rn(qa, A.y[b]);
+      const float e = __fsub_rn(qa, t_y);
       const float ae = fabsf(e);
-      const float wgt = A.weights ? A.weights[b] : 1.0f;   // prioritized replay: the IS weight scales h and dloss/dq
+      const float wgt = t_w;   // prioritized replay: the IS weight scales h and dloss/dq
       const float ge = ae <= 1.0f ? e : (e > 0.0f ? 1.0f : -1.0f);
       const float gb = __fmul_rn(wgt, ge) / (float)A.B;
       A.gsample[b] = gb;
@@ -318,26 +336,33 @@ __device__ __forceinline__ int var_of(const Adam32Args& A, int64_t i) {
 
 // norm_v for v = V0 .. 9 into nrm[v] (wave 0; lane chain over the partials lane, lane + 64, ... of v - zeros past the
 // end - then the xor butterfly).  Every partial is loaded at once (13 per lane for W3, one per lane for each smaller
-// variable: one memory round).  write: also store them to A.norms.
-template <int V0>
-__device__ __forceinline__ void norms_prologue(const Adam32Args& A, int lane, float* nrm, bool write) {
+// variable: one memory round), through buffer descriptors spanning each variable's partials (past the end reads 0, no
+// per-lane branch - the branchy form put a vmcnt(0) after several of these loads).  write: also store them to A.norms.
+struct NormPart {
   float x[kNormSegMax / 64], y[kNumVars];
+};
+template <int V0>
+__device__ __forceinline__ void norms_load(const Adam32Args& A, int lane, NormPart& P) {
   const int f6 = A.seg_first[6], c6 = A.seg_first[7] - f6;
+  const __amdgpu_buffer_rsrc_t r6 = buf_rsrc(A.partial + f6, (uint32_t)c6 * 4u);
 #pragma unroll
-  for (int i = 0; i < kNormSegMax / 64; ++i) x[i] = lane + 64 * i < c6 ? A.partial[f6 + lane + 64 * i] : 0.0f;
+  for (int i = 0; i < kNormSegMax / 64; ++i) P.x[i] = buf_ld1(r6, (uint32_t)(lane + 64 * i) * 4u, 0);
 #pragma unroll
   for (int vv = V0; vv < kNumVars; ++vv) {
     const int f = A.seg_first[vv], c = A.seg_first[vv + 1] - f;
-    y[vv] = vv != 6 && lane < c ? A.partial[f + lane] : 0.0f;   // every variable but W3 has <= 64 partials
+    P.y[vv] = vv != 6 ? buf_ld1(buf_rsrc(A.partial + f, (uint32_t)c * 4u), (uint32_t)lane * 4u, 0) : 0.0f;   // <= 64 partials
   }
+}
+template <int V0>
+__device__ __forceinline__ void norms_sum(const Adam32Args& A, int lane, const NormPart& P, float* nrm, bool write) {
 #pragma unroll
   for (int vv = V0; vv < kNumVars; ++vv) {
     float t = 0.0f;
     if (vv == 6) {
 #pragma unroll
-      for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, x[i]);
+      for (int i = 0; i < kNormSegMax / 64; ++i) t = __fadd_rn(t, P.x[i]);
     } else {
-      t = __fadd_rn(t, y[vv]);
+      t = __fadd_rn(t, P.y[vv]);
     }
     for (int o = 32; o > 0; o >>= 1) t = __fadd_rn(t, __shfl_xor(t, o));
     if (lane == 0) {
@@ -357,14 +382,14 @@ struct AdamDense {
   __device__ void run(int t, float* lds) const {
     float* nrm = lds;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (wave == 0) norms_prologue<6>(A, lane, nrm, t == 0);
-    __syncthreads();
     const int64_t o6 = A.off[6], count = A.off[kNumVars], n4 = (count - o6) / 4;   // o6 is a multiple of 4
     const int64_t st = (int64_t)nblocks * blockDim.x, q0 = (int64_t)t * blockDim.x + threadIdx.x;
-    if (2 * st > n4) {   // at most two float4 groups per thread (k_update32's grid): all eight loads in one round
-      // (measured: 16.3 -> 14.8 us per update against one group per thread on twice the blocks)
-      const int64_t qq[2] = {q0, q0 + st};
-      f32x4 g[2], w[2], m[2], v[2];
+    const bool two = 2 * st > n4;   // (wave-uniform)
+    const int64_t qq[2] = {q0, q0 + st};
+    f32x4 g[2], w[2], m[2], v[2];
+    NormPart P;
+    if (wave == 0) norms_load<6>(A, lane, P);   // the norm partials first, then the element loads: one memory round for both
+    if (two) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int64_t i0 = o6 + (qq[u] < n4 ? qq[u] : 0) * 4;
@@ -373,6 +398,11 @@ struct AdamDense {
         m[u] = ld4(A.m + i0);
         v[u] = ld4(A.v + i0);
       }
+    }
+    if (wave == 0) norms_sum<6>(A, lane, P, nrm, t == 0);
+    lds_barrier();   // (LDS only: the element loads stay in flight)
+    if (two) {   // at most two float4 groups per thread (k_update32's grid): all eight loads in one round
+      // (measured: 16.3 -> 14.8 us per update against one group per thread on twice the blocks)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (qq[u] >= n4) continue;

@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-timeout -k 10 400 python -u -m pytest tests/test_gpu_qnet32.py tests/test_gpu_qnet32_paths.py -x -q --timeout 120 \
+timeout -k 10 500 python -u -m pytest tests/test_gpu_qnet32.py tests/test_gpu_qnet32_paths.py ${AB_TESTS:-} -x -q --timeout 120 \
   --timeout-method thread > gpurun_out/ab/main.test.log 2>&1 || exit 1
 export AB_ARGS="--steps 10 --beside-steps 0 --nomemo-steps 0 --dense-steps 0 --refwork-steps 0 --dp1-steps 0 --sparsity-steps 0"
 specs=("main:")
