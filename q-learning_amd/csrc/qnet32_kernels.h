@@ -1946,9 +1946,6 @@ struct SideFc2 {
 // LDS frame layout (rows): slot c, image row x, dword y / 4 holds pixels (x, y .. y + 3) at dword c * 1776 + x * 21 + y / 4.
 // Rows of 21 dwords make 16 consecutive output positions (oh, ow) hit 16 consecutive banks (84 = 20 mod 64 dwords per
 // oh step), and the slot stride 1,776 = 48 mod 64 puts the four slots (the MFMA lane groups) on disjoint bank ranges.
-#ifndef QLX_C1F_NZFIRST
-#define QLX_C1F_NZFIRST 1   // conv1 forward: a tile's zero-step masks before the next tile's operand reads (0: interleaved)
-#endif
 constexpr int kC1SlotDw = 1776;                 // 84 rows x 21 dwords + 12 (bank skew)
 constexpr int kC1Frames = 4 * kC1SlotDw * 4;    // 28,416 B of one sample's frames in LDS
 constexpr int kC1Chunks = 4 * kFramePix / 16;   // 1,764 s2d uint4 chunks in HBM
@@ -2205,9 +2202,9 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
         uint32_t d[16];
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq) d[kq] = dn[kq];
-#if QLX_C1F_NZFIRST
         // the tile's 16 step masks are taken before the next tile's LDS reads are issued, so no branch merge of the MFMA
-        // chain waits for those reads (the compiler otherwise puts lgkmcnt(0) at the merges)
+        // chain waits for those reads (masks interleaved with the chain: the compiler put lgkmcnt(0) at the merges, 48.2 vs
+        // 46.7 us at B = 1024; with the short-circuit form of the mask, a branch per mask: 46.7 vs 42.7 us)
         bool nz[16];
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq) nz[kq] = (__builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0) | (skip == 0);   // wave-uniform, no branch
@@ -2218,15 +2215,6 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
           if (nz[kq])
 #pragma unroll
             for (int kw = 0; kw < 4; ++kw) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[kq], kw), wf[kq * 4 + kw], acc, 0, 0, 0);
-#else
-        if (j + 1 < nt) tile_dwords(j + 1, dn);
-        f32x4 acc = zero4();
-#pragma unroll
-        for (int kq = 0; kq < 16; ++kq)
-          if (!skip || __builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0)   // wave-uniform
-#pragma unroll
-            for (int kw = 0; kw < 4; ++kw) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[kq], kw), wf[kq * 4 + kw], acc, 0, 0, 0);
-#endif
         const int t = rp + 2 * j, r0 = (4 * (t / 5) + g) * 20 + 4 * (t % 5);   // rows (oh, ow .. ow + 3) of the patch
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[i] + bias);
@@ -2250,13 +2238,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 // step.  Per sample the frames (row layout) and dz1's channel half sit in LDS (54,016 B) while the next sample's are in
 // flight in registers.
 constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
-#ifndef QLX_C1W_AHEAD
-#define QLX_C1W_AHEAD 1   // samples whose frames + dz1 are in flight in registers (1 or 2)
-#endif
-static_assert(QLX_C1W_AHEAD == 1 || QLX_C1W_AHEAD == 2, "conv1 weight gradient: 1 or 2 samples ahead");
-#ifndef QLX_C1W_PIPE
-#define QLX_C1W_PIPE 5   // steps per software-pipelined operand group (0: the per-step loop)
-#endif
+
 constexpr int kC1WgradThreads = 256;
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
                                                                        float* slab, int skip) {
@@ -2270,8 +2252,9 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
   const int nb = min(QLX_F32_WGRAD_CHUNK_CONV1, B - b0);
   // this lane's A row rho = l15: kh = 2 w + rho / 8, h = (rho / 4) % 2, c = rho % 4; dword of (x = 4 oh + kh, y / 4 = ow + h)
   const int ao = (l15 & 3) * kC1SlotDw + (2 * wave + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
-  // (QLX_C1W_AHEAD = 2: two register sets, the samples two ahead in flight; the chunk loop is unrolled so each set is static)
-  uint4 pf[QLX_C1W_AHEAD][14];
+  // (the next sample's frames + dz1 in flight in registers; two samples ahead in two register sets measured slower: 43.3 ->
+  // 45.2 us)
+  uint4 pf[14];
   auto prefetch = [&](int b, uint4 (&pf)[14]) {
     const C1Ptrs f = c1_ptrs(table, b);
     const uint64_t zp = (uint64_t)(gbyte*)q32_zero4;
@@ -2301,21 +2284,20 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = zero4();
   float bsum = 0.0f;   // lane (oc, q): chain Cq of its B-operand values
-  prefetch(b0, pf[0]);
-  if (QLX_C1W_AHEAD > 1 && nb > 1) prefetch(b0 + 1, pf[QLX_C1W_AHEAD - 1]);
+  prefetch(b0, pf);
 #pragma unroll
   for (int bl = 0; bl < QLX_F32_WGRAD_CHUNK_CONV1; ++bl) {
     if (bl >= nb) break;
     __syncthreads();   // the previous sample's LDS reads are done
-    stage(pf[bl % QLX_C1W_AHEAD]);
+    stage(pf);
     __syncthreads();
-    if (bl + QLX_C1W_AHEAD < nb) prefetch(b0 + bl + QLX_C1W_AHEAD, pf[bl % QLX_C1W_AHEAD]);
-#if QLX_C1W_PIPE
+    if (bl + 1 < nb) prefetch(b0 + bl + 1, pf);
     // Operand groups of GS steps, software-pipelined: the next group's LDS reads are issued before this group's ballots and
     // MFMAs, and a group's ballots are all taken before its first branch, so no branch merge waits for a read in flight.  (In
     // the per-step form the compiler waits lgkmcnt(0) at every step's branch merge - one LDS round trip per step, 100 per
-    // sample.)  Same MFMAs on the same operands in the same order: bit-identical slabs.
-    constexpr int GS = QLX_C1W_PIPE, NG = 100 / GS;
+    // sample: 43.3 -> 39.2 us at B = 1024; groups of 2 / 10 / 25 / 50 steps: 51.5 / 40.1 / 68.5 / 123 us; branch-free
+    // masks: 36.4 us.)  Same MFMAs on the same operands in the same order: bit-identical slabs.
+    constexpr int GS = 5, NG = 100 / GS;
     static_assert(NG % 2 == 0 && NG * GS == 100, "conv1 weight gradient: operand groups");
     float bA[GS], bB[GS];
     uint32_t xA[GS], xB[GS];
@@ -2347,21 +2329,6 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
       if (grp + 2 < NG) rd(grp + 2, bA, xA);
       run(bB, xB);
     }
-#else
-#pragma unroll 10   // (2 / 4 / 10 / 20 / 25 / 50: 74.0 / 74.5 / 68.5 / 69.2 / 69.5 / 69.3 us at B = 1024, max-ILP scheduling;
-                    // with the zero-step skip, round 4: 5 / 10 / 20 / 25: 44.0 / 43.0 / 49.0 / 49.3 us, gpurun_out/w29)
-    for (int rs = 0; rs < 100; ++rs) {
-      const int r = 4 * rs + g, oh = r / 20, ow = r - oh * 20;
-      const float bv = dzs[r * 16 + l15];
-      const uint32_t px = c1w[ao + 84 * oh + ow];
-      // all 64 x 4 frame values 0: the step adds +-0 (see the forward).  (Reading a group of 10 steps' operands ahead of
-      // the previous group's branches: 42.7 -> 50.6 us.)
-      if (!skip || __builtin_amdgcn_ballot_w64(px != 0u) != 0)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px, t), bv, acc[t], 0, 0, 0);
-      if (wave == 0) bsum = __fadd_rn(bsum, bv);
-    }
-#endif
   }
   float* out = slab + (size_t)z * 257 * 32;
   const int oc = hh * 16 + l15;
