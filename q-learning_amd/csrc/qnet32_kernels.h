@@ -99,6 +99,15 @@ static const float q32_zero4[4] __attribute__((aligned(16))) = {0.0f, 0.0f, 0.0f
 static __attribute__((device)) float q32_zero4[4] __attribute__((aligned(16))) = {0.0f, 0.0f, 0.0f, 0.0f};
 #endif
 __device__ __forceinline__ f32x4 ld4m(const float* p, bool ok) { return ld4(ok ? p : q32_zero4); }
+// a value the caller knows to be equal on every lane, as a wave-uniform (scalar) value; the identity in the host replay of
+// the policies (scripts/q32_host_check.hip, QLX_Q32_POLICIES_ONLY)
+__device__ __forceinline__ int q32_uniform(int x) {
+#ifdef QLX_Q32_POLICIES_ONLY
+  return x;
+#else
+  return __builtin_amdgcn_readfirstlane(x);
+#endif
+}
 __device__ __forceinline__ f32x4 u8x4(uint32_t w) {
   return f32x4{(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu), (float)((w >> 16) & 0xFFu), (float)(w >> 24)};
 }
@@ -1031,7 +1040,7 @@ struct PConvFwdL {
   // each row's loads behind an exec-masked branch and a vmcnt(0): one memory round trip per row in the tile prologue.)
   template <int N>
   __device__ void entries(const int (&row)[N], int (&out)[N]) const {
-    const int tm = __builtin_amdgcn_readfirstlane(row[0] / BM);
+    const int tm = q32_uniform(row[0] / BM);
     if (tm == 0) {
 #pragma unroll
       for (int i = 0; i < N; ++i) out[i] = row[i] == 0 ? -2 : -1;
