@@ -310,7 +310,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     load(s + 2 < ns ? s + 2 : ns - 1, ya, yb);
     if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);   // the loads stay ahead of the slab's MFMAs
     compute(s);
-    if (s + 1 < ns) store(s + 1, xa, xb);
+    store(s + 1, xa, xb);   // unconditional, as in gemm_body_s (past the last slab: the idle buffer, never read)
     lds_barrier();
   };
   constexpr bool PRE = HasEpiPre<P>::value && MF == 16 && G == 1;
@@ -327,10 +327,12 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     store(0, ra1, rb1);
     load(ns > 1 ? 1 : 0, ra0, rb0);
     lds_barrier();
-    for (int s = 0; s < ns; s += 2) {
+    int s = 0;
+    for (; s + 1 < ns; s += 2) {
       iter(s, ra0, rb0, ra1, rb1);
-      if (s + 1 < ns) iter(s + 1, ra1, rb1, ra0, rb0);
+      iter(s + 1, ra1, rb1, ra0, rb0);
     }
+    if (s < ns) iter(s, ra0, rb0, ra1, rb1);
   }
   if constexpr (G > 1) {   // groups 1 .. G - 1 hand their accumulators to group 0 through their own LDS (free now)
     constexpr int E = MF * MF / 64;
@@ -830,11 +832,15 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
           for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     };
+    // (the store of slab s + 1 is unconditional: past the last slab it writes the idle buffer with the reloaded last slab,
+    // which nothing reads.  Skipped there, its registers' loads stayed pending on that path, and the compiler - which does
+    // not see that the path leaves the loop - waited for them at the top of every other slab step: the two register sets
+    // degenerated to one.)
     auto iter = [&](int s, Regs& xs, Regs& ys) {
       st.load(s + 2 < ns ? s + 2 : ns - 1, ys);
       if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);
       compute(s);
-      if (s + 1 < ns) st.store((s + 1) & 1 ? As1 : As0, (s + 1) & 1 ? Bs1 : Bs0, xs);
+      st.store((s + 1) & 1 ? As1 : As0, (s + 1) & 1 ? Bs1 : Bs0, xs);
       lds_barrier();
     };
     if (ns > 0) {
@@ -842,10 +848,14 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
       st.store(As0, Bs0, x1);
       st.load(ns > 1 ? 1 : 0, x0);
       lds_barrier();
-      for (int s = 0; s < ns; s += 2) {
+      // (the odd last step after the loop: a conditional second step inside it was, to the compiler, a path back to the
+      // loop head with a register set still loading - see iter)
+      int s = 0;
+      for (; s + 1 < ns; s += 2) {
         iter(s, x0, x1);
-        if (s + 1 < ns) iter(s + 1, x1, x0);
+        iter(s + 1, x1, x0);
       }
+      if (s < ns) iter(s, x0, x1);
     }
   };
   constexpr bool PRE = HasEpiPre<P>::value;
