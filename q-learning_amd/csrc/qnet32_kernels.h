@@ -142,7 +142,8 @@ struct IglpOf<P, std::void_t<decltype(P::IGLP)>> : std::integral_constant<int, P
 // loads); measured per layer with iglp_opt in place: the fc1 forward 39.8 -> 38.3 us, the chunk-size conv2 forward 404 ->
 // 389 us, the conv3 backward pair 98.8 -> 97.7 us without it; every other layer 2-5 % slower without it.  Re-measured on
 // the stream core (round 4, gpurun_out/w17: every policy with / without it, iglp 0 / none for all): off for the conv2 pair's
-// two policies too; strategy 1 stays the best default.
+// two policies too; strategy 1 stays the best default (re-measured after the round-5 slab-loop fix: strategy 0 / none for all
+// 278K / 281K env-steps/s against 288K).
 template <class P, class = void>
 struct LoadFenceOf : std::true_type {};
 template <class P>
@@ -1019,7 +1020,8 @@ template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 
 struct PConvFwdL {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false, RAW_ORDER = true;
-  static constexpr bool LOAD_FENCE = !(H == 20 && BN_ == 64);
+  // (with the slab loop's wait fixed, round 5: the fence on for conv2 too - the 8,192-sample pass 131 -> 127 us)
+  static constexpr bool LOAD_FENCE = true;
   static constexpr int R = OH * OW;
   using OA = Opnd<BM, false, 16>;
   static constexpr int T = WM * WN * 64, NA = (OA::F4 + T - 1) / T;
