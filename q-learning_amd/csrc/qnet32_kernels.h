@@ -1260,8 +1260,10 @@ struct BgRows2 {   // two background-row jobs (a2 and a3) in one launch's leadin
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1FwdT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
-  static constexpr bool LOAD_FENCE = false;
-  static constexpr int IGLP = 0;   // strategy 0 (default scheduler 40.4 / 236 us, strategy 1 42.2 / 248 us, 0 39.8 / 230 us at B = 1024 / 8,192)
+  static constexpr bool LOAD_FENCE = false;   // (round 5: with it 35.3 / 209.8 us against 33.8 / 203.4)
+  // strategy 0 at the training batch (default scheduler 40.4, strategy 1 42.2, 0 39.8 us at B = 1024; round 5: 1 39.3 against
+  // 33.8), strategy 1 for the chunk-batch tiles (round 5: 196.7 against 203.4 us)
+  static constexpr int IGLP = BM_ == 64 ? 1 : 0;
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
   const float* a3;
@@ -1310,7 +1312,7 @@ using PFc1Fwd = PFc1FwdT<>;
 // v_mfma_f32_32x32x2_f32, 212 / 215 us for 64 x 64 / 128 x 64; gpurun_out/w12)
 using PFc1FwdB = PFc1FwdT<64, 128, 2, 2, 16>;
 // (re-checked on the stream core in place: 32 x 64 / 64 x 32 / 16 x 64 ran 35.3 / 35.9 / 40.4 us against 34.1 us, w9)
-using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;
+using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;   // (round 5, after the slab-loop fix: 64 x 32 / 32 x 64 38.4 / 38.9 us against 33.8)
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
