@@ -186,6 +186,7 @@ int main(int argc, char** argv) {
   replay(PConv2DgradS{grid(B * 100, 64, 32, 32, 4), dz2, w1, a1, dz1, B * 100}, "conv2_dgrad S");
   replay(PConv2DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px");
   replay(PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px 64");
+  replay(PConv2DgradPx<64, 128, 2, 2>{Grid{(B + 63) / 64, 1, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px 64 x 128");
   check_groups<PConv2DgradPxG<>>(100, 4, "conv2 groups");
   replay(PConv2DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 2, 81}, dz2, w1, a1, dz1, B}}, "conv2_dgrad pxg");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
