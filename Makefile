@@ -35,8 +35,10 @@ $(OUT)/obj/env_breakout.o: $(SRC)/env_breakout.hip $(HDRS) | $(OUT)/obj
 $(OUT)/obj/replay.o: $(SRC)/replay.hip $(HDRS) | $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# (bf16 Q-net on the default scheduler since round 5: 789K -> 797K env-steps/s against max-ILP, the slab reduction
+# 11.4 -> 10.0 us)
 $(OUT)/obj/qnet.o: $(SRC)/qnet.hip $(HDRS) | $(OUT)/obj
-	$(HIPCC) $(HIPFLAGS) $(Q32SCHED) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # fp32 Q-net: bit-exact against the oracle, so no contraction anywhere (every fma is an explicit fmaf / MFMA)
 # Q-net objects: the backend's max-ILP scheduling strategy (measured at C3: fp32 195.5K -> 196.2K env-steps/s, every GEMM

@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 mkdir -p abvar/$name
-HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-result -I include -I q-learning_amd/csrc -munsafe-fp-atomics -ffp-contract=off ${VARIANT_SCHED--mllvm --amdgpu-sched-strategy=max-ilp} -mllvm -amdgpu-mfma-vgpr-form=1"
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-result -I include -I q-learning_amd/csrc -munsafe-fp-atomics -ffp-contract=off ${VARIANT_SCHED--mllvm --amdgpu-sched-strategy=max-ilp} ${VARIANT_VFORM--mllvm -amdgpu-mfma-vgpr-form=1}"
 src=${VARIANT_SRC:-qnet32}
 /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c q-learning_amd/csrc/$src.hip -o abvar/$name/$src.o
 objs=$(ls q-learning_amd/lib/obj/*.o | grep -v "/$src.o")
