@@ -180,15 +180,6 @@ __device__ __forceinline__ bf16 relu_bf16(float v) { return (bf16)(v > 0.0f ? v 
 // pre(t) runs at the start of tile t, before the tile's refill reads are issued, and its result is handed to
 // epi(t, acc, pre_value): an LDS value the epilogue needs (e.g. a ReLU mask) is then older than the ring
 // reads in flight, so waiting for it is lgkmcnt(D) instead of a drain of the whole ring.
-#ifndef QLX_TD1
-#define QLX_TD1 4
-#endif
-#ifndef QLX_TD2
-#define QLX_TD2 4
-#endif
-#ifndef QLX_TD3
-#define QLX_TD3 3
-#endif
 template <int KS, int D, class Addr, class Pre, class Epi>
 __device__ __forceinline__ void conv_tiles(int t0, int dt, int nt, const bf16x8 (&w)[KS], Addr addr, Pre pre, Epi epi) {
   static_assert(KS % D == 0, "ring depth must divide the k-steps");
@@ -289,7 +280,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
     frames_prefetch_slots(sptr, b + (int)gridDim.x < B, pf);
     if (threadIdx.x < 4 && b + 2 * (int)gridDim.x < B) pnext = table[(b + 2 * gridDim.x) * 4 + threadIdx.x];
     // conv1: M = 400 (25 tiles of 16), N = 32, K = 256: k-step s covers tap (i, j) = (s >> 2, (s >> 1) & 1)
-    conv_tiles<8, QLX_TD1>(
+    conv_tiles<8, 4>(
         wave >> 1, 4, 25, w1,
         [&](int t, int s) {
           const int m = t * 16 + r, ox = m / 20, oy = m - ox * 20;
@@ -304,7 +295,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
     mark(1);
     if (STORE12) lds_copy_out_pitched<400, 32, kA1S, 20, kA1W>(A1, a1 + (size_t)b * 12800);
     // conv2: 4x4 stride 2 over A1 [20][20][32]; M = 81 (6 tiles), k-step s = tap (kh, kw) = (s >> 2, s & 3)
-    conv_tiles<16, QLX_TD2>(
+    conv_tiles<16, 4>(
         wave >> 2, 2, 6, w2,
         [&](int t, int s) {
           const int m = min(t * 16 + r, 80), p = m / 9, q = m - p * 9;
@@ -319,7 +310,7 @@ __global__ __launch_bounds__(kTrunkThreads, 1) void k_trunk_fwd(const uint8_t* c
     mark(2);
     if (STORE12) lds_copy_out_pitched<81, 64, kA2S, 9, kA2W>(A2, a2 + (size_t)b * 5184);
     // conv3: 3x3 stride 1 over A2 [9][9][64]; M = 49 (4 tiles), k-step s: tap s >> 1, channel half s & 1
-    conv_tiles<18, QLX_TD3>(
+    conv_tiles<18, 3>(
         wave >> 2, 2, 4, w3,
         [&](int t, int s) {
           const int m = min(t * 16 + r, 48), p = m / 7, q = m - p * 7;
