@@ -24,7 +24,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;   // reduction depth staged per LDS slab
 // background-row lists (C1Lists): regions per list (one per XCD) and the counter stride (128 bytes)
-constexpr int kListSlots = 8;
+#ifndef QLX_LIST_SLOTS
+#define QLX_LIST_SLOTS 8   // (A/B builds only: scripts/build_variant.sh -DQLX_LIST_SLOTS=n)
+#endif
+constexpr int kListSlots = QLX_LIST_SLOTS;
 constexpr int kCntStride = 16;   // [region][layer] at (region * 2 + layer) * kCntStride
 
 // Operand tile in LDS for MFMA shape MF (16: v_mfma_f32_16x16x4_f32, 32: v_mfma_f32_32x32x2_f32).  RMAJ: t[row][k]
@@ -1117,6 +1120,9 @@ struct PConvFwdL {
   __device__ void epi_post(int, int, int col, f32x4 v, const Pre& q) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+#ifdef QLX_LIST_CHECK
+      if (q.o[r] >= 0 && (q.o[r] & 0xFFFFF) >= kListSlots * cap) printf("LISTCHK epi o %d cap %d\n", q.o[r], cap);
+#endif
       if (q.o[r] >= 0) out[(size_t)(q.o[r] & 0xFFFFF) * OC + col] = relu(v[r] + q.b);
       else if (q.o[r] == -2) cbuf[col] = relu(v[r] + q.b);
     }
@@ -1234,6 +1240,10 @@ struct BgRows {
     const f32x4 v = ld4(c_in + 4 * q);
     for (int x = 0; x < kListSlots; ++x) {
       const int nbg = (int)(uint32_t)cnt[x * 2 * kCntStride];
+#ifdef QLX_LIST_CHECK
+      if (tid == 0 && blk == 0 && (nbg > cap || (int)(cnt[x * 2 * kCntStride] >> 32) + nbg > cap))
+        printf("LISTCHK bgrows region %d nbg %d non %d cap %d\n", x, nbg, (int)(cnt[x * 2 * kCntStride] >> 32), cap);
+#endif
       const int* back = list + (size_t)(x + 1) * cap - 1;
       for (int i0 = blk * 16 * U + (tid >> 4); i0 < nbg; i0 += nblk * 16 * U) {
         int e[U];
@@ -1241,7 +1251,12 @@ struct BgRows {
         for (int u = 0; u < U; ++u) e[u] = i0 + 16 * u < nbg ? back[-(i0 + 16 * u)] : -1;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (e[u] >= 0) *reinterpret_cast<f32x4*>(out + (size_t)e[u] * 64 + 4 * q) = v;
+          if (e[u] >= 0) {
+#ifdef QLX_LIST_CHECK
+            if (e[u] >= kListSlots * cap && q == 0) printf("LISTCHK bgrows e %d cap %d region %d i %d\n", e[u], cap, x, i0 + 16 * u);
+#endif
+            *reinterpret_cast<f32x4*>(out + (size_t)e[u] * 64 + 4 * q) = v;
+          }
       }
     }
   }
@@ -2138,6 +2153,13 @@ __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int
         tap |= (int)(((q < 64 ? g0 >> q : g1 >> (q - 64)) & 1ull) << t);
       }
     }
+#ifdef QLX_LIST_CHECK
+    {
+      const int i1 = on + __builtin_popcountll(bn & below), i2 = cap - 1 - (og + __builtin_popcountll(bb & below));
+      if ((((bn >> lane) & 1ull) && (i1 < 0 || i1 >= cap)) || (((bb >> lane) & 1ull) && (i2 < 0 || i2 >= cap)) || e >= B * R)
+        printf("LISTCHK flush blk %d wave %d it %d e %d B %d i1 %d i2 %d cap %d\n", (int)blockIdx.x, wave, it, e, B, i1, i2, cap);
+    }
+#endif
     if ((bn >> lane) & 1ull) rl[on + __builtin_popcountll(bn & below)] = e | (tap << 20);
     else if ((bb >> lane) & 1ull) rl[cap - 1 - (og + __builtin_popcountll(bb & below))] = e;
     on += __builtin_popcountll(bn);
