@@ -166,6 +166,9 @@ def test_frame_sparsity():
         L.prefill(40)
         L.run(3)
         f = L.frame_sparsity()
+        # (called again at once on the same frames: the read-back of the second of two back-to-back calls once came
+        # back as zeros - the diagnostic's stream-ordered allocation, DESIGN.md round-5 notes)
+        assert L.frame_sparsity() == f
         last = L.last()
         idx = last["indices"].ravel()
         assert idx.size == last["losses"].shape[0] * 64 > 0
