@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--dp1-steps", type=int, default=5,
                     help="one GPU: timed vector steps of the data-parallel update path on a single-rank RCCL communicator "
                          "(bucketed all-reduce + the DP update tail; the cost C4 pays per rank besides the link; 0 = skip)")
+    ap.add_argument("--c5-steps", type=int, default=5,
+                    help="one GPU: timed vector steps of C5's per-GPU shard (double DQN + prioritized replay, fp32, the "
+                         "same envs / replay / batch) beside the headline; 0 = skip")
     ap.add_argument("--sparsity-steps", type=int, default=8,
                     help="fp32: untimed vector steps after the timed window, each reporting the fractions of conv work "
                          "the skips left out (qlx_learner_frame_sparsity)")
@@ -406,9 +409,17 @@ class Run:
         for k in GEMM_SCOPES[self.precision]:
             if k in c and c[k]["total_us_per_step"] > 0:
                 t = rate(c[k]["work"], c[k]["total_us_per_step"], 1e6)
-                if k in ZERO_STEP_SCOPES:   # not an MFMA utilisation: part of the dense work is not issued
-                    layers[k] = {"tflops_dense_equivalent": round(t, 2), "mfma_frac": None, "avg_us": round(c[k]["avg_us"], 2),
-                                 "note": ZERO_STEP_SCOPES[k]}
+                if k in ZERO_STEP_SCOPES:
+                    # part of the dense work is not issued: the MFMA utilisation is the issued work, dense FLOP x (1 - the
+                    # scope's measured skipped fraction), over the time; the dense-equivalent rate stays beside it
+                    note, (half, key) = ZERO_STEP_SCOPES[k]
+                    skip = self.skipped(half, key)
+                    issued = None if skip is None else t * (1.0 - skip)
+                    layers[k] = {"tflops_issued": None if issued is None else round(issued, 2),
+                                 "mfma_frac": None if issued is None else round(issued / peak, 4),
+                                 "skipped_fraction": None if skip is None else round(skip, 4),
+                                 "skipped_fraction_source": f"skipped_fractions.{half}.{key}.mean",
+                                 "tflops_dense_equivalent": round(t, 2), "avg_us": round(c[k]["avg_us"], 2), "note": note}
                 else:
                     layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
         upd = self.updates / max(self.steps, 1) / max(self.ctl.world, 1)   # updates per vector step on one GPU
@@ -439,14 +450,31 @@ class Run:
     def value(self):
         return self.env_steps / self.dt
 
+    def skipped(self, half, key):
+        """mean skipped fraction of one skip predicate over the sparsity pass (None without one)"""
+        s = self.sparsity
+        if not s or not s.get(half):
+            return None
+        return s[half][key]["mean"]
 
-# launches that do not issue part of their layer's dense work (exact): their rates are dense FLOP / time
-_C1_NOTE = "dense FLOP / time; MFMA steps whose frame operands are all 0 are not issued (exact, DESIGN.md 4.1)"
-_BG_NOTE = ("dense FLOP / time; the background rows (receptive field all-zero frame pixels) are one constant row, computed "
-            "once and written, the GEMM runs the other rows (exact, DESIGN.md 4.1)")
-ZERO_STEP_SCOPES = {"f32_conv1_fwd": _C1_NOTE, "f32_conv1_fwd_big": _C1_NOTE, "f32_conv1_wgrad": _C1_NOTE,
-                    "f32_conv2_fwd": _BG_NOTE, "f32_conv2_fwd_big": _BG_NOTE, "f32_conv3_fwd": _BG_NOTE,
-                    "f32_conv3_fwd_big": _BG_NOTE}
+
+# launches that do not issue part of their layer's dense work (exact, DESIGN.md 4.1), each with the skipped fraction that
+# applies to it: the training-batch launches take the sampled states' fraction, the chunk launches (the acting forward and
+# the target memo over the new transitions' s' - the same frames one vector step apart) the acting frames'
+_C1_NOTE = ("MFMA steps whose frame operands are all 0 are not issued (exact, DESIGN.md 4.1): mfma_frac = dense FLOP x (1 - "
+            "skipped_fraction) / time / peak; tflops_dense_equivalent = dense FLOP / time")
+_BG_NOTE = ("the background rows (receptive field all-zero frame pixels) are one constant row, computed once and written, "
+            "the GEMM runs the other rows (exact, DESIGN.md 4.1): mfma_frac = dense FLOP x (1 - skipped_fraction) / time / "
+            "peak; tflops_dense_equivalent = dense FLOP / time")
+ZERO_STEP_SCOPES = {
+    "f32_conv1_fwd": (_C1_NOTE, ("train_batches", "conv1_fwd_zero_steps")),
+    "f32_conv1_fwd_big": (_C1_NOTE, ("acting", "conv1_fwd_zero_steps")),
+    "f32_conv1_wgrad": (_C1_NOTE, ("train_batches", "conv1_wgrad_zero_steps")),
+    "f32_conv2_fwd": (_BG_NOTE, ("train_batches", "conv2_background_rows")),
+    "f32_conv2_fwd_big": (_BG_NOTE, ("acting", "conv2_background_rows")),
+    "f32_conv3_fwd": (_BG_NOTE, ("train_batches", "conv3_background_rows")),
+    "f32_conv3_fwd_big": (_BG_NOTE, ("acting", "conv3_background_rows")),
+}
 
 
 def pmc_traffic(precision, scope):
@@ -525,8 +553,13 @@ def main():
     dp1 = None
     if ctl.world == 1 and args.dp1_steps > 0:
         dp1 = Run(args, ctl, args.precision, args.dp1_steps, 1, flags, dp1=True)
+    c5 = None
+    if ctl.world == 1 and args.c5_steps > 0 and flags == 0:
+        # C5's per-GPU shard: the same workload with double-DQN targets and proportional prioritized replay (fp32)
+        c5 = Run(args, ctl, "fp32", args.c5_steps, 1, qlx.DOUBLE_DQN | qlx.PER)
     other = "bf16" if args.precision == "fp32" else "fp32"
-    beside = Run(args, ctl, other, args.beside_steps, 1, flags) if args.beside_steps > 0 else None
+    beside = Run(args, ctl, other, args.beside_steps, 1, flags, args.sparsity_steps if other == "fp32" else 0) \
+        if args.beside_steps > 0 else None
     # the measured window is the steady-state loop: greedy acting and episode ends inside it
     assert "act_forward" in head.comps, "acting forward missing from the measured loop"
     assert head.episodes > 0, "no episode ended inside the timed window"
@@ -619,6 +652,22 @@ def main():
                     "backward, its clip-norm partials after it there, conv bucket all-reduced on the learner stream, the "
                     "k_update32 tail - whose per-rank cost C4 pays besides the xGMI transfer; bit-identical to the plain "
                     "path at world 1 (tests/test_gpu_learner.py)"}
+    if c5 is not None:
+        upd = c5.updates / max(c5.steps, 1)
+        per_scopes = ("sample", "per_tree_build", "per_draw", "gather", "priorities", "per_push")
+        line["value_c5_shard"] = round(c5.value(), 1)
+        line["c5_shard"] = {
+            "value": round(c5.value(), 1), "unit": "env-steps/s", "steps": c5.steps,
+            "ms_per_step": round(c5.dt / c5.steps * 1e3, 3), "grad_updates_per_sec": round(c5.updates / c5.dt, 2),
+            "episodes_in_window": c5.episodes, "config": config_label(N, args.replay, 3, 1),
+            "per_update_us_event_timed": {
+                n: round(c5.comps[n]["total_us_per_step"] / max(upd, 1e-9), 2) for n in per_scopes if n in c5.comps},
+            "note": "C5's one-GPU shard (SURVEY 8(d)): the headline's envs, replay and batch with double-DQN targets (online "
+                    "argmax over s', target-net value; the target net evaluated per sampled batch, so no memo) and "
+                    "proportional prioritized replay (HBM f32 sum tree: per_tree_build = bottom-up rebuild, per_draw = "
+                    "stratified draws + IS weights, priorities = |td| write-back, per_push = new leaves at max priority), "
+                    "fp32, bit-exact vs the oracle (tests/test_gpu_per.py::test_f32_c5_shard); per-update figures = the "
+                    "profile pass's per-step device time / updates per step"}
     if head.sparsity is not None:
         line["skipped_fractions"] = head.sparsity
     if beside is not None:

@@ -21,7 +21,7 @@
 //   images, s64(kr) = 2 (((kr >> 1) & 1) | ((kr >> 3) & 1) << 1) for 64-row ones.  The DMA writes each wave
 //   instruction's 1 KB linearly, so the permutation is applied on the SOURCE address (each lane fetches the chunk that
 //   belongs at its linear LDS slot; the permutation stays inside one row / k-row, so coalescing is unchanged) and the
-//   same XOR on the read (cdna_hip_programming.md §5.4 rule 21).  scripts/bgemm_banks.py checks both layouts;
+//   same XOR on the read (cdna_hip_programming.md §5.4 rule 21).  scripts/lds_banks.py checks both layouts;
 // - the MFMA computes C^T (B fragment as the A operand), so each lane ends with 4 consecutive n of one m: the epilogues
 //   of gemm_kernels.h (Epi4*) move 16 bytes (fp32) or 8 bytes (bf16) per access.
 // Requirements (host-checked): row-major operands have K % 32 == 0; every split's k range is a multiple of 32 but the last.

@@ -135,6 +135,8 @@ struct Epi4ReluMask {   // dz[m][n] = v * (act[m][n] > 0) as bf16 (act rows act_
   const bf16* act;
   int ldo;
   int act_ld;
+  // every field named: a form without act_ld (the old three-field aggregate) does not compile
+  __host__ __device__ Epi4ReluMask(bf16* out_, const bf16* act_, int ldo_, int act_ld_) : out(out_), act(act_), ldo(ldo_), act_ld(act_ld_) {}
   __device__ __forceinline__ void operator()(int m, int n, f32x4 v, int) const {
     const size_t i = (size_t)m * ldo + n;
     typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));

@@ -266,6 +266,9 @@ struct qlx_learner {
   // pinned host copies read after every vector step (the solved() check): Book + the global sums
   qlx::Book* h_book = nullptr;
   double* h_gsum = nullptr;
+  // frame_sparsity's counters: a device buffer and its pinned host copy (8 x u64: the train and the acting halves)
+  unsigned long long* d_sparsity = nullptr;
+  unsigned long long* h_sparsity = nullptr;
   // Bellman-target memo per replay slot (ycache_fill): on when the target net is frozen (target_sync_steps == 0,
   // the reference) and y does not depend on the online net (no double DQN); QLX_TARGET_CACHE=0 turns it off
   bool ycache = false;
@@ -479,7 +482,10 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
   {
     ProfScope ps(&L->prof, "replay_push", s, 2.0 * 7056.0 * N + 10.0 * N);   // frame read + write + metadata
     replay_launch_push(L->rb, L->env, s, L->d_actions, L->d_rewards, L->d_dones);
-    if (L->per) per_launch_push(s, L->prio.leaves(), L->rb->cap, L->rb->total - N, N, L->prio.d_max);
+    if (L->per) {
+      ProfScope pp(&L->prof, "per_push", s);
+      per_launch_push(s, L->prio.leaves(), L->rb->cap, L->rb->total - N, N, L->prio.d_max);
+    }
   }
   debug_sync(s, "replay_push");
   if (L->ycache) {   // y of the N new transitions (all live slots after a write of the target weights)
@@ -512,7 +518,11 @@ static void learner_vector_step(qlx_learner* L, bool train = true) {
     {
       ProfScope ps(&L->prof, "sample", s);
       if (L->per) {
-        per_launch_build(s, L->prio.d_tree, L->prio.L);
+        {
+          ProfScope pb(&L->prof, "per_tree_build", s);
+          per_launch_build(s, L->prio.d_tree, L->prio.L);
+        }
+        ProfScope pd(&L->prof, "per_draw", s);
         per_launch_sample(s, L->prio.d_tree, L->prio.L, L->p.learner_seed, (uint32_t)L->update_count, U, (uint32_t)L->rank,
                           L->rb->len(), L->p.per_beta, L->B, cap, start, L->d_idx, L->prio.d_w);
       } else {
@@ -643,6 +653,8 @@ int32_t qlx_learner_create(const qlx_params* p, int32_t device, qlx_learner** ou
       QLX_HIP(hipMalloc(&L->d_book, sizeof(Book)));
       QLX_HIP(hipHostMalloc((void**)&L->h_book, sizeof(Book), hipHostMallocDefault));
       QLX_HIP(hipHostMalloc((void**)&L->h_gsum, 3 * sizeof(double), hipHostMallocDefault));
+      QLX_HIP(hipMalloc(&L->d_sparsity, 8 * sizeof(unsigned long long)));
+      QLX_HIP(hipHostMalloc((void**)&L->h_sparsity, 8 * sizeof(unsigned long long), hipHostMallocDefault));
       QLX_HIP(hipMalloc(&L->d_idx, (size_t)L->max_updates * B * sizeof(uint64_t)));
       const size_t UB = (size_t)L->max_updates * B;   // all batches of one vector step
       QLX_HIP(hipMalloc(&L->d_tab_s, UB * 4 * sizeof(void*)));
@@ -698,9 +710,9 @@ int32_t qlx_learner_destroy(qlx_learner* L) {
     void* ptrs[] = {L->d_actions, L->d_rewards, L->d_dones, L->d_reset, (void*)L->d_obs_table, L->d_eps, L->d_ep_reward,
                     L->d_hist, L->d_book, L->d_idx, (void*)L->d_tab_s, (void*)L->d_tab_sn, L->d_bact, L->d_brew,
                     L->d_bdone, L->d_losses, L->d_targets, L->d_gsum, L->d_gmin, L->d_ycache, (void*)L->d_ytab,
-                    L->d_yrew, L->d_ydone, L->d_ytmp};
+                    L->d_yrew, L->d_ydone, L->d_ytmp, L->d_sparsity};
     for (void* p : ptrs) (void)hipFree(p);
-    for (void* p : {(void*)L->h_book, (void*)L->h_gsum})
+    for (void* p : {(void*)L->h_book, (void*)L->h_gsum, (void*)L->h_sparsity})
       if (p) (void)hipHostFree(p);
     L->prio.release();
     (void)hipStreamDestroy(L->stream);
@@ -876,8 +888,9 @@ int32_t qlx_learner_priorities(qlx_learner* L, float* is_weights, float* leaves,
 int32_t qlx_learner_frame_sparsity(qlx_learner* L, double* out) {
   return guard([&] {
     QLX_CHECK(L && out, QLX_E_INVALID, "null argument");
-    frame_sparsity(L->d_tab_s, (int)(L->last_updates * L->B), out, L->stream);
-    frame_sparsity(L->d_obs_table, (int)L->N, out + 4, L->stream);
+    QLX_HIP(hipSetDevice(L->device));
+    frame_sparsity(L->d_tab_s, (int)(L->last_updates * L->B), L->d_sparsity, L->h_sparsity, out, L->stream);
+    frame_sparsity(L->d_obs_table, (int)L->N, L->d_sparsity + 4, L->h_sparsity + 4, out + 4, L->stream);
   });
 }
 

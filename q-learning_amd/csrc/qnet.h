@@ -183,5 +183,7 @@ void f32_dense_async(qlx_model* m, hipStream_t s);
 void model_dense_join(qlx_model* m, hipStream_t s);
 // fractions of a batch's fp32 conv work the exact skips leave out (qnet32.hip k_frame_sparsity; synchronises s):
 // out = {conv1 forward zero steps, conv1 weight-gradient zero steps, conv2 background rows, conv3 background rows}
-void frame_sparsity(const uint8_t* const* table, int n, double* out, hipStream_t s);
+// d_cnt: 4 device counters, h_cnt: their pinned host copy (both the caller's, allocated once)
+void frame_sparsity(const uint8_t* const* table, int n, unsigned long long* d_cnt, unsigned long long* h_cnt, double* out,
+                    hipStream_t s);
 }  // namespace qlx

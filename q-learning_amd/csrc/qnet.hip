@@ -608,8 +608,17 @@ static void set_lds_attr(Kern k, size_t bytes) {
 
 // XCD-grouped tile order (xcd_tile): each XCD runs a contiguous range of the tile order, so the operand panels its tiles
 // share are fetched into its own L2 once (for the split forward: about one k split per XCD)
+// bgemm.h's host-checked requirements: every split's k range a multiple of 32, and K % 32 == 0 for a row-major operand
+// (its buffer descriptor spans the whole tensor, so a ragged K would read the next row's data instead of zeros)
+template <class C, class Epi>
+static void bgemm_check(const BGemmProblem<Epi>& P) {
+  QLX_CHECK(P.kps > 0 && P.kps % 32 == 0, QLX_E_STATE, "bgemm: k per split must be a multiple of 32");
+  QLX_CHECK((C::AK && C::BKM) || P.K % 32 == 0, QLX_E_STATE, "bgemm: a row-major operand needs K % 32 == 0");
+}
+
 template <class C, class Epi>
 static void launch_bgemm(const BGemmProblem<Epi>& P, hipStream_t s) {
+  bgemm_check<C>(P);
   set_lds_attr(k_bgemm<C, Epi>, C::LDS);
   hipLaunchKernelGGL((k_bgemm<C, Epi>), dim3(xcd_grid(P.tiles())), dim3(C::T), C::LDS, s, P, 1);
 }
@@ -706,6 +715,8 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
                          m->d_sqf + sq_first(8), m->d_sqf + sq_first(9)};
     auto launch = [&](const auto& Pw, auto kern) {
       QLX_CHECK(Pw.tiles() == kFc1WgradTiles, QLX_E_STATE, "fc1 wgrad tiling changed: update kSqSlots");
+      bgemm_check<CfgFc1Wg>(Pw);
+      bgemm_check<CfgFc1Dg>(Pd);
       fc1_bwd_map(m, Pw, Pd, kFc2WgradBlocks, s);
       constexpr size_t lds_req = CfgFc1Wg::LDS;
       static_assert(lds_req >= (kFc1BwdThreads / 64 + 1) * 24 * sizeof(float), "fc2 wgrad block scratch");

@@ -1094,23 +1094,20 @@ __global__ __launch_bounds__(256) void k_frame_sparsity(const uint8_t* const* ta
   if (threadIdx.x < 4) atomicAdd(cnt + threadIdx.x, (unsigned long long)tot[threadIdx.x]);
 }
 
-void frame_sparsity(const uint8_t* const* table, int n, double* out, hipStream_t s) {
+void frame_sparsity(const uint8_t* const* table, int n, unsigned long long* d_cnt, unsigned long long* h_cnt, double* out,
+                    hipStream_t s) {
   for (int k = 0; k < 4; ++k) out[k] = std::nan("");
   if (n <= 0) return;
-  // (plain allocation and a synchronous read-back after the stream drains: with a stream-ordered allocation and an
-  // asynchronous copy into pageable memory the second of two back-to-back calls now and then read back zeros -
-  // gpurun_out/ls: act [0, 0, 0, 0], then the right fractions from the next call on the same frames)
-  unsigned long long* d = nullptr;
-  QLX_HIP(hipMalloc((void**)&d, 4 * sizeof(unsigned long long)));
-  QLX_HIP(hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), s));
-  hipLaunchKernelGGL(k_frame_sparsity, dim3(std::min(n, 4 * num_cus())), dim3(256), 0, s, table, n, d);
+  // counters and read-back buffer allocated once by the caller; memset, kernel, copy into the pinned buffer and the
+  // drain all on s (round 5's stream-ordered allocation + asynchronous copy into pageable memory returned zeros now and
+  // then for the second of two back-to-back calls: scripts/readback_probe.hip)
+  QLX_HIP(hipMemsetAsync(d_cnt, 0, 4 * sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_frame_sparsity, dim3(std::min(n, 4 * num_cus())), dim3(256), 0, s, table, n, d_cnt);
   QLX_HIP(hipGetLastError());
+  QLX_HIP(hipMemcpyAsync(h_cnt, d_cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   QLX_HIP(hipStreamSynchronize(s));
-  unsigned long long h[4];
-  QLX_HIP(hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost));
-  QLX_HIP(hipFree(d));
   const double per[4] = {400.0, 400.0, 81.0, 49.0};
-  for (int k = 0; k < 4; ++k) out[k] = (double)h[k] / (per[k] * n);
+  for (int k = 0; k < 4; ++k) out[k] = (double)h_cnt[k] / (per[k] * n);
 }
 
 }  // namespace qlx
