@@ -147,6 +147,11 @@ int32_t qlx_model_batch_max_q(qlx_model* m, const uint8_t* obs, uint32_t n, floa
  * concatenated; norms_out (may be NULL) the 10 per-variable L2 norms before clipping. */
 int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions, const float* y, uint32_t batch,
                         float* loss_out, float* grads_out, float* norms_out);
+// Test hook of the data-parallel update tail (round 6): clip_by_norm(grads * scale) per variable + legacy Adam
+// (ResourceApplyAdam, iterations + 1) on host gradients [1,685,667] in the flat variable order, as learner_update runs the
+// tail after an all-reduce with scale = 1 / world (self_driving_tf_q_learner.rs:201 train -> q_learning_model.rs:165-189,
+// split by the build's DP).  norms_out [10] (or NULL): the clip norms of the scaled gradient.
+int32_t qlx_model_apply_gradient(qlx_model* m, const float* grads, float scale, float* norms_out);
 /* Load a TF SavedModel / checkpoint bundle of the reference Breakout model (layer_with_weights-0..4 kernel /
  * bias, OPTIMIZER_SLOT m / v, optimizer/iter; shapes checked against saved/ql_model_breakout_84x84x4_3_32). */
 int32_t qlx_model_load_tf(qlx_model* m, const char* bundle_prefix);

@@ -1074,6 +1074,33 @@ int32_t qlx_model_train(qlx_model* m, const uint8_t* obs, const uint8_t* actions
   });
 }
 
+// The update tail alone on a given gradient (test hook of the data-parallel tail, whose all-reduced gradient is scaled by
+// 1 / world): clip_by_norm of (grads x scale) per variable + legacy Adam, exactly as learner_update runs them after an
+// all-reduce (model_norms, then model_adam at that scale).  fp32: the same two launches as a rank's DP tail; bf16: the
+// explicit sum-of-squares pass (the backward's fused partials do not belong to this gradient) and the Adam launch.
+int32_t qlx_model_apply_gradient(qlx_model* m, const float* grads, float scale, float* norms_out) {
+  return guard([&] {
+    QLX_CHECK(m && grads, QLX_E_INVALID, "null argument");
+    QLX_CHECK(std::isfinite(scale) && scale > 0.0f, QLX_E_INVALID, "scale must be finite and > 0");
+    QLX_HIP(hipSetDevice(m->device));
+    hipStream_t s = m->stream;
+    model_dense_join(m, s);
+    model_workspace(m, std::max(m->ws_batch, 1));   // (the norm partial buffers)
+    QLX_HIP(hipMemcpyAsync(m->d_grads, grads, kNumParams * 4, hipMemcpyHostToDevice, s));
+    if (m->f32) {
+      m->f32_update_scheduled = false;
+      model_norms(m, s, scale);
+    } else {
+      m->norms_fused = false;
+      hipLaunchKernelGGL(k_sumsq, dim3(m->n_ranges), dim3(256), 0, s, m->d_grads, m->d_rbeg, m->d_rend, scale, m->d_partial);
+      QLX_HIP(hipGetLastError());
+    }
+    model_adam(m, s, scale);
+    if (norms_out) QLX_HIP(hipMemcpyAsync(norms_out, m->d_norms, kNumVars * 4, hipMemcpyDeviceToHost, s));
+    QLX_HIP(hipStreamSynchronize(s));
+  });
+}
+
 int32_t qlx_model_last_activation(qlx_model* m, int32_t layer, float* out) {
   return guard([&] {
     QLX_CHECK(m && out && layer >= 1 && layer <= 4 && m->ws_batch > 0, QLX_E_INVALID, "bad argument");

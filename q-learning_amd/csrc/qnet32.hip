@@ -576,6 +576,12 @@ static int num_cus();
 // background flags in LDS until it writes its lists) - so a part with few CUs (a CPX partition) runs more blocks
 constexpr int kC1MaxIt = 64;
 static int c1_blocks(int n) { return std::max(std::min(n, 2 * num_cus()), (n + kC1MaxIt - 1) / kC1MaxIt); }
+// the training-batch forward (n <= 2,048: not a chunk pass) runs one sample per block (k_conv1_fwd32 ONE)
+#ifndef QLX_C1_ONE
+#define QLX_C1_ONE 1
+#endif
+static bool c1_one(int n) { return QLX_C1_ONE && n <= 2048; }
+static int c1_grid(int n) { return c1_one(n) ? n : c1_blocks(n); }
 
 void f32_workspace(qlx_model* m, int B) {
   if (B <= m->ws_batch) return;
@@ -598,9 +604,10 @@ void f32_workspace(qlx_model* m, int B) {
   const size_t o_loss = take(64);
   // row lists: kListSlots regions of ceil(G / kListSlots) blocks x ceil(n / G) samples each (G = c1_blocks(n) for a chunk of
   // n <= C samples): kListSlots x that <= (G + kListSlots)(n / G + 1) = n + G + kListSlots n / G + kListSlots, with
-  // G >= min(n, 2 CUs) and G <= max(2 CUs, C / kC1MaxIt + 1)
+  // G >= min(n, 2 CUs) and G <= max(2 CUs, C / kC1MaxIt + 1) (one sample per block, c1_one: G = n, n + kListSlots)
   const int frl_cap = C + kListSlots * (C / std::max(1, std::min(C, 2 * num_cus())) + 1) +
                       std::max(2 * num_cus(), C / kC1MaxIt + 1) + kListSlots;
+  static_assert(2048 + kListSlots <= 2048 + kListSlots * 2, "c1_one list capacity");
   const size_t o_rl2 = take((size_t)frl_cap * 81 * 4), o_rl3 = take((size_t)frl_cap * 49 * 4);
   const size_t o_rcnt = take(2 * 2 * kListSlots * kCntStride * 8), o_bgc = take(160 * 4);
   QLX_HIP(hipMalloc(&m->ws, off));
@@ -748,7 +755,8 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     // background rows: conv1 lists them, conv2 / conv3 run the rest (the list counters alternate between forwards)
     const bool lists = bg_rows(m);
     unsigned long long* cnt = w.frcnt + 2 * kListSlots * kCntStride * w.fparity;
-    const int G = c1_blocks(n);                                        // conv1 blocks
+    const bool one = c1_one(n);
+    const int G = c1_grid(n);                                          // conv1 blocks
     const int per_slot = ((G + kListSlots - 1) / kListSlots) * ((n + G - 1) / G);   // samples of a list region, at most
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
@@ -759,10 +767,11 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
       hipEvent_t ea = nullptr, eb = nullptr;
       if (m->prof) m->prof->ext(sc, 2.0 * n * 400 * 32 * 256, &ea, &eb);
-      auto kern = big ? k_conv1_fwd32<1> : k_conv1_fwd32<0>;
-      QLX_CHECK((n + G - 1) / G <= kC1MaxIt, QLX_E_STATE, "conv1 forward: too many samples per block");
-      const size_t lds = 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
-      set_lds_limit((const void*)kern, 2 * kC1Frames + 3 * kC1RmDw * 4 + (size_t)kC1MaxIt * 6 * 8);
+      auto kern = big ? k_conv1_fwd32<1> : one ? k_conv1_fwd32<0, true> : k_conv1_fwd32<0>;
+      QLX_CHECK((n + G - 1) / G <= (one ? 1 : kC1MaxIt), QLX_E_STATE, "conv1 forward: too many samples per block");
+      const size_t frames = (one ? 1 : 2) * kC1Frames;
+      const size_t lds = frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
+      set_lds_limit((const void*)kern, frames + 3 * kC1RmDw * 4 + (size_t)(one ? 1 : kC1MaxIt) * 6 * 8);
       hipExtLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
                             p + voff(0), p + voff(1), w.fa1, c1_skip(m), L);
       QLX_HIP(hipGetLastError());

@@ -45,11 +45,22 @@ __host__ __device__ constexpr int kmaj_pitch(int rows, int mf) {
 static_assert(kmaj_pitch(32, 16) == 48 && kmaj_pitch(64, 16) == 80 && kmaj_pitch(128, 16) == 144 && kmaj_pitch(64, 32) == 96,
               "KMAJ pitches");
 
-// (RMAJ pitch 36 leaves ds_read_b32 fragment reads 2-way conflicted: rows i and i + 8 share a bank.  A k-pair swap for rows
-// 8..15 that removes it measured slower at C3 in round 3 - fc1 forward 39.0 -> 43.1 us, 198.6K -> 194.9K env-steps/s.)
+// RMAJ images of the 16x16x4 MFMA (P8, round 6): lane l of a fragment read needs (row r0 + l % 16, k = 4 kk + l / 16) at
+// k step kk, so over one slab a lane reads k = g, g + 4, .., g + 28 (g = l / 16).  The image stores a row's 32 k at the
+// permuted positions P(k) = (k % 4) * 8 + k / 4, which puts those eight k of lane group g side by side (P = 8 g + kk):
+// two ds_read_b128 (16-byte chunks 2 g and 2 g + 1) fetch a lane's operands of all eight k steps, in the same k order
+// as before - the chains, and so every result, are unchanged.  The chunk index is XORed with row & 1 and the pitch is
+// 40 floats: with the ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS every fragment read is conflict-free, and so
+// are the stores, which become four ds_write_b32 per float4 of k (positions 8 q + j, q = 0..3, for the float4 j of a row)
+// (scripts/lds_banks.py --p8 checks both).  Before: pitch 36 and one ds_read_b32 per k step and fragment, 2-way
+// conflicted (rows i and i + 8 share a bank; a k-pair swap for rows 8..15 that removed it measured slower in round 3).
+#ifndef QLX_Q32_P8
+#define QLX_Q32_P8 1   // (A/B builds: -DQLX_Q32_P8=0 restores the round-5 pitch-36 image and ds_read_b32 fragments)
+#endif
 template <int ROWS, bool KMAJ, int MF = 16>
 struct Opnd {
-  static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS, MF) : BK + 4;
+  static constexpr bool P8 = QLX_Q32_P8 && !KMAJ && MF == 16;
+  static constexpr int PITCH = KMAJ ? kmaj_pitch(ROWS, MF) : P8 ? BK + 8 : BK + 4;
   static constexpr int FLOATS = KMAJ ? BK * PITCH : ROWS * PITCH;
   static constexpr int F4 = ROWS * BK / 4;   // float4 per slab
   static constexpr int KG = 64 / MF;         // k per MFMA (lane groups)
@@ -57,15 +68,73 @@ struct Opnd {
     if (KMAJ) { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
     else { row = idx >> 3; k = (idx & 7) * 4; }
   }
+  // P8: float offset of (row, k) in the image
+  __host__ __device__ static constexpr int p8_off(int row, int k) {
+    return row * PITCH + 4 * ((((k & 3) * 8 + (k >> 2)) >> 2) ^ (row & 1)) + ((k >> 2) & 3);
+  }
   __device__ static void put(float* t, int row, int k, f32x4 v) {
-    *reinterpret_cast<f32x4*>(t + (KMAJ ? k * PITCH + row : row * PITCH + k)) = v;
+    if constexpr (P8) {   // k = 4 j: the four k of the float4 go to positions 8 q + j
+      const int j = k >> 2, o = row * PITCH + (j & 3), x = row & 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[o + 4 * ((2 * q + (j >> 2)) ^ x)] = v[q];
+    } else {
+      *reinterpret_cast<f32x4*>(t + (KMAJ ? k * PITCH + row : row * PITCH + k)) = v;
+    }
   }
   __device__ static float at(const float* t, int row, int k) {
+    if constexpr (P8) return t[p8_off(row, k)];
     return KMAJ ? t[k * PITCH + row] : t[row * PITCH + k];
   }
   // MFMA operand of the MF rows from r0, k step kk: lane l holds (r0 + l % MF, KG kk + l / MF)
   __device__ static float frag(const float* t, int r0, int kk, int lane) { return at(t, r0 + (lane & (MF - 1)), KG * kk + lane / MF); }
+  // P8: the operands of k steps 4 h .. 4 h + 3 of the slab (element q = k step 4 h + q): one ds_read_b128
+  __device__ static f32x4 frag4(const float* t, int r0, int h, int lane) {
+    const int row = r0 + (lane & 15);
+    return *reinterpret_cast<const f32x4*>(t + row * PITCH + 4 * ((2 * (lane >> 4) + h) ^ (lane & 1)));
+  }
 };
+
+// One slab's MFMA chains of a wave's TM x TN fragments (k steps in ascending order; P8 operands read four k steps per
+// ds_read_b128, the others one ds_read_b32 per k step).  bsum (DB): the B fragments' running column sums (bias chains).
+template <class OA, class OB, int TM, int TN, bool DB, class Acc>
+__device__ __forceinline__ void slab_mfma16(const float* a, const float* b, int wm, int wn, int lane, Acc (&acc)[TM][TN],
+                                            float (&bsum)[TN], bool do_bias = true) {
+  constexpr int MF = 16;
+#pragma unroll
+  for (int h = 0; h < BK / 16; ++h) {
+    f32x4 a4[TM], b4[TN];
+    if constexpr (OA::P8)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a4[i] = OA::frag4(a, (wm * TM + i) * MF, h, lane);
+    if constexpr (OB::P8)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b4[j] = OB::frag4(b, (wn * TN + j) * MF, h, lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = 4 * h + q;
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (OA::P8) af[i] = a4[i][q];
+        else af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (OB::P8) bf[j] = b4[j][q];
+        else bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
+      }
+      if constexpr (DB) {
+        if (do_bias)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bsum[j] = __fadd_rn(bsum[j], bf[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+}
 
 // K-split groups of a policy: its member KSPLIT when it has one, else 1 (gemm_body)
 template <class P, class = void>
@@ -288,23 +357,24 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     const float* a = (s & 1) ? As1 : As0;
     const float* b = (s & 1) ? Bs1 : Bs0;
     if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
+    if constexpr (MF == 16) {
+      slab_mfma16<OA, OB, TM, TN, P::BIAS>(a, b, wm, wn, lane, acc, bsum, do_bias);
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < BK / OA::KG; ++kk) {
-      float af[TM], bf[TN];
+      for (int kk = 0; kk < BK / OA::KG; ++kk) {
+        float af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
+        for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
-      if (P::BIAS && do_bias)
+        for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
+        if (P::BIAS && do_bias)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bsum[j] = __fadd_rn(bsum[j], bf[j]);
+          for (int j = 0; j < TN; ++j) bsum[j] = __fadd_rn(bsum[j], bf[j]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (MF == 16) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-          else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-        }
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
     }
   };
   // iteration s: x holds slab s + 1, y is free.  Every iteration issues its loads unconditionally (the last slab again
@@ -522,18 +592,8 @@ __device__ __forceinline__ void gemm_body_chain(const P& p, int lb, float* lds) 
     const float* a = (s & 1) ? As1 : As0;
     const float* b = (s & 1) ? Bs1 : Bs0;
     if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
-#pragma unroll
-    for (int kk = 0; kk < BK / OA::KG; ++kk) {
-      float af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
+    float nobias[TN];
+    slab_mfma16<OA, OB, TM, TN, false>(a, b, wm, wn, lane, acc, nobias);
   };
   constexpr bool PRE = HasEpiPre<P>::value;
   f32x4 pre[TM][TN];
@@ -820,21 +880,7 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
       const float* a = (s & 1) ? As1 : As0;
       const float* b = (s & 1) ? Bs1 : Bs0;
       if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
-#pragma unroll
-      for (int kk = 0; kk < BK / OA::KG; ++kk) {
-        float af[TM], bf[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = OA::frag(a, (wm * TM + i) * MF, kk, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bf[j] = OB::frag(b, (wn * TN + j) * MF, kk, lane);
-        if constexpr (DB)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bsum[j] = __fadd_rn(bsum[j], bf[j]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-      }
+      slab_mfma16<OA, OB, TM, TN, DB>(a, b, wm, wn, lane, acc, bsum);
     };
     // (the store of slab s + 1 is unconditional: past the last slab it writes the idle buffer with the reloaded last slab,
     // which nothing reads.  Skipped there, its registers' loads stayed pending on that path, and the compiler - which does
@@ -916,8 +962,24 @@ __global__ __launch_bounds__(threads_of<P>()) void k_gemm32(const P p) {
 
 // two independent GEMMs in one grid (hardware blocks [side.blocks(), side.blocks() + G1) run P1), plus `side` leading
 // blocks running S and `tail` trailing blocks running T (independent work that fills CU slots beside / after the tiles)
+// Occupancy floor of a pair launch (waves per SIMD the register allocation must allow): the larger of QLX_PAIR_MINW and
+// the policies' MINW members.  Round 6: the P8 fragments' b128 reads let the compiler hoist a whole slab's operands; at
+// the default allocation the conv2 pair grew 112 -> 154 VGPRs (3 waves / SIMD, 95.0 -> 98.0 us); held to 4 waves it
+// takes 106 VGPRs (93.4 us).
+#ifndef QLX_PAIR_MINW
+#define QLX_PAIR_MINW 4
+#endif
+template <class P, class = void>
+struct MinWOf : std::integral_constant<int, 1> {};
+template <class P>
+struct MinWOf<P, std::void_t<decltype(P::MINW)>> : std::integral_constant<int, P::MINW> {};
+template <class P1, class P2>
+constexpr int pair_minw() {
+  return QLX_PAIR_MINW > MinWOf<P1>::value ? (QLX_PAIR_MINW > MinWOf<P2>::value ? QLX_PAIR_MINW : MinWOf<P2>::value)
+                                           : (MinWOf<P1>::value > MinWOf<P2>::value ? MinWOf<P1>::value : MinWOf<P2>::value);
+}
 template <class P1, class P2, class S, class T>
-__global__ __launch_bounds__(256) void k_gemm32_pair(const P1 p1, const P2 p2, const S side, const T tail) {
+__global__ __launch_bounds__(256, (pair_minw<P1, P2>())) void k_gemm32_pair(const P1 p1, const P2 p2, const S side, const T tail) {
   static_assert(KSplitOf<P1>::value == 1 && KSplitOf<P2>::value == 1, "pair launches: 256 threads");
   extern __shared__ float lds[];
   const int b = blockIdx.x, ns = side.blocks();
@@ -1390,6 +1452,11 @@ using PFc1DgradS = PFc1DgradT<32, 64, 2, 2>;
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1WgradT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  // the pair at >= 6 waves per SIMD (78 VGPRs; at the default allocation the P8 fragments took it to 86, 5 waves)
+#ifndef QLX_FC1_MINW
+#define QLX_FC1_MINW 6
+#endif
+  static constexpr int MINW = QLX_FC1_MINW;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, BIAS = true;
   Grid g;
   const float* a3;
@@ -2167,73 +2234,15 @@ __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int
   }
 }
 
-// forward: a1[b][r][oc] = relu(chain over k = (kh, kw, c) of x * W0[kh][kw][c][oc] + b0[oc]), r = (oh, ow).
-// Wave w owns output channels (w & 1) * 16 .. + 15 and the tiles t = (w >> 1) + 2 j (13 / 12 of the 25); tile t is the
-// 4 x 4 patch of output positions oh = 4 (t / 5) + 0..3, ow = 4 (t % 5) + 0..3 (tile row l = (oh % 4, ow % 4)); one
-// v_mfma_f32_16x16x4_f32 per (tile, kh, kw) with c on the lane groups, W0 fragments resident in VGPRs.
-// Zero steps (skip != 0): an MFMA whose 64 frame values are all 0 adds +-0 to each of its 16 x 16 chains, which leaves
-// every chain as it is (a chain from +0 never holds -0: x + (-x) and +0 + -0 round to +0), so it is not issued.  The
-// frames are mostly background (0), and a patch tile's receptive field (20 x 20 pixels per frame) is often all of it
-// (~70 % of the steps at C3), where a tile of 16 consecutive positions crosses the side walls.  Exact for finite W0.
-// ROLE only names the instantiation (0: training batches, 1: chunk-size target / acting passes), so a kernel trace
-// tells the two launch shapes apart
-template <int ROLE>
-__global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0, const float* b0,
-                                                        float* a1, int skip, const C1Lists L) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // [2][4 slots][1776 dwords], rm [3][24], flags
-  uint32_t* rm = c1w + 2 * 4 * kC1SlotDw;
-  unsigned long long* cl = reinterpret_cast<unsigned long long*>(rm + 3 * kC1RmDw);   // [iteration][3][2] (c1_flags)
-  const bool lists = L.rl2 != nullptr;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (lists) {
-    if (blockIdx.x == 0 && tid < 2 * kListSlots) L.cnt_next[tid * kCntStride] = 0ull;
-    if (blockIdx.x == 0 && tid < 32) L.xbg[tid] = relu(0.0f + b0[tid]);   // conv2's constant input row
-    if (tid < 3 * kC1RmDw) rm[tid] = 0u;
-    __syncthreads();
-  }
-  const int ct = wave & 1, rp = wave >> 1;
-  const int col = ct * 16 + (lane & 15), g = lane >> 4;
-  float wf[64];
-#pragma unroll
-  for (int kk = 0; kk < 64; ++kk) wf[kk] = w0[(kk * 4 + g) * 32 + col];
-  const float bias = b0[col];
-  // dword offsets of the lane's 13 tile rows (lane group g reads ring slot g), two 16-bit offsets per register
-  uint32_t ob2[7];
-#pragma unroll
-  for (int j = 0; j < 7; ++j) ob2[j] = 0;
-#pragma unroll
-  for (int j = 0; j < 13; ++j) {
-    const int t = rp + 2 * j < 25 ? rp + 2 * j : 0, l = lane & 15;
-    const int oh = 4 * (t / 5) + (l >> 2), ow = 4 * (t % 5) + (l & 3);
-    ob2[j >> 1] |= (uint32_t)(g * kC1SlotDw + 4 * oh * 21 + ow) << (16 * (j & 1));
-  }
-  const int nt = rp == 0 ? 13 : 12;
-  int b = blockIdx.x;
-  if (b >= B) return;
-  uint4 pf[7];
-  c1_prefetch(c1_ptrs(table, b), pf);
-  // frame pointers one sample ahead of the frames (scalar registers)
-  C1Ptrs nxt = c1_ptrs(table, b + (int)gridDim.x < B ? b + (int)gridDim.x : b);
-  c1_stage(c1w, pf);
-  if (lists) c1_mark(rm, pf);
-  __syncthreads();
-  for (int it = 0; b < B; b += gridDim.x, ++it) {
-    const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
-    const int nb = b + gridDim.x;
-    if (nb < B) {
-      c1_prefetch(nxt, pf);
-      nxt = c1_ptrs(table, nb + (int)gridDim.x < B ? nb + (int)gridDim.x : nb);
-    }
-    // row masks: buffer it % 3 holds sample b's (complete since the last barrier, read by c1_flags at the end of this
-    // iteration); (it + 1) % 3 gets the next sample's at the end of this iteration; (it + 2) % 3, read at the end of
-    // it - 1, is cleared for it + 1
-    if (lists && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
-    // tile-outer: each tile's chain over (kq, kw) runs to completion and its four rows are stored before the next tile's
-    // chain, so the sample's a1 stores (51 KB) leave during its MFMAs instead of after the last one; the next tile's 16
-    // frame dwords are read while this tile multiplies (against the kq-outer loop over all 13 accumulators: 49.1 -> 47.9 us
-    // at B = 1024, 320 -> 309 us per 8,192-sample chunk, 256 -> 218 VGPRs; gpurun_out/w4).  One branch per (kq, tile) with
-    // its four kw steps back to back (a branch per MFMA: 60 vs 46 us at C3)
+// One sample's conv1 forward in one wave (k_conv1_fwd32): its 12 / 13 patch tiles of 16 output channels from the frames fr
+// staged in LDS; tile-outer: each tile's chain over (kq, kw) runs to completion and its four rows are stored before the
+// next tile's chain, so the sample's a1 stores (51 KB) leave during its MFMAs instead of after the last one; the next
+// tile's 16 frame dwords are read while this tile multiplies (against the kq-outer loop over all 13 accumulators: 49.1 ->
+// 47.9 us at B = 1024, 320 -> 309 us per 8,192-sample chunk, 256 -> 218 VGPRs; gpurun_out/w4).  One branch per (kq, tile)
+// with its four kw steps back to back (a branch per MFMA: 60 vs 46 us at C3)
+__device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t (&ob2)[7], int nt, int rp, int g, int col,
+                                              const float (&wf)[64], float bias, int skip, float* a1, int b) {
+  {
     uint32_t dn[16];
     auto tile_dwords = [&](int j, uint32_t (&d)[16]) {
       const uint32_t base = (ob2[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
@@ -2264,6 +2273,96 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd32(const uint8_t* const* ta
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[i] + bias);
       }
+  }
+}
+
+// forward: a1[b][r][oc] = relu(chain over k = (kh, kw, c) of x * W0[kh][kw][c][oc] + b0[oc]), r = (oh, ow).
+// Wave w owns output channels (w & 1) * 16 .. + 15 and the tiles t = (w >> 1) + 2 j (13 / 12 of the 25); tile t is the
+// 4 x 4 patch of output positions oh = 4 (t / 5) + 0..3, ow = 4 (t % 5) + 0..3 (tile row l = (oh % 4, ow % 4)); one
+// v_mfma_f32_16x16x4_f32 per (tile, kh, kw) with c on the lane groups, W0 fragments resident in VGPRs.
+// Zero steps (skip != 0): an MFMA whose 64 frame values are all 0 adds +-0 to each of its 16 x 16 chains, which leaves
+// every chain as it is (a chain from +0 never holds -0: x + (-x) and +0 + -0 round to +0), so it is not issued.  The
+// frames are mostly background (0), and a patch tile's receptive field (20 x 20 pixels per frame) is often all of it
+// (~70 % of the steps at C3), where a tile of 16 consecutive positions crosses the side walls.  Exact for finite W0.
+// ROLE only names the instantiation (0: training batches, 1: chunk-size target / acting passes), so a kernel trace
+// tells the two launch shapes apart.
+// ONE (round 6, the training batch): one sample per block, grid = B.  The persistent form (two blocks per CU, each block's
+// samples in turn, the next sample's frames in flight in registers) holds 220 VGPRs and two frame buffers (57 KB), so a
+// CU runs two samples at a time and a B = 1,024 batch is two samples deep per block: a sample's frame fetch, its
+// 13-tile chains and its a1 stores follow each other.  One sample per block needs one frame buffer (28 KB) and no prefetch
+// registers, so 4 blocks share a CU and all of a CU's samples run at once (VGPRs held to 128 by the launch bound).
+#ifndef QLX_C1_ONE_MINW
+#define QLX_C1_ONE_MINW 4
+#endif
+template <int ROLE, bool ONE = false>
+__global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(const uint8_t* const* table, int B, const float* w0,
+                                                                           const float* b0, float* a1, int skip, const C1Lists L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // [2 (ONE: 1)][4 slots][1776 dwords], rm [3][24], flags
+  uint32_t* rm = c1w + (ONE ? 1 : 2) * 4 * kC1SlotDw;
+  unsigned long long* cl = reinterpret_cast<unsigned long long*>(rm + 3 * kC1RmDw);   // [iteration][3][2] (c1_flags)
+  const bool lists = L.rl2 != nullptr;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (lists) {
+    if (blockIdx.x == 0 && tid < 2 * kListSlots) L.cnt_next[tid * kCntStride] = 0ull;
+    if (blockIdx.x == 0 && tid < 32) L.xbg[tid] = relu(0.0f + b0[tid]);   // conv2's constant input row
+    if (tid < 3 * kC1RmDw) rm[tid] = 0u;
+    __syncthreads();
+  }
+  const int ct = wave & 1, rp = wave >> 1;
+  const int col = ct * 16 + (lane & 15), g = lane >> 4;
+  float wf[64];
+#pragma unroll
+  for (int kk = 0; kk < 64; ++kk) wf[kk] = w0[(kk * 4 + g) * 32 + col];
+  const float bias = b0[col];
+  // dword offsets of the lane's 13 tile rows (lane group g reads ring slot g), two 16-bit offsets per register
+  uint32_t ob2[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) ob2[j] = 0;
+#pragma unroll
+  for (int j = 0; j < 13; ++j) {
+    const int t = rp + 2 * j < 25 ? rp + 2 * j : 0, l = lane & 15;
+    const int oh = 4 * (t / 5) + (l >> 2), ow = 4 * (t % 5) + (l & 3);
+    ob2[j >> 1] |= (uint32_t)(g * kC1SlotDw + 4 * oh * 21 + ow) << (16 * (j & 1));
+  }
+  const int nt = rp == 0 ? 13 : 12;
+  int b = blockIdx.x;
+  if (b >= B) return;
+  if constexpr (ONE) {
+    {
+      uint4 pf[7];
+      c1_prefetch(c1_ptrs(table, b), pf);
+      c1_stage(c1w, pf);
+      if (lists) c1_mark(rm, pf);
+    }
+    __syncthreads();
+    c1_fwd_sample(c1w, ob2, nt, rp, g, col, wf, bias, skip, a1, b);
+    if (lists) {
+      if (wave < 3) c1_flags(rm, cl + wave * 2, wave, tid);
+      __syncthreads();
+      if (wave < 3) c1_lists_flush(cl, 1, blockIdx.x, gridDim.x, L, wave, tid, B);
+    }
+    return;
+  }
+  uint4 pf[7];
+  c1_prefetch(c1_ptrs(table, b), pf);
+  // frame pointers one sample ahead of the frames (scalar registers)
+  C1Ptrs nxt = c1_ptrs(table, b + (int)gridDim.x < B ? b + (int)gridDim.x : b);
+  c1_stage(c1w, pf);
+  if (lists) c1_mark(rm, pf);
+  __syncthreads();
+  for (int it = 0; b < B; b += gridDim.x, ++it) {
+    const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
+    const int nb = b + gridDim.x;
+    if (nb < B) {
+      c1_prefetch(nxt, pf);
+      nxt = c1_ptrs(table, nb + (int)gridDim.x < B ? nb + (int)gridDim.x : nb);
+    }
+    // row masks: buffer it % 3 holds sample b's (complete since the last barrier, read by c1_flags at the end of this
+    // iteration); (it + 1) % 3 gets the next sample's at the end of this iteration; (it + 2) % 3, read at the end of
+    // it - 1, is cleared for it + 1
+    if (lists && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
+    c1_fwd_sample(fr, ob2, nt, rp, g, col, wf, bias, skip, a1, b);
     if (lists && wave < 3) c1_flags(rm + (it % 3) * kC1RmDw, cl + it * 6 + wave * 2, wave, tid);
     if (nb < B) {
       c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);

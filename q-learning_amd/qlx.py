@@ -133,6 +133,7 @@ def lib():
         "qlx_model_iterations": ([vp], C.c_int64), "qlx_model_copy_weights": ([vp, vp], i32),
         "qlx_model_predict": ([vp, vp, u32, vp, vp], i32), "qlx_model_batch_max_q": ([vp, vp, u32, vp], i32),
         "qlx_model_train": ([vp, vp, vp, vp, u32, vp, vp, vp], i32),
+        "qlx_model_apply_gradient": ([vp, vp, C.c_float, vp], i32),
         "qlx_model_last_activation": ([vp, i32, vp], i32),
         "qlx_model_write_checkpoint": ([vp, C.c_char_p], i32), "qlx_model_read_checkpoint": ([vp, C.c_char_p], i32),
         "qlx_model_sync": ([vp], i32),
@@ -442,6 +443,14 @@ class DeepQLearningModel:
             out.append(grads[off:off + n].reshape(s))
             off += n
         return loss.value, out, norms
+
+    def apply_gradient(self, flat_grads, scale=1.0):
+        """the update tail alone (qlx_model_apply_gradient): clip_by_norm(flat_grads * scale) + Adam; the clip norms"""
+        g = np.ascontiguousarray(flat_grads, dtype=np.float32)
+        assert g.size == sum(int(np.prod(s)) for s in VAR_SHAPES)
+        norms = np.zeros(NUM_VARS, np.float32)
+        _check(lib().qlx_model_apply_gradient(self.h, _p(g), C.c_float(scale), _p(norms)))
+        return norms
 
     def write_checkpoint(self, path):
         _check(lib().qlx_model_write_checkpoint(self.h, path.encode()))

@@ -421,13 +421,19 @@ def test_learner_runs_many_steps_without_faults():
     assert np.isfinite(w).all()
 
 
-def test_data_parallel_path_single_rank_bit_identical():
-    """The data-parallel update path (dense gradient bucket all-reduced on the communicator's stream while the conv
-    backward runs, then the conv bucket, Adam after both) on a single-rank RCCL communicator equals the plain
-    single-GPU path bit for bit: the stream hand-offs order every read and write."""
+@pytest.mark.parametrize("prec", [0, 1], ids=["fp32", "bf16"])
+@pytest.mark.parametrize("overlap", ["1", "0"], ids=["two_buckets", "one_allreduce"])
+def test_data_parallel_path_single_rank_bit_identical(monkeypatch, overlap, prec):
+    """The data-parallel update path on a single-rank RCCL communicator equals the plain single-GPU path bit for bit, in
+    both precisions and both DP schedules: QLX_DP_OVERLAP=1 (the default: dense gradient bucket all-reduced on the
+    communicator's stream while the conv backward runs, its clip-norm partials there, then the conv bucket, the update
+    tail after both) and QLX_DP_OVERLAP=0 (one whole-gradient all-reduce after the backward, then the tail): the stream
+    hand-offs order every read and write.  (At world 1 the tail's scale is exactly 1; scale != 1 is
+    test_update_tail_scaled_gradient.)"""
     qlx = _qlx()
+    monkeypatch.setenv("QLX_DP_OVERLAP", overlap)   # read by dist_init
     p = dict(n_envs=64, batch_size=64, history_buffer_len=4000, update_after_actions=16, epsilon_pure_random_steps=1000,
-             max_steps_per_episode=300)
+             max_steps_per_episode=300, qnet_precision=prec)
     plain = qlx.SelfDrivingQLearner(qlx.Parameter(**p))
     dp = qlx.SelfDrivingQLearner(qlx.Parameter(**p))
     dp.dist_init(1, 0, qlx.dist_unique_id())
@@ -441,6 +447,38 @@ def test_data_parallel_path_single_rank_bit_identical():
         for which in range(3):
             assert np.array_equal(plain.model.get(var, which), dp.model.get(var, which)), (var, which)
     assert plain.stats()["update_count"] == dp.stats()["update_count"] > 50
+
+
+@pytest.mark.parametrize("scale", [0.5, 0.25, 1.0 / 3.0, 1.0 / 8.0, 1.0])
+def test_update_tail_scaled_gradient(scale):
+    """The update tail a data-parallel rank runs after the all-reduce (learner.hip learner_update: model_norms +
+    model_adam at scale = 1 / world) on a known gradient, bit for bit against the oracle's clip_by_norm(g * scale) + legacy
+    Adam (oracle/qnet32_ref.cpp, orc_qnet32_apply - the definition tests/test_dist_cpu.py's world-2 restatement uses):
+    three consecutive updates with different gradients, clip norms and w / m / v after each.  The gradients are the
+    oracle's own chain gradients of a batch, so some variables clip (norm > 1) and some do not."""
+    qlx = _qlx()
+    ref = O.QNet(seed=31, f32=True)
+    gpu = qlx.DeepQLearningModel(seed=31)
+    for v in range(10):
+        gpu.set(v, ref.get(v, 0))
+    rng = np.random.default_rng(77)
+    x = rng.integers(0, 256, (64, 84, 84, 4), dtype=np.uint8)
+    x[:, 20:60] = 0
+    a = rng.integers(0, 3, 64).astype(np.uint8)
+    for t in range(3):
+        scratch = O.QNet(seed=31, f32=True)
+        scratch.load_state_from(ref)
+        y = rng.normal(0, 4.0 * (t + 1), 64).astype(np.float32)
+        _, grads, _ = scratch.train(x, a, y)
+        flat = np.concatenate([g.ravel() for g in grads]).astype(np.float32) * np.float32(3.0 - t)
+        want = O.qnet32_apply(ref, flat, np.float32(scale))
+        got = gpu.apply_gradient(flat, scale)
+        assert same(got, want), (t, got, want)
+        assert (want > 1.0).any() and (want < 1.0).any(), want   # both sides of clip_by_norm exercised
+        for var in range(10):
+            for which in range(3):
+                assert same(gpu.get(var, which), ref.get(var, which)), (scale, t, var, which)
+    assert gpu.iterations() == ref.iterations() == 3
 
 
 def test_invalid_parameters_fail_loudly():
