@@ -214,6 +214,20 @@ def config_label(N, replay, flags, world):
     return f"custom ({world} GPU)"
 
 
+class stdout_to_stderr:
+    """fd 1 -> fd 2 while RCCL initialises a communicator (its version banner goes to stdout; the bench's stdout is the
+    one JSON line)"""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def log(msg):
     """progress on stderr (one line per phase, so a long run shows it is alive)"""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -240,9 +254,11 @@ class Run:
         try:
             if ctl.world > 1:
                 uid = ctl.bcast_bytes(qlx.dist_unique_id() if ctl.rank == 0 else bytes(128))
-                L.dist_init(ctl.world, ctl.rank, uid)
+                with stdout_to_stderr():
+                    L.dist_init(ctl.world, ctl.rank, uid)
             elif dp1:   # a single-rank communicator: the data-parallel update path on one GPU
-                L.dist_init(1, 0, qlx.dist_unique_id())
+                with stdout_to_stderr():
+                    L.dist_init(1, 0, qlx.dist_unique_id())
             self.rccl_world = L.comm_size()   # read back from the communicator (ncclCommCount)
             # steady state: replay at capacity and past the pure-random phase, whatever --warmup is
             prefill = max(-(-args.replay // N), -(-p.epsilon_pure_random_steps // N))
