@@ -9,7 +9,8 @@
 // autograd of the Keras graph (activations, Q, loss, all ten gradients, norms, w / m / v after two Adam steps; B 4..256)
 // and against the double-accumulating restatement qnet_ref.cpp at B = 1024.
 //   conv1 .. conv3  z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
-//   dense 3136->512 z = sum over k ascending (Flatten order h, w, c)
+//   dense 3136->512 z = C0 + C1, Ch = chain over k in [1568 h, 1568 h + 1568) ascending (Flatten order h, w, c; round 6 -
+//                   before: one chain over all k)
 //   dense 512->3    z = ((C0 + C1) + C2) + C3, Cw = chain over k in [128 w, 128 w + 128) ascending
 //   every sum: acc = 0; acc = fmaf(x, w, acc) in that order; then + bias, ReLU (v > 0 ? v : 0)
 //   Huber head      e = q_a - y, h = w (|e| <= 1 ? (0.5 e) e : |e| - 0.5), g = (w clip(e, -1, 1)) / B,
@@ -89,23 +90,29 @@ static void conv_fwd(const Cfg& c, const float* in, int B, const float* W, const
       }
 }
 
-// y[b][n] = act(chain over k of x[b][k] W[k][n] + bias[n])
-static void dense_fwd(const float* x, int B, int K, int N, const float* W, const float* bias, bool relu_out, float* y) {
+// y[b][n] = act(((C0 + C1) + ..) + bias[n]), Ch = chain over k in [h K / chains, (h + 1) K / chains) of x[b][k] W[k][n]
+static void dense_fwd(const float* x, int B, int K, int N, const float* W, const float* bias, bool relu_out, float* y,
+                      int chains) {
 #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b) {
-    std::vector<float> acc(N, 0.0f);
-    for (int k = 0; k < K; ++k) {
-      const float v = x[(size_t)b * K + k];
-      if (v == 0.0f) continue;
-      const float* wr = W + (size_t)k * N;
-      for (int n = 0; n < N; ++n) acc[n] = fma32(v, wr[n], acc[n]);
+    std::vector<float> tot(N, 0.0f), acc(N);
+    for (int h = 0; h < chains; ++h) {
+      std::fill(acc.begin(), acc.end(), 0.0f);
+      for (int k = h * K / chains; k < (h + 1) * K / chains; ++k) {
+        const float v = x[(size_t)b * K + k];
+        if (v == 0.0f) continue;
+        const float* wr = W + (size_t)k * N;
+        for (int n = 0; n < N; ++n) acc[n] = fma32(v, wr[n], acc[n]);
+      }
+      for (int n = 0; n < N; ++n) tot[n] = h == 0 ? acc[n] : tot[n] + acc[n];
     }
     for (int n = 0; n < N; ++n) {
-      const float t = acc[n] + bias[n];
+      const float t = tot[n] + bias[n];
       y[(size_t)b * N + n] = relu_out ? relu(t) : t;
     }
   }
 }
+constexpr int kFc1Chains = 2;   // (qnet32_kernels.h kFc1Chains)
 
 // dense 512 -> 3 head: q[b][n] = (((C0 + C1) + C2) + C3) + b4[n], Cw = fmaf chain over k in [128 w, 128 w + 128)
 static void head_fwd(const float* x, int B, const float* W, const float* bias, float* y) {
@@ -131,7 +138,7 @@ void qnet32_forward(const QNet& q, const uint8_t* x8, int B, Acts& a) {
   conv1_fwd(x8, B, q.w[0].data(), q.w[1].data(), a.a1.data());
   conv_fwd(kC2, a.a1.data(), B, q.w[2].data(), q.w[3].data(), a.a2.data());
   conv_fwd(kC3, a.a2.data(), B, q.w[4].data(), q.w[5].data(), a.a3.data());
-  dense_fwd(a.a3.data(), B, 3136, 512, q.w[6].data(), q.w[7].data(), true, a.a4.data());
+  dense_fwd(a.a3.data(), B, 3136, 512, q.w[6].data(), q.w[7].data(), true, a.a4.data(), kFc1Chains);
   head_fwd(a.a4.data(), B, q.w[8].data(), q.w[9].data(), a.q.data());
 }
 

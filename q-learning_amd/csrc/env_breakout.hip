@@ -539,7 +539,7 @@ int32_t qlx_env_destroy(qlx_env* e) {
     (void)hipStreamSynchronize(e->stream);
     (void)hipFree(e->d_state); (void)hipFree(e->d_obs); (void)hipFree(e->d_hash); (void)hipFree(e->d_flags);
     (void)hipFree(e->d_ep_steps);
-    (void)hipFree(e->d_tmp_u8); (void)hipFree(e->d_tmp_u8b); (void)hipFree(e->d_tmp_f32);
+    (void)hipFree(e->d_tmp_u8); (void)hipFree(e->d_tmp_u8b); (void)hipFree(e->d_tmp_f32); (void)hipFree(e->d_obs_view);
     if (e->own_stream) (void)hipStreamDestroy(e->stream);
     delete e;
   });
@@ -583,15 +583,14 @@ int32_t qlx_env_obs(qlx_env* e, uint8_t* out) {
   return guard([&] {
     QLX_CHECK(e && out, QLX_E_INVALID, "null argument");
     QLX_HIP(hipSetDevice(e->device));
-    uint8_t* d_out = nullptr;
     const size_t bytes = (size_t)e->n * kFramePix * kSlots;
-    QLX_HIP(hipMalloc(&d_out, bytes));
+    // (a device buffer kept by the env: the Rust Environment::step of INTEGRATION.md reads the state every step)
+    if (!e->d_obs_view) QLX_HIP(hipMalloc(&e->d_obs_view, bytes));
     const size_t total = (size_t)e->n * kFramePix;
-    hipLaunchKernelGGL(k_env_obs_view, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, e->d_obs, e->n, d_out);
+    hipLaunchKernelGGL(k_env_obs_view, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, e->d_obs, e->n, e->d_obs_view);
     QLX_HIP(hipGetLastError());
-    QLX_HIP(hipMemcpyAsync(out, d_out, bytes, hipMemcpyDeviceToHost, e->stream));
+    QLX_HIP(hipMemcpyAsync(out, e->d_obs_view, bytes, hipMemcpyDeviceToHost, e->stream));
     QLX_HIP(hipStreamSynchronize(e->stream));
-    QLX_HIP(hipFree(d_out));
   });
 }
 

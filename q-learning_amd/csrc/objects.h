@@ -22,6 +22,7 @@ struct qlx_env {
   uint8_t* d_tmp_u8 = nullptr;     // [n] staging
   uint8_t* d_tmp_u8b = nullptr;    // [n]
   float* d_tmp_f32 = nullptr;      // [n]
+  uint8_t* d_obs_view = nullptr;   // [n][84][84][4] qlx_env_obs's tensor view (allocated on its first call, kept)
   float acos_thr = 0.0f;
   bool hashing = true;
 };

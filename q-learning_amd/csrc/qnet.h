@@ -162,7 +162,10 @@ void model_backward(qlx_model* m, const uint8_t* const* table, int B, const uint
                     hipStream_t s, const float* weights = nullptr, float* td_abs = nullptr, bool fuse_update = false);
 void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
                           const float* weights = nullptr, float* td_abs = nullptr);
-void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update = false);
+// dense_ready (fp32, data parallel): the dense bucket's all-reduce event; the reduction launch then waits for it and computes
+// the dense variables' clip-norm partials of the reduced gradient x dense_scale as its extra blocks (no f32_norms launch)
+void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update = false,
+                         hipEvent_t dense_ready = nullptr, float dense_scale = 1.0f);
 // per-variable norm partials for Adam: with scale == 1 (no all-reduce since the backward) the producers'
 // fused partials are used as they are; otherwise per-range sums of squares of the scaled gradients
 void model_norms(qlx_model* m, hipStream_t s, float scale);
@@ -174,7 +177,8 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
 void f32_head(int mode, const Fc2Args& a, int B, hipStream_t s);   // mode 3 = training head
 void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float* y, float* loss_dev, hipStream_t s,
                         const float* weights, float* td_abs);
-void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update);
+void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update,
+                       hipEvent_t dense_ready = nullptr, float dense_scale = 1.0f);
 void f32_norms(qlx_model* m, hipStream_t s, float scale);
 void f32_adam(qlx_model* m, hipStream_t s, float scale);
 // the dense variables' norm partials + Adam of the update in flight on m->f32_aux (after the fc1 backward on s)

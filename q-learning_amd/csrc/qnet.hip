@@ -733,8 +733,9 @@ void model_backward_dense(qlx_model* m, int B, const uint8_t* actions, const flo
 
 // the conv part of the backward (after model_backward_dense on the same batch): dz3 -> dz2 -> dz1 and the
 // three conv weight gradients into m->d_grads
-void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update) {
-  if (m->f32) { f32_backward_conv(m, table, B, s, fuse_update); return; }
+void model_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update, hipEvent_t dense_ready,
+                         float dense_scale) {
+  if (m->f32) { f32_backward_conv(m, table, B, s, fuse_update, dense_ready, dense_scale); return; }
   ModelWs& w = m->w;
   float* G = m->d_grads;
   // dz2 = convT(dz3, W2) * (a2 > 0); dz1 = convT(dz2, W1) * (a1 > 0), fused per sample (trunk_kernels.h)

@@ -661,7 +661,7 @@ template <class P>
 static void launch(qlx_model* m, const P& p, const char* scope, double work, hipStream_t s) {
   hipEvent_t ea = nullptr, eb = nullptr;
   if (m->prof) m->prof->ext(scope, work, &ea, &eb);
-  hipExtLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(256), gemm_lds_bytes<P>(), s, ea, eb, 0u, p);
+  hipExtLaunchKernelGGL(k_gemm32<P>, dim3(p.g.blocks()), dim3(threads_of<P>()), gemm_lds_bytes<P>(), s, ea, eb, 0u, p);
   QLX_HIP(hipGetLastError());
   debug_sync(s, scope);
 }
@@ -911,10 +911,12 @@ static Adam32Args adam_args(qlx_model* m, float scale) {
   return a;
 }
 
-void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update) {
+void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s, bool fuse_update, hipEvent_t dense_ready,
+                       float dense_scale) {
   ModelWs& w = m->w;
   m->f32_update_scheduled = fuse_update;
-  const NormArgs N = norm_args(m, 1.0f);
+  QLX_CHECK(!(fuse_update && dense_ready), QLX_E_STATE, "dense partials: the scheduled update or the data-parallel form");
+  const NormArgs N = norm_args(m, dense_ready ? dense_scale : 1.0f);
   const float* p = m->d_params;
   float* G = m->d_grads;
   const int z3 = (B + kSC3 - 1) / kSC3, z2 = (B + kSC2 - 1) / kSC2, z1 = (B + kSC1 - 1) / kSC1;
@@ -938,11 +940,12 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
-    constexpr size_t lds = kC1Frames + 400 * 16 * 4;   // 54,016 B
+    constexpr size_t lds = kC1WgradLds;   // 79,488 B
     hipEvent_t ea = nullptr, eb = nullptr;
     if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);
-    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(2 * z1), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1, w.fslab1, c1_skip(m));
+    hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(c1_wgrad_blocks(z1)), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1,
+                          w.fslab1, c1_skip(m));
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv1_wgrad32");
   }
@@ -960,11 +963,19 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
       R.nb[L] = (R.count[L] + per - 1) / per;
       nred += R.nb[L];
     }
-    // the scheduled update: + the dense variables' clip-norm segment partials (4 per block)
-    const int dseg = m->f32_update_scheduled && !m->f32_dense_async ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
+    // the scheduled update: + the dense variables' clip-norm segment partials (4 per block); data parallel (dense_ready):
+    // the same blocks over the reduced dense gradient x dense_scale, once its all-reduce has landed (long before the conv
+    // backward ends) - the launch waits for it, so the update tail is the plain path's two launches (+ the conv all-reduce)
+    const bool dp_dense = dense_ready != nullptr;
+    if (dp_dense) QLX_HIP(hipStreamWaitEvent(s, dense_ready, 0));
+    const int dseg = (m->f32_update_scheduled && !m->f32_dense_async) || dp_dense ? N.seg_first[kNumVars] - N.seg_first[6] : 0;
     hipLaunchKernelGGL(k_wreduce32, dim3(nred + (dseg + 3) / 4), dim3(1024), 0, s, R, N, nred, N.seg_first[6], dseg);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_wreduce32");
+    if (dp_dense) {
+      m->f32_dense_partials = true;
+      m->f32_partials_scale = dense_scale;
+    }
   }
 }
 
@@ -974,6 +985,7 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
 // as soon as the dense bucket is reduced (learner.hip: on the communicator stream, beside the conv backward).
 void f32_norms(qlx_model* m, hipStream_t s, float scale) {
   if (m->f32_update_scheduled) return;   // the backward scheduled them (f32_backward_conv)
+  if (m->f32_dense_partials && m->f32_partials_scale == scale) return;   // the data-parallel reduction launch computed them
   ProfScope ps(m->prof, "f32_norms", s, 4.0 * (kNumParams - kVarOffsetDense));
   const NormArgs N = norm_args(m, scale);
   const int dseg = N.seg_first[kNumVars] - N.seg_first[6];

@@ -833,6 +833,16 @@ template <class P>
 struct HasStreams<P, std::void_t<typename P::Streams>> : std::bool_constant<!std::is_void_v<typename P::Streams>> {};
 #endif
 
+// K-split chains of a policy run one after another in the same waves: its member KSEQ when it has one, else 1
+template <class P, class = void>
+struct KSeqOf : std::integral_constant<int, 1> {};
+template <class P>
+struct KSeqOf<P, std::void_t<decltype(P::KSEQ)>> : std::integral_constant<int, P::KSEQ> {};
+
+// K split (round 6, policies with KSPLIT = G > 1 or KSEQ = Q > 1): the reduction is G (Q) chains over consecutive equal
+// slab ranges, combined ((C0 + C1) + ..) before the epilogue - the same value either way: KSPLIT runs the chains in G
+// wave groups of the block at once (group 0 sums them through LDS), KSEQ one after another in the same waves (the
+// finished chains wait in registers).  ns must be a multiple of G (Q).
 template <class P>
 __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   constexpr int MF = 16;
@@ -841,9 +851,15 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   using Acc = f32x4;
   constexpr int TM = P::BM / (P::WM * MF), TN = P::BN / (P::WN * MF);
   static_assert(TM >= 1 && TN >= 1 && TM * P::WM * MF == P::BM && TN * P::WN * MF == P::BN, "tile shape");
+  constexpr int G = KSplitOf<P>::value, Q = KSeqOf<P>::value;
+  static_assert((G == 1 && Q <= 2) || (Q == 1 && !P::BIAS), "K split: two sequential chains, or wave groups without bias");
+  static_assert(G == 1 || TM * TN * 4 * P::WM * P::WN * 64 <= 2 * (OA::FLOATS + OB::FLOATS), "K-split hand-off fits a group's LDS");
+  constexpr int T = P::WM * P::WN * 64;   // threads of one K group
+  constexpr int GROUP_LDS = 2 * (OA::FLOATS + OB::FLOATS);
   using St = typename P::Streams;
   using Regs = typename St::Regs;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int kg = G > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6) / (P::WM * P::WN)) : 0;
+  const int tid = threadIdx.x - kg * T, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % P::WM, wn = wave / P::WM;
   int tm, tn, z;
@@ -852,8 +868,10 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   if constexpr (HasActive<P>::value) {
     if (!p.active(z, row0)) return;
   }
-  const int ns = p.nslabs(z);
+  const int ns = p.nslabs(z) / G, s_base = kg * ns;   // this group's slabs: s_base + [0, ns)
+  const int s_half = Q > 1 ? ns / 2 : -1;              // KSEQ: the second chain starts at this slab
   St st = p.streams(z, row0, col0, tid);
+  lds += kg * GROUP_LDS;
   float* As0 = lds;
   float* As1 = lds + OA::FLOATS;
   float* Bs0 = lds + 2 * OA::FLOATS;
@@ -868,6 +886,7 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+  Acc first[Q > 1 ? TM : 1][Q > 1 ? TN : 1];   // KSEQ: the finished first chain
   float bsum[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) bsum[j] = 0.0f;
@@ -879,6 +898,17 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
     auto compute = [&](int s) {
       const float* a = (s & 1) ? As1 : As0;
       const float* b = (s & 1) ? Bs1 : Bs0;
+      if constexpr (Q > 1) {
+        if (s == s_half) {   // (wave-uniform) the first chain is done: keep it, start the second from zero
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              first[i][j] = acc[i][j];
+              acc[i][j] = zero4();
+            }
+        }
+      }
       if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
       slab_mfma16<OA, OB, TM, TN, DB>(a, b, wm, wn, lane, acc, bsum);
     };
@@ -887,16 +917,16 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
     // not see that the path leaves the loop - waited for them at the top of every other slab step: the two register sets
     // degenerated to one.)
     auto iter = [&](int s, Regs& xs, Regs& ys) {
-      st.load(s + 2 < ns ? s + 2 : ns - 1, ys);
+      st.load(s_base + (s + 2 < ns ? s + 2 : ns - 1), ys);
       if constexpr (LoadFenceOf<P>::value) __builtin_amdgcn_sched_barrier(0);
       compute(s);
       st.store((s + 1) & 1 ? As1 : As0, (s + 1) & 1 ? Bs1 : Bs0, xs);
       lds_barrier();
     };
     if (ns > 0) {
-      st.load(0, x1);
+      st.load(s_base, x1);
       st.store(As0, Bs0, x1);
-      st.load(ns > 1 ? 1 : 0, x0);
+      st.load(s_base + (ns > 1 ? 1 : 0), x0);
       lds_barrier();
       // (the odd last step after the loop: a conditional second step inside it was, to the compiler, a path back to the
       // loop head with a register set still loading - see iter)
@@ -911,17 +941,47 @@ __device__ __forceinline__ void gemm_body_s(const P& p, int lb, float* lds) {
   constexpr bool PRE = HasEpiPre<P>::value;
   typename PreOf<P>::type pre[TM][TN];
   if constexpr (PRE) {
+    if (kg == 0) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+        for (int j = 0; j < TN; ++j)
+          pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+    }
   }
   if constexpr (P::BIAS) {
     if (do_bias) slab_loop(std::true_type{});
     else slab_loop(std::false_type{});
   } else {
     slab_loop(std::false_type{});
+  }
+  if constexpr (Q > 1) {   // C0 + C1
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = __fadd_rn(ns > s_half ? first[i][j][e] : acc[i][j][e], ns > s_half ? acc[i][j][e] : 0.0f);
+  }
+  if constexpr (G > 1) {   // groups 1 .. G - 1 hand their chains to group 0 through their own LDS (free now); ((C0 + C1) + ..)
+    if (kg > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) lds[((i * TN + j) * 4 + e) * T + tid] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (kg > 0) return;
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = __fadd_rn(acc[i][j][e], lds[g * GROUP_LDS + ((i * TN + j) * 4 + e) * T + tid]);
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1333,10 +1393,18 @@ struct BgRows2 {   // two background-row jobs (a2 and a3) in one launch's leadin
   }
 };
 
-// fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3)
-template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
+// fc1 forward: a4 [B][512] = relu(a3 [B][3136] W3 + b3), the reduction as kFc1Chains chains over consecutive k halves
+// (C0 + C1; round 6): at the training batch the two chains run in two wave groups of a block at once (KS_ =
+// 2: twice the waves on the chip for the same 512 output tiles), at chunk batches one after the other (KQ_ = 2)
+#ifndef QLX_FC1_CHAINS
+#define QLX_FC1_CHAINS 2   // (A/B timing builds only: 1 = the round-5 single chain, which the oracle no longer follows)
+#endif
+constexpr int kFc1Chains = QLX_FC1_CHAINS;
+template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16, int KS_ = 1, int KQ_ = kFc1Chains>
 struct PFc1FwdT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  static constexpr int KSPLIT = KS_, KSEQ = KQ_;
+  static_assert(KS_ * KQ_ == kFc1Chains && MF_ == 16, "fc1 forward: the chain definition");
   static constexpr bool LOAD_FENCE = false;   // (round 5: with it 35.3 / 209.8 us against 33.8 / 203.4)
   // strategy 0 at the training batch (default scheduler 40.4, strategy 1 42.2, 0 39.8 us at B = 1024; round 5: 1 39.3 against
   // 33.8), strategy 1 for the chunk-batch tiles (round 5: 196.7 against 203.4 us)
@@ -1384,12 +1452,12 @@ struct PFc1FwdT {
     return st;
   }
 };
-using PFc1Fwd = PFc1FwdT<>;
+using PFc1Fwd = PFc1FwdT<32, 64, 2, 2, 16, 1, kFc1Chains>;
 // chunk-size batches: 64 x 128 tiles on the stream core (in place: 208 us against 228 us for 64 x 64 on
 // v_mfma_f32_32x32x2_f32, 212 / 215 us for 64 x 64 / 128 x 64; gpurun_out/w12)
-using PFc1FwdB = PFc1FwdT<64, 128, 2, 2, 16>;
+using PFc1FwdB = PFc1FwdT<64, 128, 2, 2, 16, 1, kFc1Chains>;
 // (re-checked on the stream core in place: 32 x 64 / 64 x 32 / 16 x 64 ran 35.3 / 35.9 / 40.4 us against 34.1 us, w9)
-using PFc1FwdS = PFc1FwdT<32, 32, 2, 2>;   // (round 5, after the slab-loop fix: 64 x 32 / 32 x 64 38.4 / 38.9 us against 33.8)
+using PFc1FwdS = PFc1FwdT<32, 32, 2, 2, 16, kFc1Chains, 1>;   // (round 5, after the slab-loop fix: 64 x 32 / 32 x 64 38.4 / 38.9 us against 33.8)
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
@@ -2376,52 +2444,65 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
 // x[r][m] dz1[r][oc] (steps whose frame values are all 0 skipped when skip != 0, exactly as in the forward; exact for
 // finite dz1), m = (kh, kw, c) HWIO; bias slab[z][256][oc] = ((C0 + C1) + C2) + C3 with Cq the chain over (b, rs)
-// ascending of dz1[b][4 rs + q][oc] (the four lane groups' chains of the MFMA B operand).  Block (z, hh)
-// covers output channels hh * 16 .. + 15.  Wave w owns kh = 2 w, 2 w + 1: lane row rho = (kh low bit, h, c), tile
-// t = kw - 4 h, so one LDS dword (pixels 4 ow + 4 h .. + 3 of image row 4 oh + kh) feeds the lane's four MFMAs of a
-// step.  Per sample the frames (row layout) and dz1's channel half sit in LDS (54,016 B) while the next sample's are in
-// flight in registers.
-constexpr int kC1DzChunks = 400 * 16 / 4;   // 1,600 uint4 of one sample's dz1 half
-
-constexpr int kC1WgradThreads = 256;
+// ascending of dz1[b][4 rs + q][oc] (the four lane groups' chains of the MFMA B operand).  One block per
+// chunk, 8 waves: waves 0..3 cover output channels 0..15, waves 4..7 channels 16..31 (round 6: before, one block per
+// (chunk, channel half) - both blocks fetched the chunk's frames, 29 of the launch's 110 MB).  Wave w owns kh = 2 (w % 4),
+// 2 (w % 4) + 1: lane row rho = (kh low bit, h, c), tile t = kw - 4 h, so one LDS dword (pixels 4 ow + 4 h .. + 3 of image
+// row 4 oh + kh) feeds the lane's four MFMAs of a step.  Per sample the frames (row layout, slot stride kC1WgSlotDw) and
+// dz1 (all 32 channels) sit in LDS (79,488 B) while the next sample's are in flight in registers.
+constexpr int kC1DzChunks = 400 * 32 / 4;   // 3,200 uint4 of one sample's dz1
+// frame slot stride of the weight gradient's image: 1,768 = 8 mod 32 dwords puts the four slots of a step's 32-lane half
+// (lane l % 4) on distinct banks (1,776 = 16 mod 32, the forward's, pairs slots 0 / 2 and 1 / 3: 2-way)
+constexpr int kC1WgSlotDw = 1768;
+constexpr int kC1WgradThreads = 512;
+constexpr int kC1WgradPf = (kC1Chunks + kC1DzChunks + kC1WgradThreads - 1) / kC1WgradThreads;   // 10 uint4 per thread
+constexpr size_t kC1WgradLds = (size_t)4 * kC1WgSlotDw * 4 + (size_t)400 * 32 * 4;          // 79,488 B
+__host__ __device__ constexpr int c1_wgrad_blocks(int nz) { return nz; }
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
                                                                        float* slab, int skip) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1776] dwords, then dz [400][16] f32
-  float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1SlotDw);
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1768] dwords, then dz [400][32] f32
+  float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1WgSlotDw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.x % nz, hh = blockIdx.x / nz;
+  const int z = blockIdx.x, hh = wave >> 2, wq = wave & 3;
   const int g = lane >> 4, l15 = lane & 15;
   const int b0 = z * QLX_F32_WGRAD_CHUNK_CONV1;
   const int nb = min(QLX_F32_WGRAD_CHUNK_CONV1, B - b0);
-  // this lane's A row rho = l15: kh = 2 w + rho / 8, h = (rho / 4) % 2, c = rho % 4; dword of (x = 4 oh + kh, y / 4 = ow + h)
-  const int ao = (l15 & 3) * kC1SlotDw + (2 * wave + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
-  // (the next sample's frames + dz1 in flight in registers; two samples ahead in two register sets measured slower: 43.3 ->
-  // 45.2 us)
-  uint4 pf[14];
-  auto prefetch = [&](int b, uint4 (&pf)[14]) {
+  // this lane's A row rho = l15: kh = 2 wq + rho / 8, h = (rho / 4) % 2, c = rho % 4; dword of (x = 4 oh + kh, y / 4 = ow + h)
+  const int ao = (l15 & 3) * kC1WgSlotDw + (2 * wq + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
+  const int bo = hh * 16 + l15;   // the lane's dz1 column
+  uint4 pf[kC1WgradPf];
+  auto prefetch = [&](int b, uint4 (&pf)[kC1WgradPf]) {
     const C1Ptrs f = c1_ptrs(table, b);
     const uint64_t zp = (uint64_t)(gbyte*)q32_zero4;
-    const uint64_t dzb = (uint64_t)(dz1 + (size_t)b * 400 * 32 + hh * 16);
+    const uint64_t dzb = (uint64_t)(dz1 + (size_t)b * 400 * 32);
 #pragma unroll
-    for (int j = 0; j < 14; ++j) {   // one unconditional 16-byte load per j: a frame chunk, a dz1 chunk or the zero page
-      const int q = tid + 256 * j;
+    for (int j = 0; j < kC1WgradPf; ++j) {   // one unconditional 16-byte load per j: a frame chunk, a dz1 chunk or the zero page
+      const int q = tid + kC1WgradThreads * j;
       const bool isf = q < kC1Chunks, isd = !isf && q < kC1Chunks + kC1DzChunks;
       const int qf = isf ? q : 0, slot = qf / 441, pos = qf - slot * 441;
-      const int e = isd ? q - kC1Chunks : 0, r = e >> 2, part = e & 3;
+      const int e = isd ? q - kC1Chunks : 0;
       const uint64_t fp = (uint64_t)c1_slot(f, slot);
       const uint64_t fa = fp ? fp + (uint64_t)(pos * 16) : zp;
-      const uint64_t da = dzb + (uint64_t)((r * 32 + part * 4) * 4);
+      const uint64_t da = dzb + (uint64_t)e * 16;
       const u32x4v v = *(gu4*)(isf ? fa : (isd ? da : zp));
       pf[j] = uint4{v.x, v.y, v.z, v.w};
     }
   };
-  auto stage = [&](const uint4 (&pf)[14]) {
+  auto stage = [&](const uint4 (&pf)[kC1WgradPf]) {
 #pragma unroll
-    for (int j = 0; j < 14; ++j) {
-      const int q = tid + 256 * j;
-      if (q < kC1Chunks) c1_put(c1w, q, pf[j]);
-      else if (q < kC1Chunks + kC1DzChunks) *reinterpret_cast<uint4*>(dzs + (q - kC1Chunks) * 4) = pf[j];
+    for (int j = 0; j < kC1WgradPf; ++j) {
+      const int q = tid + kC1WgradThreads * j;
+      if (q < kC1Chunks) {
+        const int slot = q / 441, pos = q - slot * 441, bx = pos / 21, by = pos - bx * 21;
+        uint32_t* d = c1w + slot * kC1WgSlotDw + 4 * bx * 21 + by;
+        d[0] = pf[j].x;
+        d[21] = pf[j].y;
+        d[42] = pf[j].z;
+        d[63] = pf[j].w;
+      } else if (q < kC1Chunks + kC1DzChunks) {
+        *reinterpret_cast<uint4*>(dzs + (q - kC1Chunks) * 4) = pf[j];
+      }
     }
   };
   f32x4 acc[4];
@@ -2449,7 +2530,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
 #pragma unroll
       for (int j = 0; j < GS; ++j) {
         const int r = 4 * (grp * GS + j) + g, oh = r / 20, ow = r - oh * 20;
-        bv[j] = dzs[r * 16 + l15];
+        bv[j] = dzs[r * 32 + bo];
         px[j] = c1w[ao + 84 * oh + ow];
       }
     };
@@ -2463,7 +2544,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
         if (nz[j])
 #pragma unroll
           for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px[j], t), bv[j], acc[t], 0, 0, 0);
-        bsum = __fadd_rn(bsum, bv[j]);   // (every wave; wave 0's is stored)
+        bsum = __fadd_rn(bsum, bv[j]);   // (every wave; wave wq = 0's is stored)
       }
     };
     rd(0, bA, xA);
@@ -2475,17 +2556,16 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
     }
   }
   float* out = slab + (size_t)z * 257 * 32;
-  const int oc = hh * 16 + l15;
-  if (wave == 0) {   // ((C0 + C1) + C2) + C3 in row 0
+  if (wq == 0) {   // ((C0 + C1) + C2) + C3 in row 256
     const float c1 = __shfl(bsum, lane + 16), c2 = __shfl(bsum, lane + 32), c3 = __shfl(bsum, lane + 48);
-    if (g == 0) out[256 * 32 + oc] = __fadd_rn(__fadd_rn(__fadd_rn(bsum, c1), c2), c3);
+    if (g == 0) out[256 * 32 + bo] = __fadd_rn(__fadd_rn(__fadd_rn(bsum, c1), c2), c3);
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // output row rho = 4 g + i of tile t -> HWIO (kh, kw = 4 h + t, c)
-      const int rho = 4 * g + i, kh = 2 * wave + (rho >> 3), kw = 4 * ((rho >> 2) & 1) + t, c = rho & 3;
-      out[(size_t)((kh * 8 + kw) * 4 + c) * 32 + oc] = acc[t][i];
+      const int rho = 4 * g + i, kh = 2 * wq + (rho >> 3), kw = 4 * ((rho >> 2) & 1) + t, c = rho & 3;
+      out[(size_t)((kh * 8 + kw) * 4 + c) * 32 + bo] = acc[t][i];
     }
 }
 
