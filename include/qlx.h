@@ -52,8 +52,8 @@ extern "C" {
 /* the same net with bf16 MFMA operands, fp32 accumulation and fp32 master weights (the labelled fast path) */
 #define QLX_ARCH_NATURE_DQN_BF16 2
 /* fp32 weight gradients of the conv layers: per-chunk fmaf chains over this many samples, chunks summed in order */
-#ifndef QLX_F32_WGRAD_CHUNK_CONV1   /* (overridable only for A/B timing builds; the oracle follows 4) */
-#define QLX_F32_WGRAD_CHUNK_CONV1 4
+#ifndef QLX_F32_WGRAD_CHUNK_CONV1   /* (overridable only for A/B timing builds; the oracle follows 2) */
+#define QLX_F32_WGRAD_CHUNK_CONV1 2   /* round 6: 4 -> 2 (twice the conv1 weight-gradient blocks: 36.2 -> 31.1 us at B = 1024) */
 #endif
 #define QLX_F32_WGRAD_CHUNK_CONV2 16
 #define QLX_F32_WGRAD_CHUNK_CONV3 16

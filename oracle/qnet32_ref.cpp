@@ -38,7 +38,7 @@
 namespace orc {
 
 // chunk sizes of the conv weight-gradient partials (include/qlx.h QLX_F32_WGRAD_CHUNK_CONV*; tests check equality)
-constexpr int kSC1 = 4, kSC2 = 16, kSC3 = 16;
+constexpr int kSC1 = 2, kSC2 = 16, kSC3 = 16;   // (round 6: conv1 4 -> 2)
 constexpr int kNormSeg = 2048;
 
 static inline float fma32(float a, float b, float c) { return std::fmaf(a, b, c); }

@@ -257,7 +257,8 @@ struct qlx_learner {
   ncclComm_t comm = nullptr;
   hipStream_t comm_stream = nullptr;   // the communicator's collectives (bucketed gradient all-reduce)
   bool dp_overlap = true;              // QLX_DP_OVERLAP=0: one whole-gradient all-reduce after the backward
-  bool dp_fold = false;                // QLX_DP_FOLD=1: fp32 dense norm partials in the conv backward's reduction launch
+  bool dp_fold = true;                 // fp32 dense norm partials in the conv backward's reduction launch (QLX_DP_FOLD=0:
+                                       // a launch of their own on the communicator stream)
   hipEvent_t ev_dense = nullptr, ev_reduced = nullptr;
   int world = 1, rank = 0;
   // global solved() over ranks: per vector step, {sum running_reward, sum has_history, sum episodes} (f64) and {min
@@ -416,9 +417,9 @@ static void learner_update(qlx_learner* L, uint32_t u_local) {
                                            ncclFloat, ncclSum, L->comm, L->comm_stream);
       QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     }
-    // fp32: the dense variables' clip-norm partials of the reduced bucket follow it on the communicator stream (they read
-    // the dense gradient only), or (QLX_DP_FOLD=1) ride in the conv backward's reduction launch, which then waits for this
-    // all-reduce
+    // fp32: the dense variables' clip-norm partials of the reduced bucket ride in the conv backward's reduction launch,
+    // which waits for this all-reduce (round 6: dp_single_rank 0.963 -> 0.967 of the plain path), or (QLX_DP_FOLD=0) follow
+    // it on the communicator stream in a launch of their own
     if (on->f32 && !L->dp_fold) model_norms(on, L->comm_stream, scale);
     QLX_HIP(hipEventRecord(L->ev_reduced, L->comm_stream));
     if (on->f32 && L->dp_fold) model_backward_conv(on, tab_s, (int)B, s, false, L->ev_reduced, scale);
@@ -1030,20 +1031,13 @@ int32_t qlx_learner_dist_init(qlx_learner* L, int32_t world, int32_t rank, const
     std::memcpy(&id, uid, 128);
     const ncclResult_t r = ncclCommInitRank(&L->comm, world, id, rank);
     QLX_CHECK(r == ncclSuccess, QLX_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    // QLX_COMM_PRIO=1: the communicator stream at the device's highest priority, so the dense bucket's all-reduce (and its
-    // norm partials) get CUs between the conv backward's blocks instead of after them
-    const char* cp = std::getenv("QLX_COMM_PRIO");
-    if (cp && cp[0] == '1') {
-      int lo = 0, hi = 0;
-      QLX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      QLX_HIP(hipStreamCreateWithPriority(&L->comm_stream, hipStreamNonBlocking, hi));
-    } else {
-      QLX_HIP(hipStreamCreateWithFlags(&L->comm_stream, hipStreamNonBlocking));
-    }
+    // (measured and not kept, round 6: the communicator stream at the device's highest priority - dp_single_rank 0.96 ->
+    // 0.41 of the plain path)
+    QLX_HIP(hipStreamCreateWithFlags(&L->comm_stream, hipStreamNonBlocking));
     const char* ov = std::getenv("QLX_DP_OVERLAP");
     L->dp_overlap = !(ov && ov[0] == '0');
     const char* fo = std::getenv("QLX_DP_FOLD");
-    L->dp_fold = fo && fo[0] == '1';
+    L->dp_fold = !(fo && fo[0] == '0');
     for (hipEvent_t* e : {&L->ev_dense, &L->ev_reduced}) QLX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     L->world = world;
     L->rank = rank;

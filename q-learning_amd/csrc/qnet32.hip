@@ -242,7 +242,7 @@ __device__ __forceinline__ float norm32_lane(const float* gall, const int64_t* o
 // loads in flight each); the group sums meet in LDS and the slice's wave 0 chains them in q order.  (One slice per block
 // left 12 of 16 waves idle at 64 chunks - conv2 / conv3 at B = 1024 - and held the CUs' wave slots.)
 constexpr int kWGroup = 16;
-constexpr int kWGroupsMax = 128;   // chunks <= 2,048 (conv1 at the largest fp32 batch, 8,192)
+constexpr int kWGroupsMax = 256;   // chunks <= 4,096 (conv1 at the largest fp32 batch, 8,192, in chunks of 2)
 struct WRed {
   const float* slab[3];
   int nz[3];

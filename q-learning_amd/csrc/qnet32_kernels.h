@@ -2332,12 +2332,17 @@ __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t
         for (int kq = 0; kq < 16; ++kq) nz[kq] = (__builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0) | (skip == 0);   // wave-uniform, no branch
         if (j + 1 < nt) tile_dwords(j + 1, dn);
         f32x4 acc = zero4();
+#if QLX_C1_EXP != 2   // (timing experiments only: 2 = no MFMA, 1 = no a1 stores)
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq)
           if (nz[kq])
 #pragma unroll
             for (int kw = 0; kw < 4; ++kw) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(d[kq], kw), wf[kq * 4 + kw], acc, 0, 0, 0);
+#endif
         const int t = rp + 2 * j, r0 = (4 * (t / 5) + g) * 20 + 4 * (t % 5);   // rows (oh, ow .. ow + 3) of the patch
+#if QLX_C1_EXP == 1
+        if (acc[0] == 1234.5f)
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) a1[((size_t)b * 400 + r0 + i) * 32 + col] = relu(acc[i] + bias);
       }
@@ -2359,6 +2364,9 @@ __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t
 // CU runs two samples at a time and a B = 1,024 batch is two samples deep per block: a sample's frame fetch, its
 // 13-tile chains and its a1 stores follow each other.  One sample per block needs one frame buffer (28 KB) and no prefetch
 // registers, so 4 blocks share a CU and all of a CU's samples run at once (VGPRs held to 128 by the launch bound).
+#ifndef QLX_C1_EXP
+#define QLX_C1_EXP 0
+#endif
 #ifndef QLX_C1_ONE_MINW
 #define QLX_C1_ONE_MINW 4
 #endif

@@ -421,17 +421,19 @@ def test_learner_runs_many_steps_without_faults():
     assert np.isfinite(w).all()
 
 
-@pytest.mark.parametrize("prec", [0, 1], ids=["fp32", "bf16"])
+@pytest.mark.parametrize("prec,fold", [(0, "1"), (0, "0"), (1, "1")], ids=["fp32", "fp32_norms_launch", "bf16"])
 @pytest.mark.parametrize("overlap", ["1", "0"], ids=["two_buckets", "one_allreduce"])
-def test_data_parallel_path_single_rank_bit_identical(monkeypatch, overlap, prec):
+def test_data_parallel_path_single_rank_bit_identical(monkeypatch, overlap, prec, fold):
     """The data-parallel update path on a single-rank RCCL communicator equals the plain single-GPU path bit for bit, in
     both precisions and both DP schedules: QLX_DP_OVERLAP=1 (the default: dense gradient bucket all-reduced on the
-    communicator's stream while the conv backward runs, its clip-norm partials there, then the conv bucket, the update
-    tail after both) and QLX_DP_OVERLAP=0 (one whole-gradient all-reduce after the backward, then the tail): the stream
+    communicator's stream while the conv backward runs; fp32: its clip-norm partials in the conv backward's reduction launch
+    once it has landed, or with QLX_DP_FOLD=0 in a launch of their own on the communicator stream; then the conv bucket,
+    the update tail after both) and QLX_DP_OVERLAP=0 (one whole-gradient all-reduce after the backward, then the tail): the stream
     hand-offs order every read and write.  (At world 1 the tail's scale is exactly 1; scale != 1 is
     test_update_tail_scaled_gradient.)"""
     qlx = _qlx()
     monkeypatch.setenv("QLX_DP_OVERLAP", overlap)   # read by dist_init
+    monkeypatch.setenv("QLX_DP_FOLD", fold)         # fp32: dense norm partials in the reduction launch (1) or their own (0)
     p = dict(n_envs=64, batch_size=64, history_buffer_len=4000, update_after_actions=16, epsilon_pure_random_steps=1000,
              max_steps_per_episode=300, qnet_precision=prec)
     plain = qlx.SelfDrivingQLearner(qlx.Parameter(**p))
