@@ -580,7 +580,10 @@ static int c1_blocks(int n) { return std::max(std::min(n, 2 * num_cus()), (n + k
 #ifndef QLX_C1_ONE
 #define QLX_C1_ONE 1
 #endif
-static bool c1_one(int n) { return QLX_C1_ONE && n <= 2048; }
+static bool c1_one(int n) {
+  static const bool all = [] { const char* e = std::getenv("QLX_C1_ONE_ALL"); return e && e[0] == '1'; }();   // (A/B)
+  return QLX_C1_ONE && (n <= 2048 || all);
+}
 static int c1_grid(int n) { return c1_one(n) ? n : c1_blocks(n); }
 
 void f32_workspace(qlx_model* m, int B) {
@@ -770,8 +773,8 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       auto kern = big ? k_conv1_fwd32<1> : one ? k_conv1_fwd32<0, true> : k_conv1_fwd32<0>;
       QLX_CHECK((n + G - 1) / G <= (one ? 1 : kC1MaxIt), QLX_E_STATE, "conv1 forward: too many samples per block");
       const size_t frames = (one ? 1 : 2) * kC1Frames;
-      const size_t lds = frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8;   // frames, row masks, flags
-      set_lds_limit((const void*)kern, frames + 3 * kC1RmDw * 4 + (size_t)(one ? 1 : kC1MaxIt) * 6 * 8);
+      const size_t lds = frames + 3 * kC1RmDw * 4 + (size_t)((n + G - 1) / G) * 6 * 8 + 8;   // frames, row masks, flags, claim
+      set_lds_limit((const void*)kern, frames + 3 * kC1RmDw * 4 + (size_t)(one ? 1 : kC1MaxIt) * 6 * 8 + 8);
       hipExtLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, ea, eb, 0u, table + (size_t)c0 * 4, n,
                             p + voff(0), p + voff(1), w.fa1, c1_skip(m), L);
       QLX_HIP(hipGetLastError());

@@ -2119,6 +2119,9 @@ struct SideFc2 {
 // LDS frame layout (rows): slot c, image row x, dword y / 4 holds pixels (x, y .. y + 3) at dword c * 1776 + x * 21 + y / 4.
 // Rows of 21 dwords make 16 consecutive output positions (oh, ow) hit 16 consecutive banks (84 = 20 mod 64 dwords per
 // oh step), and the slot stride 1,776 = 48 mod 64 puts the four slots (the MFMA lane groups) on disjoint bank ranges.
+#ifndef QLX_C1_EXP
+#define QLX_C1_EXP 0   // (timing experiments of the conv1 forward only, scripts/build_variant.sh: 1 no a1 stores, 2 no MFMA, 3 no list claims)
+#endif
 constexpr int kC1SlotDw = 1776;                 // 84 rows x 21 dwords + 12 (bank skew)
 constexpr int kC1Frames = 4 * kC1SlotDw * 4;    // 28,416 B of one sample's frames in LDS
 constexpr int kC1Chunks = 4 * kFramePix / 16;   // 1,764 s2d uint4 chunks in HBM
@@ -2259,19 +2262,37 @@ __device__ __forceinline__ void c1_flags(const uint32_t* rm, unsigned long long*
   }
 }
 // cl: [iteration][3 waves][2]; the block's samples b0, b0 + G, .. (nit of them)
+// Called by every wave of the block (it holds a block barrier); waves 0..2 write.  One claim per layer and block: wave 0
+// claims the conv2 rows of waves 0 and 1 together and hands wave 1 its start through LDS (xch), wave 2 claims the conv3
+// rows (round 6: with one sample per block - k_conv1_fwd32 ONE - the claims doubled, and a claim per wave put 256 of them
+// on each region's conv2 counter).
 __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int nit, int b0, int G, const C1Lists& L, int wave,
-                                               int tid, int B) {
+                                               int tid, int B, unsigned long long* xch) {
   const int lane = tid & 63, R = wave < 2 ? 81 : 49, p = wave < 2 ? tid : tid - 128;
   int* rl = wave < 2 ? L.rl2 : L.rl3;
-  unsigned long long tot = 0;
-  for (int it = 0; it < nit; ++it)
-    tot += ((unsigned long long)__builtin_popcountll(cl[(it * 3 + wave) * 2]) << 32) |
-           (unsigned long long)__builtin_popcountll(cl[(it * 3 + wave) * 2 + 1]);
+  auto wave_tot = [&](int wv) {   // (non-background << 32 | background) rows of wave wv's share over the block's samples
+    unsigned long long t = 0;
+    for (int it = 0; it < nit; ++it)
+      t += ((unsigned long long)__builtin_popcountll(cl[(it * 3 + wv) * 2]) << 32) |
+           (unsigned long long)__builtin_popcountll(cl[(it * 3 + wv) * 2 + 1]);
+    return t;
+  };
   unsigned long long old = 0;
   const int slot = blockIdx.x % kListSlots, cap = wave < 2 ? L.cap2 : L.cap3;
   rl += slot * cap;
-  if (lane == 0)
+#if QLX_C1_EXP == 3   // (timing experiment: no claim - every block writes a fixed, overlapping range; wrong lists)
+  old = ((unsigned long long)((blockIdx.x / kListSlots) % 64) << 32) | (unsigned long long)((blockIdx.x / kListSlots) % 64);
+  __syncthreads();
+#else
+  if ((wave == 0 || wave == 2) && lane == 0) {
+    const unsigned long long tot = wave == 0 ? wave_tot(0) + wave_tot(1) : wave_tot(2);
     old = __hip_atomic_fetch_add(L.cnt + (slot * 2 + (wave < 2 ? 0 : 1)) * kCntStride, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) *xch = old;
+  }
+  __syncthreads();
+  if (wave == 1) old = *xch + wave_tot(0);   // wave 1's rows follow wave 0's in the claimed range
+#endif
+  if (wave >= 3) return;
   old = __shfl(old, 0);
   int on = (int)(old >> 32), og = (int)(uint32_t)old;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -2364,9 +2385,6 @@ __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t
 // CU runs two samples at a time and a B = 1,024 batch is two samples deep per block: a sample's frame fetch, its
 // 13-tile chains and its a1 stores follow each other.  One sample per block needs one frame buffer (28 KB) and no prefetch
 // registers, so 4 blocks share a CU and all of a CU's samples run at once (VGPRs held to 128 by the launch bound).
-#ifndef QLX_C1_EXP
-#define QLX_C1_EXP 0
-#endif
 #ifndef QLX_C1_ONE_MINW
 #define QLX_C1_ONE_MINW 4
 #endif
@@ -2416,7 +2434,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
     if (lists) {
       if (wave < 3) c1_flags(rm, cl + wave * 2, wave, tid);
       __syncthreads();
-      if (wave < 3) c1_lists_flush(cl, 1, blockIdx.x, gridDim.x, L, wave, tid, B);
+      c1_lists_flush(cl, 1, blockIdx.x, gridDim.x, L, wave, tid, B, cl + 6);
     }
     return;
   }
@@ -2446,7 +2464,10 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
     }
     __syncthreads();
   }
-  if (lists && wave < 3) c1_lists_flush(cl, (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x, blockIdx.x, gridDim.x, L, wave, tid, B);
+  if (lists) {
+    const int nit = (B - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    c1_lists_flush(cl, nit, blockIdx.x, gridDim.x, L, wave, tid, B, cl + nit * 6);
+  }
 }
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
