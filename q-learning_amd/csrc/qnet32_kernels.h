@@ -204,8 +204,11 @@ __device__ __forceinline__ int xcd_logical(int b, int G) {
 // conv2 / conv3 forward 61.5 / 46.1 -> 58.0 / 43.7 us, the fc1 / conv2 backward pairs 73.3 / 117.1 -> 69.5 / 112.9 us,
 // the chunk-size conv3 forward 281.5 -> 272 us (strategy 0 for all: 1-4 % slower than 1 on these); the fc1 forward runs
 // slower with strategy 1 and best with 0 (PFc1FwdT); the conv1 kernels' MFMA loops gain nothing from either.
+#ifndef QLX_IGLP_DEFAULT
+#define QLX_IGLP_DEFAULT 1   // (A/B builds: the strategy of the policies without an IGLP member)
+#endif
 template <class P, class = void>
-struct IglpOf : std::integral_constant<int, 1> {};
+struct IglpOf : std::integral_constant<int, QLX_IGLP_DEFAULT> {};
 template <class P>
 struct IglpOf<P, std::void_t<decltype(P::IGLP)>> : std::integral_constant<int, P::IGLP> {};
 

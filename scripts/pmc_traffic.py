@@ -16,21 +16,22 @@ import sys
 # bench.py profiler scope -> substring of the demangled kernel name (rocprofv3 Kernel_Name)
 SCOPES = {
     "fp32": {
-        "f32_conv1_fwd": "k_conv1_fwd32<0>",
-        "f32_conv1_fwd_big": "k_conv1_fwd32<1>",
+        "f32_conv1_fwd": "k_conv1_fwd32<0, true>",   # one sample per block (round 6)
+        "f32_conv1_fwd_big": "k_conv1_fwd32<1, false>",
         # row-list forwards (non-background rows + the background rows' side blocks)
-        "f32_conv2_fwd": "k_gemm32_side<qlx::q32::PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, 64, 32,",
+        # (the training-batch and the chunk-batch conv2 forward are one instantiation (64 x 64 list tiles): one entry, the
+        # average over both kinds of dispatch)
         "f32_conv2_fwd_big": "k_gemm32_side<qlx::q32::PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, 64, 64,",
-        "f32_conv3_fwd": "k_gemm32_side<qlx::q32::PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, 64, 32,",
+        "f32_conv3_fwd": "k_gemm32_side<qlx::q32::PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, 32, 64,",
         "f32_conv3_fwd_big": "k_gemm32_side<qlx::q32::PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, 64, 64,",
         "f32_fc1_fwd": "k_gemm32<qlx::q32::PFc1FwdT<32, 32, 2, 2,",
-        "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<64, 64, 2, 2,",
+        "f32_fc1_fwd_big": "k_gemm32<qlx::q32::PFc1FwdT<64, 128, 2, 2,",
         "f32_fc1_bwd": "k_gemm32_pair<qlx::q32::PFc1WgradT",
         "f32_conv3_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<9, 9",
         "f32_conv2_bwd": "k_gemm32_pair<qlx::q32::PConvWgrad<20, 20",
         "f32_conv1_wgrad": "k_conv1_wgrad32",
         "f32_norms": "k_wreduce32",
-        "f32_head": "k_head32<3>",
+        "f32_head": "k_head32<3, 4>",
         "f32_wgrad_reduce": "k_wreduce32",
         "f32_adam": "k_update32",   # update schedule 2 (default): every variable's clip_by_norm + Adam in one launch
     },
