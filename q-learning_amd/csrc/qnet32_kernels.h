@@ -2492,7 +2492,7 @@ constexpr size_t kC1WgradLds = (size_t)4 * kC1WgSlotDw * 4 + (size_t)400 * 32 * 
 __host__ __device__ constexpr int c1_wgrad_blocks(int nz) { return nz; }
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
                                                                        float* slab, int skip) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1768] dwords, then dz [400][32] f32
+  extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1768] dwords, then dz [2 halves][400][16] f32
   float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1WgSlotDw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2503,6 +2503,9 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
   // this lane's A row rho = l15: kh = 2 wq + rho / 8, h = (rho / 4) % 2, c = rho % 4; dword of (x = 4 oh + kh, y / 4 = ow + h)
   const int ao = (l15 & 3) * kC1WgSlotDw + (2 * wq + (l15 >> 3)) * 21 + ((l15 >> 2) & 1);
   const int bo = hh * 16 + l15;   // the lane's dz1 column
+  // dz1 in LDS as two [400][16] channel halves: a step's reads (rows r, r + 1 on lane groups g, g + 1; 16 channels each) are
+  // 32 consecutive dwords - conflict-free (a [400][32] image puts both rows on the same 16 banks: 2-way)
+
   uint4 pf[kC1WgradPf];
   auto prefetch = [&](int b, uint4 (&pf)[kC1WgradPf]) {
     const C1Ptrs f = c1_ptrs(table, b);
@@ -2533,7 +2536,8 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
         d[42] = pf[j].z;
         d[63] = pf[j].w;
       } else if (q < kC1Chunks + kC1DzChunks) {
-        *reinterpret_cast<uint4*>(dzs + (q - kC1Chunks) * 4) = pf[j];
+        const int e = q - kC1Chunks, r = e >> 3, part = e & 7;   // dz1[r][4 part .. 4 part + 3]
+        *reinterpret_cast<uint4*>(dzs + (part >> 2) * 6400 + r * 16 + (part & 3) * 4) = pf[j];
       }
     }
   };
@@ -2562,7 +2566,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
 #pragma unroll
       for (int j = 0; j < GS; ++j) {
         const int r = 4 * (grp * GS + j) + g, oh = r / 20, ow = r - oh * 20;
-        bv[j] = dzs[r * 32 + bo];
+        bv[j] = dzs[hh * 6400 + r * 16 + l15];
         px[j] = c1w[ao + 84 * oh + ow];
       }
     };
