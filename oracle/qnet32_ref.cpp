@@ -9,6 +9,7 @@
 // autograd of the Keras graph (activations, Q, loss, all ten gradients, norms, w / m / v after two Adam steps; B 4..256)
 // and against the double-accumulating restatement qnet_ref.cpp at B = 1024.
 //   conv1 .. conv3  z = sum over (kh, kw, c) of in[S oh+kh][S ow+kw][c] W[kh][kw][c][oc]          (HWIO order)
+//                   conv2 / conv3 (round 6): z = C0 + C1, Ch = chain over the half h of the flattened (kh, kw, c)
 //   dense 3136->512 z = C0 + C1, Ch = chain over k in [1568 h, 1568 h + 1568) ascending (Flatten order h, w, c; round 6 -
 //                   before: one chain over all k)
 //   dense 512->3    z = ((C0 + C1) + C2) + C3, Cw = chain over k in [128 w, 128 w + 128) ascending
@@ -68,23 +69,34 @@ static void conv1_fwd(const uint8_t* x, int B, const float* W, const float* bias
 struct Cfg { int H, W, C, K, S, OH, OW, OC; };
 static const Cfg kC2 = {20, 20, 32, 4, 2, 9, 9, 64}, kC3 = {9, 9, 64, 3, 1, 7, 7, 64};
 
+// conv2 / conv3 forward: z = C0 + C1, Ch = chain over the half h of k = (kh, kw, c) (flattened HWIO order; round 6)
+constexpr int kConvFwdChains = 2;   // (qnet32_kernels.h kConvFwdChains)
 static void conv_fwd(const Cfg& c, const float* in, int B, const float* W, const float* bias, float* out) {
+  const int K = c.K * c.K * c.C, half = K / kConvFwdChains;
 #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b)
     for (int oh = 0; oh < c.OH; ++oh)
       for (int ow = 0; ow < c.OW; ++ow) {
-        float acc[64];
+        float acc[64], first[64];
         for (int oc = 0; oc < c.OC; ++oc) acc[oc] = 0.0f;
         for (int kh = 0; kh < c.K; ++kh)
           for (int kw = 0; kw < c.K; ++kw) {
             const float* src = in + (((size_t)b * c.H + oh * c.S + kh) * c.W + ow * c.S + kw) * c.C;
             for (int ch = 0; ch < c.C; ++ch) {
+              if (kConvFwdChains == 2 && (kh * c.K + kw) * c.C + ch == half) {   // the second chain starts here
+                for (int oc = 0; oc < c.OC; ++oc) {
+                  first[oc] = acc[oc];
+                  acc[oc] = 0.0f;
+                }
+              }
               const float v = src[ch];
               if (v == 0.0f) continue;
               const float* wr = W + ((size_t)(kh * c.K + kw) * c.C + ch) * c.OC;
               for (int oc = 0; oc < c.OC; ++oc) acc[oc] = fma32(v, wr[oc], acc[oc]);
             }
           }
+        if (kConvFwdChains == 2)
+          for (int oc = 0; oc < c.OC; ++oc) acc[oc] = first[oc] + acc[oc];
         float* o = out + (((size_t)b * c.OH + oh) * c.OW + ow) * c.OC;
         for (int oc = 0; oc < c.OC; ++oc) o[oc] = relu(acc[oc] + bias[oc]);
       }

@@ -580,6 +580,14 @@ static int c1_blocks(int n) { return std::max(std::min(n, 2 * num_cus()), (n + k
 #ifndef QLX_C1_ONE
 #define QLX_C1_ONE 1
 #endif
+#ifndef QLX_C2_FWD_KS
+#define QLX_C2_FWD_KS 2   // training-batch conv2 / conv3 list forwards: chains in wave groups (2) or in turn (1)
+#endif
+#ifndef QLX_C3_FWD_KS
+#define QLX_C3_FWD_KS 2
+#endif
+constexpr int kC2FwdKs = QLX_C2_FWD_KS <= kConvFwdChains ? QLX_C2_FWD_KS : 1;
+constexpr int kC3FwdKs = QLX_C3_FWD_KS <= kConvFwdChains ? QLX_C3_FWD_KS : 1;
 static bool c1_one(int n) {
   static const bool all = [] { const char* e = std::getenv("QLX_C1_ONE_ALL"); return e && e[0] == '1'; }();   // (A/B)
   return QLX_C1_ONE && (n <= 2048 || all);
@@ -787,14 +795,15 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       float* c2 = w.fbgc + 32;
       float* c3 = w.fbgc + 96;
       const BgRows2 s23{{nw, w.frl2, cnt, cap2, c2, w.fa2}, {nw, w.frl3, cnt + kCntStride, cap3, c3, w.fa3}};
-      using PC2 = PConv2FwdL<16, 64, 1, 4>;
-      using PC3 = PConv3FwdL<16, 64, 1, 4>;
-      const ConstRows<PC2, PC3> cr{PC2{Grid{1, 1, 1}, w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, c2},
-                                   PC3{Grid{1, 1, 1}, w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride, c2, c3}};
       auto lgrid = [&](int cap, int BM, int BN) { return Grid{1 + kListSlots * ((cap + BM - 1) / BM), 64 / BN, 1}; };
       auto run = [&](auto t2, auto t3, const char* sc2, const char* sc3) {
         using P2 = decltype(t2);
         using P3 = decltype(t3);
+        // the constant rows' chains in the conv2 launch's blocks: the same K split form as its list tiles (block size)
+        using PC2 = PConv2FwdL<16, 64, 1, 4, P2::KSPLIT>;
+        using PC3 = PConv3FwdL<16, 64, 1, 4, P2::KSPLIT>;
+        const ConstRows<PC2, PC3> cr{PC2{Grid{1, 1, 1}, w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, c2},
+                                     PC3{Grid{1, 1, 1}, w.fa2, p + voff(4), p + voff(5), w.fa3, w.frl3, cap3, cnt + kCntStride, c2, c3}};
         // (the list tiles start at row tile 1; row tile 0, the constant row, is ConstRows' work: its blocks return)
         P2 p2{lgrid(cap2, P2::BM, P2::BN), w.fa1, p + voff(2), p + voff(3), w.fa2, w.frl2, cap2, cnt, w.fbgc, nullptr};
         p2.pre_batched = big;
@@ -811,7 +820,8 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
       } else {
         // (on the stream core, in place: conv2 64 x 64 24.3 us against 27.9 us for 64 x 32 and 28.7 for 32 x 64; conv3 32 x 64
         // 27.6 us against 28.5 / 29.8 for 64 x 32 / 64 x 64 - gpurun_out/w10)
-        run(PConv2FwdL<64, 64, 2, 2>{}, PConv3FwdL<32, 64, 2, 2>{}, "f32_conv2_fwd", "f32_conv3_fwd");
+        // round 6: the two k chains (§6) in two wave groups per block (KSPLIT): twice the waves for the same tiles
+        run(PConv2FwdL<64, 64, 2, 2, kC2FwdKs>{}, PConv3FwdL<32, 64, 2, 2, kC3FwdKs>{}, "f32_conv2_fwd", "f32_conv3_fwd");
         model_dense_join(m, s);
         launch(m, PFc1FwdS{grid(n, PFc1FwdS::BM, 512, PFc1FwdS::BN, 1), w.fa3, p + voff(6), p + voff(7), w.fa4 + (size_t)c0 * 512, n}, "f32_fc1_fwd",
                2.0 * n * 3136 * 512, s);

@@ -143,6 +143,11 @@ template <class P>
 struct KSplitOf<P, std::void_t<decltype(P::KSPLIT)>> : std::integral_constant<int, P::KSPLIT> {};
 template <class P>
 constexpr int threads_of() { return P::WM * P::WN * 64 * KSplitOf<P>::value; }
+// K-split chains of a policy run one after another in the same waves: its member KSEQ when it has one, else 1
+template <class P, class = void>
+struct KSeqOf : std::integral_constant<int, 1> {};
+template <class P>
+struct KSeqOf<P, std::void_t<decltype(P::KSEQ)>> : std::integral_constant<int, P::KSEQ> {};
 
 // MFMA shape of a policy: its member MF when it has one, else 16
 template <class P, class = void>
@@ -290,6 +295,9 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     if (!p.active(z, row0)) return;
   }
   const int ns = p.nslabs(z) / G, s_base = kg * ns;   // this group's slabs: s_base + [0, ns)
+  constexpr int Q = KSeqOf<P>::value;   // (KSEQ: see gemm_body_s)
+  static_assert(Q == 1 || (Q == 2 && G == 1 && MF == 16 && !P::BIAS), "sequential K split: two chains, 16x16x4, no bias");
+  const int s_half = Q > 1 ? ns / 2 : -1;
   typename ACtxOf<P>::type actx{};
   if constexpr (HasACtx<P>::value) actx = p.a_ctx(z, row0, tid);
   lds += kg * GROUP_LDS;
@@ -350,6 +358,7 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < MF * MF / 64; ++e) acc[i][j][e] = 0.0f;
+  Acc first[Q > 1 ? TM : 1][Q > 1 ? TN : 1];   // KSEQ: the finished first chain
   // bias (BIAS policies, row-tile 0): column sums of B as KG interleaved chains - lane group q of the wave's B fragments
   // chains the k = q mod KG rows - combined in group order at the end
   float bsum[TN];
@@ -359,6 +368,17 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
   auto compute = [&](int s) {
     const float* a = (s & 1) ? As1 : As0;
     const float* b = (s & 1) ? Bs1 : Bs0;
+    if constexpr (Q > 1) {
+      if (s == s_half) {   // (wave-uniform) the first chain is done: keep it, start the second from zero
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            first[i][j] = acc[i][j];
+            acc[i][j] = zero4();
+          }
+      }
+    }
     if constexpr (IglpOf<P>::value >= 0) __builtin_amdgcn_iglp_opt(IglpOf<P>::value);
     if constexpr (MF == 16) {
       slab_mfma16<OA, OB, TM, TN, P::BIAS>(a, b, wm, wn, lane, acc, bsum, do_bias);
@@ -390,14 +410,16 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
     store(s + 1, xa, xb);   // unconditional, as in gemm_body_s (past the last slab: the idle buffer, never read)
     lds_barrier();
   };
-  constexpr bool PRE = HasEpiPre<P>::value && MF == 16 && G == 1;
+  constexpr bool PRE = HasEpiPre<P>::value && MF == 16;
   typename PreOf<P>::type pre[TM][TN];
   if constexpr (PRE) {
+    if (kg == 0) {   // (K groups: group 0 runs the epilogue)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+        for (int j = 0; j < TN; ++j)
+          pre[i][j] = p.epi_pre(z, row0 + (wm * TM + i) * 16 + (lane >> 4) * 4, col0 + (wn * TN + j) * 16 + (lane & 15));
+    }
   }
   if (ns > 0) {
     load(0, ra1, rb1);
@@ -410,6 +432,14 @@ __device__ __forceinline__ void gemm_body(const P& p, int lb, float* lds) {
       iter(s + 1, ra1, rb1, ra0, rb0);
     }
     if (s < ns) iter(s, ra0, rb0, ra1, rb1);
+  }
+  if constexpr (Q > 1) {   // C0 + C1
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = __fadd_rn(ns > s_half ? first[i][j][e] : acc[i][j][e], ns > s_half ? acc[i][j][e] : 0.0f);
   }
   if constexpr (G > 1) {   // groups 1 .. G - 1 hand their accumulators to group 0 through their own LDS (free now)
     constexpr int E = MF * MF / 64;
@@ -836,12 +866,6 @@ template <class P>
 struct HasStreams<P, std::void_t<typename P::Streams>> : std::bool_constant<!std::is_void_v<typename P::Streams>> {};
 #endif
 
-// K-split chains of a policy run one after another in the same waves: its member KSEQ when it has one, else 1
-template <class P, class = void>
-struct KSeqOf : std::integral_constant<int, 1> {};
-template <class P>
-struct KSeqOf<P, std::void_t<decltype(P::KSEQ)>> : std::integral_constant<int, P::KSEQ> {};
-
 // K split (round 6, policies with KSPLIT = G > 1 or KSEQ = Q > 1): the reduction is G (Q) chains over consecutive equal
 // slab ranges, combined ((C0 + C1) + ..) before the epilogue - the same value either way: KSPLIT runs the chains in G
 // wave groups of the block at once (group 0 sums them through LDS), KSEQ one after another in the same waves (the
@@ -1036,10 +1060,16 @@ template <class P, class = void>
 struct MinWOf : std::integral_constant<int, 1> {};
 template <class P>
 struct MinWOf<P, std::void_t<decltype(P::MINW)>> : std::integral_constant<int, P::MINW> {};
+template <class P, class = void>
+struct HasMinW : std::false_type {};
+template <class P>
+struct HasMinW<P, std::void_t<decltype(P::MINW)>> : std::true_type {};
+// the policies' own floors when either declares one (the larger), else QLX_PAIR_MINW
 template <class P1, class P2>
 constexpr int pair_minw() {
-  return QLX_PAIR_MINW > MinWOf<P1>::value ? (QLX_PAIR_MINW > MinWOf<P2>::value ? QLX_PAIR_MINW : MinWOf<P2>::value)
-                                           : (MinWOf<P1>::value > MinWOf<P2>::value ? MinWOf<P1>::value : MinWOf<P2>::value);
+  return (HasMinW<P1>::value || HasMinW<P2>::value)
+             ? (MinWOf<P1>::value > MinWOf<P2>::value ? MinWOf<P1>::value : MinWOf<P2>::value)
+             : QLX_PAIR_MINW;
 }
 template <class P1, class P2, class S, class T>
 __global__ __launch_bounds__(256, (pair_minw<P1, P2>())) void k_gemm32_pair(const P1 p1, const P2 p2, const S side, const T tail) {
@@ -1077,11 +1107,21 @@ struct NoSide {
 //   conv dgrad      k = (kh, kw, oc) over the valid taps                                   fc1 dgrad   k = n
 //   weight grads    r = (b, oh, ow) ascending inside a sample chunk; fc1 / fc2 over b ascending, no chunks
 
+// conv2 / conv3 forward chains: z = C0 + C1, Ch = chain over the k = (kh, kw, c) half h (conv2: taps
+// 0..7 / 8..15; conv3: k < 288 / the rest), so that the training-batch list launch can run the two chains in two wave groups
+// of a block (KSPLIT); the chunk-batch launches run them one after the other (KSEQ)
+#ifndef QLX_CONV_FWD_CHAINS
+#define QLX_CONV_FWD_CHAINS 2   // (A/B timing builds only: 1 = the round-5 single chain, which the oracle no longer follows)
+#endif
+constexpr int kConvFwdChains = QLX_CONV_FWD_CHAINS;
 // conv2 / conv3 forward on fp32 NHWC input: out = relu(conv + bias); slab s: tap = 32 s / C, c0 = 32 s % C
 template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
           int MF_ = 16>
 struct PConvFwd {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
+  static constexpr int KSEQ = kConvFwdChains;
+  static constexpr int MINW = 3;   // (pair launches of the dense forward: the finished first chain's registers, no spill)
+  static_assert(MF_ == 16, "conv forward chains: 16x16x4");
   static constexpr bool LOAD_FENCE = !(H == 20 && BN_ == 64);   // the chunk-size conv2 forward runs without it
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false;
   Grid g;
@@ -1144,15 +1184,17 @@ using PConv3FwdR = RowShift<PConvFwd<9, 9, 64, 3, 1, 7, 7, 64, 16, 64, 1, 4>>;
 // background in the layer below (list entry bits 20..28, written by conv1) read cx = that layer's constant row instead of
 // `in` (those rows are written by this launch's side blocks).
 template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
-          bool SEL = false>
+          bool SEL = false, int KS_ = 1>
 struct PConvFwdL {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int KSPLIT = KS_, KSEQ = kConvFwdChains / KS_;   // the two chains in wave groups (KS_ = 2) or in turn
+  static_assert(KSPLIT * KSEQ == kConvFwdChains, "conv forward: the chain definition");
   static constexpr bool A_KMAJ = false, B_KMAJ = true, BIAS = false, RAW_ORDER = true;
   // (with the slab loop's wait fixed, round 5: the fence on for conv2 too - the 8,192-sample pass 131 -> 127 us)
   static constexpr bool LOAD_FENCE = true;
   static constexpr int R = OH * OW;
   using OA = Opnd<BM, false, 16>;
-  static constexpr int T = WM * WN * 64, NA = (OA::F4 + T - 1) / T;
+  static constexpr int T = WM * WN * 64, NA = (OA::F4 + T - 1) / T;   // (T: threads of one K group)
   Grid g;            // tiles_m = 1 + kListSlots * tiles per region
   const float* in;
   const float* w;    // [KS][KS][C][OC]
@@ -1325,10 +1367,10 @@ struct PConvFwdL {
     return st;
   }
 };
-template <int BM, int BN, int WM, int WN>
-using PConv2FwdL = PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, BM, BN, WM, WN, false>;
-template <int BM, int BN, int WM, int WN>
-using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN, true>;
+template <int BM, int BN, int WM, int WN, int KS_ = 1>
+using PConv2FwdL = PConvFwdL<20, 20, 32, 4, 2, 9, 9, 64, BM, BN, WM, WN, false, KS_>;
+template <int BM, int BN, int WM, int WN, int KS_ = 1>
+using PConv3FwdL = PConvFwdL<9, 9, 64, 3, 1, 7, 7, 64, BM, BN, WM, WN, true, KS_>;
 
 // The constant rows as the first block of the conv2 launch: the conv2 constant row (input relu(0 + b0) -> c2), then, from
 // c2, the conv3 constant row (-> c3), each as the constant-row tile of a 16 x 64 list policy (4 waves x 16 channels, the
@@ -1348,8 +1390,8 @@ struct ConstRows {
   }
 };
 
-// Leading blocks of a list launch (256 threads): the layer below's background rows get its constant row c_in, 16 lanes
-// (256 bytes) per row, 8 list entries per lane loaded together (the back ends of the list regions).
+// Leading blocks of a list launch (its block size: 256 or 512 threads): the layer below's background rows get its constant row
+// c_in, 16 lanes (256 bytes) per row, 8 list entries per lane loaded together (the back ends of the list regions).
 struct BgRows {
   static constexpr size_t LDS = 64 * sizeof(float);
   static constexpr int U = 8;
@@ -1361,7 +1403,7 @@ struct BgRows {
   float* out;              // [rows][64]
   __host__ __device__ int blocks() const { return nblk; }
   __device__ void run(int blk, float* lds) const {
-    const int tid = threadIdx.x, q = tid & 15;
+    const int tid = threadIdx.x, q = tid & 15, RB = (int)blockDim.x >> 4;   // RB rows per pass (the launch's block size)
     const f32x4 v = ld4(c_in + 4 * q);
     for (int x = 0; x < kListSlots; ++x) {
       const int nbg = (int)(uint32_t)cnt[x * 2 * kCntStride];
@@ -1370,15 +1412,15 @@ struct BgRows {
         printf("LISTCHK bgrows region %d nbg %d non %d cap %d\n", x, nbg, (int)(cnt[x * 2 * kCntStride] >> 32), cap);
 #endif
       const int* back = list + (size_t)(x + 1) * cap - 1;
-      for (int i0 = blk * 16 * U + (tid >> 4); i0 < nbg; i0 += nblk * 16 * U) {
+      for (int i0 = blk * RB * U + (tid >> 4); i0 < nbg; i0 += nblk * RB * U) {
         int e[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) e[u] = i0 + 16 * u < nbg ? back[-(i0 + 16 * u)] : -1;
+        for (int u = 0; u < U; ++u) e[u] = i0 + RB * u < nbg ? back[-(i0 + RB * u)] : -1;
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (e[u] >= 0) {
 #ifdef QLX_LIST_CHECK
-            if (e[u] >= kListSlots * cap && q == 0) printf("LISTCHK bgrows e %d cap %d region %d i %d\n", e[u], cap, x, i0 + 16 * u);
+            if (e[u] >= kListSlots * cap && q == 0) printf("LISTCHK bgrows e %d cap %d region %d i %d\n", e[u], cap, x, i0 + RB * u);
 #endif
             *reinterpret_cast<f32x4*>(out + (size_t)e[u] * 64 + 4 * q) = v;
           }

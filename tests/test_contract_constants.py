@@ -23,3 +23,9 @@ def test_fc1_chain_count_matches_oracle():
     k = re.search(r"#define QLX_FC1_CHAINS (\d+)", _read("q-learning_amd", "csrc", "qnet32_kernels.h"))
     o = re.search(r"constexpr int kFc1Chains = (\d+);", _read("oracle", "qnet32_ref.cpp"))
     assert k and o and int(k.group(1)) == int(o.group(1)), (k and k.group(1), o and o.group(1))
+
+
+def test_conv_fwd_chain_count_matches_oracle():
+    k = re.search(r"#define QLX_CONV_FWD_CHAINS (\d+)", _read("q-learning_amd", "csrc", "qnet32_kernels.h"))
+    o = re.search(r"constexpr int kConvFwdChains = (\d+);", _read("oracle", "qnet32_ref.cpp"))
+    assert k and o and int(k.group(1)) == int(o.group(1)), (k and k.group(1), o and o.group(1))
