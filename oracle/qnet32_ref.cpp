@@ -70,7 +70,7 @@ struct Cfg { int H, W, C, K, S, OH, OW, OC; };
 static const Cfg kC2 = {20, 20, 32, 4, 2, 9, 9, 64}, kC3 = {9, 9, 64, 3, 1, 7, 7, 64};
 
 // conv2 / conv3 forward: z = C0 + C1, Ch = chain over the half h of k = (kh, kw, c) (flattened HWIO order; round 6)
-constexpr int kConvFwdChains = 2;   // (qnet32_kernels.h kConvFwdChains)
+constexpr int kConvFwdChains = 1;   // (qnet32_kernels.h kConvFwdChains; 2 = two chains over the k halves, measured slower)
 static void conv_fwd(const Cfg& c, const float* in, int B, const float* W, const float* bias, float* out) {
   const int K = c.K * c.K * c.C, half = K / kConvFwdChains;
 #pragma omp parallel for schedule(static)

@@ -1111,7 +1111,7 @@ struct NoSide {
 // 0..7 / 8..15; conv3: k < 288 / the rest), so that the training-batch list launch can run the two chains in two wave groups
 // of a block (KSPLIT); the chunk-batch launches run them one after the other (KSEQ)
 #ifndef QLX_CONV_FWD_CHAINS
-#define QLX_CONV_FWD_CHAINS 2   // (A/B timing builds only: 1 = the round-5 single chain, which the oracle no longer follows)
+#define QLX_CONV_FWD_CHAINS 1   // (2 measured slower, round 6: conv3 forward 26.4 -> 29.5 us in wave groups, the chunk pass 166 -> 175 us in turn; the oracle follows this value)
 #endif
 constexpr int kConvFwdChains = QLX_CONV_FWD_CHAINS;
 // conv2 / conv3 forward on fp32 NHWC input: out = relu(conv + bias); slab s: tap = 32 s / C, c0 = 32 s % C
