@@ -52,7 +52,7 @@ static_assert(kmaj_pitch(32, 16) == 48 && kmaj_pitch(64, 16) == 80 && kmaj_pitch
 // as before - the chains, and so every result, are unchanged.  The chunk index is XORed with row & 1 and the pitch is
 // 40 floats: with the ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS every fragment read is conflict-free, and so
 // are the stores, which become four ds_write_b32 per float4 of k (positions 8 q + j, q = 0..3, for the float4 j of a row)
-// (scripts/lds_banks.py --p8 checks both).  Before: pitch 36 and one ds_read_b32 per k step and fragment, 2-way
+// (scripts/p8_layout_search.py checks both).  Before: pitch 36 and one ds_read_b32 per k step and fragment, 2-way
 // conflicted (rows i and i + 8 share a bank; a k-pair swap for rows 8..15 that removed it measured slower in round 3).
 #ifndef QLX_Q32_P8
 #define QLX_Q32_P8 1   // (A/B builds: -DQLX_Q32_P8=0 restores the round-5 pitch-36 image and ds_read_b32 fragments)
@@ -2374,8 +2374,16 @@ __device__ __forceinline__ void c1_lists_flush(const unsigned long long* cl, int
 // tile's 16 frame dwords are read while this tile multiplies (against the kq-outer loop over all 13 accumulators: 49.1 ->
 // 47.9 us at B = 1024, 320 -> 309 us per 8,192-sample chunk, 256 -> 218 VGPRs; gpurun_out/w4).  One branch per (kq, tile)
 // with its four kw steps back to back (a branch per MFMA: 60 vs 46 us at C3)
+struct C1NoHook {
+  __device__ void operator()(int) const {}
+};
+// Hook (ONE, staged rows): called by every wave before its first tile of tile row R = 1 .. 4 (t / 5; every wave has tiles in
+// every row), so it may hold a block barrier; the next tile's frame dwords are not read ahead across a row boundary
+template <class Hook = C1NoHook>
 __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t (&ob2)[7], int nt, int rp, int g, int col,
-                                              const float (&wf)[64], float bias, int skip, float* a1, int b) {
+                                              const float (&wf)[64], float bias, int skip, float* a1, int b,
+                                              const Hook& hook = Hook{}) {
+  constexpr bool HOOK = !std::is_same_v<Hook, C1NoHook>;
   {
     uint32_t dn[16];
     auto tile_dwords = [&](int j, uint32_t (&d)[16]) {
@@ -2387,6 +2395,13 @@ __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t
 #pragma unroll
     for (int j = 0; j < 13; ++j)
       if (j < nt) {
+        if constexpr (HOOK) {
+          const int row = (rp + 2 * j) / 5;
+          if (j > 0 && row != (rp + 2 * (j - 1)) / 5) {   // (wave-uniform) the first tile of tile row `row`
+            hook(row);
+            tile_dwords(j, dn);
+          }
+        }
         uint32_t d[16];
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq) d[kq] = dn[kq];
@@ -2396,7 +2411,7 @@ __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t
         bool nz[16];
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq) nz[kq] = (__builtin_amdgcn_ballot_w64(d[kq] != 0u) != 0) | (skip == 0);   // wave-uniform, no branch
-        if (j + 1 < nt) tile_dwords(j + 1, dn);
+        if (j + 1 < nt && (!HOOK || (rp + 2 * (j + 1)) / 5 == (rp + 2 * j) / 5)) tile_dwords(j + 1, dn);
         f32x4 acc = zero4();
 #if QLX_C1_EXP != 2   // (timing experiments only: 2 = no MFMA, 1 = no a1 stores)
 #pragma unroll
@@ -2430,6 +2445,10 @@ __device__ __forceinline__ void c1_fwd_sample(const uint32_t* fr, const uint32_t
 // CU runs two samples at a time and a B = 1,024 batch is two samples deep per block: a sample's frame fetch, its
 // 13-tile chains and its a1 stores follow each other.  One sample per block needs one frame buffer (28 KB) and no prefetch
 // registers, so 4 blocks share a CU and all of a CU's samples run at once (VGPRs held to 128 by the launch bound).
+#ifndef QLX_C1_ROWS
+#define QLX_C1_ROWS 0   // ONE: stage the frames by tile rows (measured slower, round 6: 37.2 -> 48.1 us at B = 1024 - the four
+                        // row barriers cost more than the overlap wins, and the live load registers spill at 4 waves / SIMD)
+#endif
 #ifndef QLX_C1_ONE_MINW
 #define QLX_C1_ONE_MINW 4
 #endif
@@ -2468,6 +2487,43 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
   int b = blockIdx.x;
   if (b >= B) return;
   if constexpr (ONE) {
+#if QLX_C1_ROWS
+    // Staged by tile rows (round 6): the sample's 1,764 frame chunks in row order (block row bx, slot, block column by), a
+    // thread's load j = chunk tid + 256 j; tile row R needs block rows <= 4 R + 4, i.e. loads j < 2, 3, 5, 6, 7 for R = 0..4.
+    // Loads 0..2 are issued first and 0, 1 staged; the hook before row R stages what R needs and issues the loads row R + 1
+    // needs, so the first tiles multiply while the later rows are in flight (all of a CU's blocks start together: with one
+    // stage up front their fetches and their MFMAs did not overlap)
+    const C1Ptrs f = c1_ptrs(table, b);
+    uint4 pf[7];
+    auto issue = [&](int j) {
+      const int q = tid + 256 * j;
+      const bool ok = q < kC1Chunks;
+      const int qq = ok ? q : 0, bx = qq / 84, rem = qq - bx * 84, slot = rem / 21, by = rem - slot * 21;
+      pf[j] = ldg_frame(ok ? c1_slot(f, slot) : nullptr, bx * 21 + by);
+    };
+    auto stage = [&](int j) {
+      const int q = tid + 256 * j;
+      if (q < kC1Chunks) {
+        const int bx = q / 84, rem = q - bx * 84, slot = rem / 21, by = rem - slot * 21;
+        c1_put(c1w, slot * 441 + bx * 21 + by, pf[j]);
+        if (lists && (pf[j].x | pf[j].y | pf[j].z | pf[j].w) != 0u) atomicOr(&rm[bx], 1u << by);
+      }
+    };
+    issue(0);
+    issue(1);
+    issue(2);
+    stage(0);
+    stage(1);
+    __syncthreads();
+    auto hook = [&](int R) {
+      if (R == 1) { stage(2); issue(3); issue(4); }
+      else if (R == 2) { stage(3); stage(4); issue(5); }
+      else if (R == 3) { stage(5); issue(6); }
+      else { stage(6); }
+      __syncthreads();
+    };
+    c1_fwd_sample(c1w, ob2, nt, rp, g, col, wf, bias, skip, a1, b, hook);
+#else
     {
       uint4 pf[7];
       c1_prefetch(c1_ptrs(table, b), pf);
@@ -2476,6 +2532,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
     }
     __syncthreads();
     c1_fwd_sample(c1w, ob2, nt, rp, g, col, wf, bias, skip, a1, b);
+#endif
     if (lists) {
       if (wave < 3) c1_flags(rm, cl + wave * 2, wave, tid);
       __syncthreads();
