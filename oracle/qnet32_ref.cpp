@@ -156,7 +156,8 @@ void qnet32_forward(const QNet& q, const uint8_t* x8, int B, Acts& a) {
 
 // conv weight gradient of one layer, chunked: dW [K*K*C][OC] and db [OC] from input `in` (fp32 NHWC, or the u8
 // tensor view when in8 != null: conv1) and the ReLU-masked output gradient dz [B][OH][OW][OC]
-static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const float* dz, int B, int SC, float* dW, float* db) {
+static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const float* dz, int B, int SC, float* dW, float* db,
+                       const float* pb = nullptr) {
   const int KK = c.K * c.K * c.C, nz = (B + SC - 1) / SC;
   std::vector<float> part((size_t)nz * (KK + 1) * c.OC, 0.0f);
   std::vector<float> Pq((size_t)nz * 4 * c.OC, 0.0f);   // bias: chains C0..C3 per chunk
@@ -198,11 +199,28 @@ static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const 
     return t;
   };
   for (int i = 0; i < KK * c.OC; ++i) dW[i] = combine(i);
-  for (int z = 0; z < nz; ++z)   // bias partial of chunk z = ((C0 + C1) + C2) + C3
-    for (int oc = 0; oc < c.OC; ++oc) {
-      const float* C = Pq.data() + (size_t)z * 4 * c.OC;
-      part[((size_t)z * (KK + 1) + KK) * c.OC + oc] = ((C[oc] + C[c.OC + oc]) + C[2 * c.OC + oc]) + C[3 * c.OC + oc];
-    }
+  if (!pb) {
+    for (int z = 0; z < nz; ++z)   // bias partial of chunk z = ((C0 + C1) + C2) + C3
+      for (int oc = 0; oc < c.OC; ++oc) {
+        const float* C = Pq.data() + (size_t)z * 4 * c.OC;
+        part[((size_t)z * (KK + 1) + KK) * c.OC + oc] = ((C[oc] + C[c.OC + oc]) + C[2 * c.OC + oc]) + C[3 * c.OC + oc];
+      }
+  } else {
+    // conv1 (round 6): rows i = g16 * (OH OW) + position of the backward's partials pb, R per chunk; chunk z's bias partial
+    // = chain over jb = 0..15 of (chain over i = z R + jb + 16 k, k ascending, of pb[i][oc]) (k_conv1_wgrad32)
+    const int NR = (B + 15) / 16 * c.OH * c.OW, R = (NR + nz - 1) / nz;
+    for (int z = 0; z < nz; ++z)
+      for (int oc = 0; oc < c.OC; ++oc) {
+        const int i0 = z * R, i1 = std::min(NR, i0 + R);
+        float sb = 0.0f;
+        for (int jb = 0; jb < 16; ++jb) {
+          float t = 0.0f;
+          for (int i = i0 + jb; i < i1; i += 16) t = t + pb[(size_t)i * c.OC + oc];
+          sb = sb + t;
+        }
+        part[((size_t)z * (KK + 1) + KK) * c.OC + oc] = sb;
+      }
+  }
   for (int oc = 0; oc < c.OC; ++oc) db[oc] = combine((size_t)KK * c.OC + oc);
 }
 
@@ -315,7 +333,24 @@ float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* acti
   conv_wgrad(kC2, a.a1.data(), nullptr, dz2.data(), B, kSC2, g.g[2].data(), g.g[3].data());
   conv_dgrad(kC2, dz2.data(), B, q.w[2].data(), a.a1.data(), dz1.data());
   const Cfg c1 = {84, 84, 4, 8, 4, 20, 20, 32};
-  conv_wgrad(c1, nullptr, x8, dz1.data(), B, kSC1, g.g[0].data(), g.g[1].data());
+  // conv1's bias partials as the conv2 backward-data epilogue forms them (PConv2DgradPx::pb): per 16-sample group and
+  // position, (Q0 + Q1) + (Q2 + Q3) with Qg = ((d0 + d1) + d2) + d3 over samples 16 g16 + 4 g .. + 3 (0 past B)
+  std::vector<float> pb1((size_t)(B + 15) / 16 * 400 * 32);
+  for (int g16 = 0; g16 < (B + 15) / 16; ++g16)
+    for (int r = 0; r < 400; ++r)
+      for (int oc = 0; oc < 32; ++oc) {
+        float Q[4];
+        for (int gq = 0; gq < 4; ++gq) {
+          float d[4];
+          for (int e = 0; e < 4; ++e) {
+            const int b = 16 * g16 + 4 * gq + e;
+            d[e] = b < B ? dz1[((size_t)b * 400 + r) * 32 + oc] : 0.0f;
+          }
+          Q[gq] = ((d[0] + d[1]) + d[2]) + d[3];
+        }
+        pb1[((size_t)g16 * 400 + r) * 32 + oc] = (Q[0] + Q[1]) + (Q[2] + Q[3]);
+      }
+  conv_wgrad(c1, nullptr, x8, dz1.data(), B, kSC1, g.g[0].data(), g.g[1].data(), pb1.data());
   return loss;
 }
 

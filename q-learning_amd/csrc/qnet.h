@@ -37,12 +37,16 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float *fa1 = nullptr, *fa2 = nullptr, *fa3 = nullptr, *fa4 = nullptr;
   float *fdz1 = nullptr, *fdz2 = nullptr, *fdz3 = nullptr, *fdz4 = nullptr;
   float *fslab1 = nullptr, *fslab2 = nullptr, *fslab3 = nullptr;
+  float* fpb1 = nullptr;    // conv1 bias partials of the conv2 backward [ceil(B / 16)][400][32]
   float* fpart = nullptr;   // clip_by_norm segment partials
   // background rows of the conv2 / conv3 forward (qnet32_kernels.h C1Lists): row lists of the forward chunk, the list
   // counters of two forwards (double-buffered by forward parity), the constant rows relu(b0) / c2 / c3
   int *frl2 = nullptr, *frl3 = nullptr;
   unsigned long long* frcnt = nullptr;
   float* fbgc = nullptr;
+  uint32_t* fsteps = nullptr;   // the forward chunk's conv1 step masks [fchunk][4] (written when the row lists are)
+  uint8_t* fneed = nullptr;     // the same bits as bytes [100][fneed_ld] (step-major)
+  int fneed_ld = 0;
   int fparity = 0;
   int frl_cap = 0;   // samples the row lists hold
   int fchunk = 0;

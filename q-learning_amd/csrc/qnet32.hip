@@ -555,6 +555,9 @@ static int conv_adam_blocks() {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+#ifndef QLX_PB_OFF
+#define QLX_PB_OFF 0   // (timing only: the conv2 backward without conv1's bias partials - the conv1 bias is then wrong)
+#endif
 constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2, kSC3 = QLX_F32_WGRAD_CHUNK_CONV3;
 // weight-gradient chunk tiles 64 x 64 on 1 x 4 waves (each wave 64 rows x 16 channels): conv3 / conv2 pairs 73.0 -> 72.3 /
 // 102.2 -> 101.2 us in place against 2 x 2 (4 x 1: no change; gpurun_out/w14)
@@ -620,7 +623,9 @@ void f32_workspace(qlx_model* m, int B) {
                       std::max(2 * num_cus(), C / kC1MaxIt + 1) + kListSlots;
   static_assert(2048 + kListSlots <= 2048 + kListSlots * 2, "c1_one list capacity");
   const size_t o_rl2 = take((size_t)frl_cap * 81 * 4), o_rl3 = take((size_t)frl_cap * 49 * 4);
-  const size_t o_rcnt = take(2 * 2 * kListSlots * kCntStride * 8), o_bgc = take(160 * 4);
+  const size_t o_rcnt = take(2 * 2 * kListSlots * kCntStride * 8), o_bgc = take(160 * 4), o_steps = take((size_t)C * 4 * 4);
+  const int need_ld = (C + 63) / 64 * 64;   // (the conv2 backward-data tiles read 64-row blocks of it)
+  const size_t o_need = take((size_t)100 * need_ld);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -635,6 +640,9 @@ void f32_workspace(qlx_model* m, int B) {
   w.frl2 = (int*)(base + o_rl2); w.frl3 = (int*)(base + o_rl3);
   w.frcnt = (unsigned long long*)(base + o_rcnt);
   w.fbgc = (float*)(base + o_bgc);
+  w.fsteps = (uint32_t*)(base + o_steps);
+  w.fneed = (uint8_t*)(base + o_need);
+  w.fneed_ld = need_ld;
   QLX_HIP(hipMemset(w.frcnt, 0, 2 * 2 * kListSlots * kCntStride * 8));
   w.frl_cap = frl_cap;
   w.fparity = 0;
@@ -656,6 +664,7 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   const size_t o_s1 = take((size_t)((B + kSC1 - 1) / kSC1) * 257 * 32 * 4);
   const size_t o_s2 = take((size_t)((B + kSC2 - 1) / kSC2) * 513 * 64 * 4);
   const size_t o_s3 = take((size_t)((B + kSC3 - 1) / kSC3) * 577 * 64 * 4);
+  const size_t o_pb = take((size_t)((B + 15) / 16) * 400 * 32 * 4);
   void* p = nullptr;
   QLX_HIP(hipMalloc(&p, off));
   w.fgrad = p;
@@ -663,6 +672,7 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   w.fdz1 = (float*)(base + o_dz1); w.fdz2 = (float*)(base + o_dz2); w.fdz3 = (float*)(base + o_dz3);
   w.fdz4 = (float*)(base + o_dz4);
   w.fslab1 = (float*)(base + o_s1); w.fslab2 = (float*)(base + o_s2); w.fslab3 = (float*)(base + o_s3);
+  w.fpb1 = (float*)(base + o_pb);
   w.fgrad_batch = B;
 }
 
@@ -737,6 +747,12 @@ static void launch_list(qlx_model* m, const P& p, const S& side, const char* sco
 // conv2 / conv3 row (qlx_model::f32_bg_rows)
 static bool bg_rows(const qlx_model* m) { return m->f32_bg_rows; }
 
+// the conv1 step masks of the training forward (written with its row lists) select the dz1 rows the conv2 backward
+// stores and the conv1 weight gradient fetches; without zero-step skipping every row is multiplied, so every row
+#ifndef QLX_DZ1_SKIP
+#define QLX_DZ1_SKIP 1   // 0: the conv2 backward stores every dz1 row (the weight gradient still fetches the set steps' only)
+#endif
+static bool c1_sparse_dz(const qlx_model* m) { return bg_rows(m) && c1_skip(m); }
 template <class PW, class PR, class PF>
 static void conv_fwd(qlx_model* m, int M, const float* in, const float* wt, const float* bias, float* out, const char* scope,
                      double work, hipStream_t s, const PF& plain) {
@@ -772,7 +788,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
     const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1),
-                    w.fbgc};
+                    w.fbgc, w.fsteps, w.fneed, w.fneed_ld};
     if (lists) w.fparity ^= 1;
     {
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
@@ -948,8 +964,12 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
-    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B};
-    
+    PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B, QLX_PB_OFF ? nullptr : w.fpb1};
+    if (QLX_DZ1_SKIP && c1_sparse_dz(m)) {   // dz1 rows of clear conv1 steps are neither stored here nor fetched by the conv1 weight gradient
+      Pd.need = w.fneed;
+      Pd.need_ld = w.fneed_ld;
+    }
+
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
@@ -957,8 +977,10 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     hipEvent_t ea = nullptr, eb = nullptr;
     if (m->prof) m->prof->ext("f32_conv1_wgrad", 2.0 * B * 400 * 256 * 32, &ea, &eb);
     set_lds_limit((const void*)k_conv1_wgrad32, lds);
+    // the forward's step masks (when it built row lists) select the dz1 rows to fetch; without skipping, every row
+    const uint32_t* steps = c1_sparse_dz(m) ? w.fsteps : nullptr;
     hipExtLaunchKernelGGL(k_conv1_wgrad32, dim3(c1_wgrad_blocks(z1)), dim3(kC1WgradThreads), lds, s, ea, eb, 0u, table, w.fdz1, B, z1,
-                          w.fslab1, c1_skip(m));
+                          w.fslab1, c1_skip(m), steps, (const float*)w.fpb1);
     QLX_HIP(hipGetLastError());
     debug_sync(s, "k_conv1_wgrad32");
   }

@@ -1757,6 +1757,29 @@ struct PConv3DgradPx {
 // conv2 backward-data, pixel-major over the class grid: z = (i, j) of 10 x 10; rows b; cols (py, px, c) = 128 (the four
 // output parity classes share the A operand: dz2[b][i - th][j - tw]); k = valid (th, tw) x oc, which is the valid
 // (kh = py + 2 th, kw = px + 2 tw, oc) lexicographic order of every class
+#ifndef QLX_PB_XCH
+#define QLX_PB_XCH 1   // conv1 bias partials: lane exchanges by v_permlane16/32_swap (1) or ds_bpermute (0)
+#endif
+// (Q0 + Q1) + (Q2 + Q3) of a 16-row MFMA fragment column, Qg = ((d0 + d1) + d2) + d3 of lane group g's four rows, in every
+// lane (PConv2DgradPx::pb)
+#ifndef QLX_Q32_POLICIES_ONLY
+__device__ __forceinline__ float pb_sum16(const float (&d)[4]) {
+  float s = __fadd_rn(__fadd_rn(__fadd_rn(d[0], d[1]), d[2]), d[3]);
+#if QLX_PB_XCH
+  // VALU lane swaps (gfx950): with both operands s, the pair holds the lower and the upper row's (half's) value in every
+  // lane, so both partners form the same sum (an fp32 sum of two does not depend on the order)
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  s = __fadd_rn(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __fadd_rn(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+#else
+  s = __fadd_rn(s, __shfl_xor(s, 16));
+  return __fadd_rn(s, __shfl_xor(s, 32));
+#endif
+}
+#else
+inline float pb_sum16(const float (&d)[4]) { return ((d[0] + d[1]) + d[2]) + d[3]; }   // (host address replay)
+#endif
 template <int BM_ = 32, int BN_ = 128, int WM_ = 2, int WN_ = 2, bool DIRECT = false>
 struct PConv2DgradPx {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
@@ -1768,9 +1791,21 @@ struct PConv2DgradPx {
   const float* a1;
   float* dz1;         // [B][20][20][32]
   int B;
+  // conv1's bias partials [ceil(B / 16)][20][20][32] (null: none): per 16-sample row group g16 and position,
+  // (Q0 + Q1) + (Q2 + Q3), Qg = ((d0 + d1) + d2) + d3 over samples 16 g16 + 4 g .. + 3 of the stored dz1 (0 past B) -
+  // the lane's four rows, then its partners in lane groups g ^ 1 and g ^ 2 (k_conv1_wgrad32 chains them)
+  float* pb = nullptr;
+  // the forward's conv1 step bits as bytes [100][need_ld] (c1_steps; null: every row): dz1 rows of a clear step are not
+  // stored - no wave of k_conv1_wgrad32 multiplies them and it does not fetch them (their bias share is in pb all the same)
+  const uint8_t* need = nullptr;
+  int need_ld = 0;
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   struct Px {
     int i, j, th0, tw0, ntw, ntap;
+  };
+  struct Pre {
+    f32x4 m;       // a1 of the four rows (the ReLU mask)
+    uint32_t nb;   // their step bytes
   };
   __host__ __device__ static Px px(int z) {
     Px q;
@@ -1795,30 +1830,30 @@ struct PConv2DgradPx {
     const int cls = col >> 5, kh = (cls >> 1) + 2 * th, kw = (cls & 1) + 2 * tw;
     return ld4(w1 + ((size_t)(kh * 4 + kw) * 32 + (col & 31)) * 64 + (s & 1) * 32 + k);
   }
-  __device__ void epi(int z, int row, int col, f32x4 v) const {
+  __device__ void epi(int z, int row, int col, f32x4 v) const { epi_post(z, row, col, v, epi_pre(z, row, col)); }
+  __device__ Pre epi_pre(int z, int row, int col) const {
     const Px q = px(z);
     const int cls = col >> 5, ih = 2 * q.i + (cls >> 1), iw = 2 * q.j + (cls & 1);
+    Pre pr;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < B) {
-        const size_t o = ((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31);
-        dz1[o] = a1[o] > 0.0f ? v[r] : 0.0f;
-      }
+    for (int r = 0; r < 4; ++r) pr.m[r] = a1[((size_t)((row + r < B ? row + r : 0) * 20 + ih) * 20 + iw) * 32 + (col & 31)];
+    // (row is a multiple of 4 and row + 3 < need_ld: the four samples' bytes are one aligned dword)
+    pr.nb = need ? *reinterpret_cast<const uint32_t*>(need + (size_t)((ih * 20 + iw) >> 2) * need_ld + row) : ~0u;
+    return pr;
   }
-  __device__ f32x4 epi_pre(int z, int row, int col) const {
+  __device__ void epi_post(int z, int row, int col, f32x4 v, const Pre& pr) const {
     const Px q = px(z);
     const int cls = col >> 5, ih = 2 * q.i + (cls >> 1), iw = 2 * q.j + (cls & 1);
-    f32x4 m;
+    float d[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) m[r] = a1[((size_t)((row + r < B ? row + r : 0) * 20 + ih) * 20 + iw) * 32 + (col & 31)];
-    return m;
-  }
-  __device__ void epi_post(int z, int row, int col, f32x4 v, f32x4 m) const {
-    const Px q = px(z);
-    const int cls = col >> 5, ih = 2 * q.i + (cls >> 1), iw = 2 * q.j + (cls & 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < B) dz1[((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31)] = m[r] > 0.0f ? v[r] : 0.0f;
+    for (int r = 0; r < 4; ++r) {
+      d[r] = row + r < B && pr.m[r] > 0.0f ? v[r] : 0.0f;
+      if (row + r < B && ((pr.nb >> (8 * r)) & 0xFFu) != 0u) dz1[((size_t)((row + r) * 20 + ih) * 20 + iw) * 32 + (col & 31)] = d[r];
+    }
+    if (pb) {   // (uniform: every lane of the wave takes part in the exchanges)
+      const float s = pb_sum16(d);
+      if ((row & 15) == 0 && row < B) pb[((size_t)(row >> 4) * 400 + ih * 20 + iw) * 32 + (col & 31)] = s;
+    }
   }
   // streams (gemm_body_s): A = dz2 rows of the tile's samples (rows past B read zeros), B = W1 rows of the tile's class
   // channels; a slab's tap (th, tw) and oc half are wave-uniform offsets
@@ -2189,6 +2224,7 @@ __device__ __forceinline__ uint4 ldg_frame(const uint8_t* f, int pos) {
 // every store and load still in flight (a whole sample's a1 stores in the forward), and serialises the prefetch branches
 // behind one memory round trip each.
 typedef const __attribute__((address_space(4))) unsigned long long cu64;
+typedef const __attribute__((address_space(4))) uint32_t cu32;
 struct C1Ptrs {
   const uint8_t* p[4];
 };
@@ -2255,6 +2291,9 @@ struct C1Lists {
   unsigned long long* cnt;        // this forward's counters
   unsigned long long* cnt_next;   // the next forward's (double-buffered by forward parity), zeroed here
   float* xbg;                     // relu(0 + b0) [32]
+  uint32_t* steps;                // null, or the samples' conv1 step masks [n][4] (c1_steps)
+  uint8_t* need;                  // null, or the same bits as bytes [100][need_ld] (step-major: PConv2DgradPx::need)
+  int need_ld;
 };
 constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
 
@@ -2275,6 +2314,32 @@ __device__ __forceinline__ void c1_mark(uint32_t* rm, const uint4 (&pf)[7]) {
       atomicOr(&rm[bx], 1u << by);
     }
   }
+}
+
+// A sample's conv1 step mask (the weight gradient's 100 steps of 4 output positions r = 4 s .. 4 s + 3, all in row oh = s / 5,
+// columns ow = 4 t .. 4 t + 3, t = s % 5): bit s is set when any of the four positions' 8 x 8 x 4 patches holds a non-zero
+// byte, i.e. when a block of rows oh, oh + 1 and columns 4 t .. 4 t + 4 is marked.  Bits 100..127 are 0.  One wave: two
+// ballots, stored by lanes 0..3 (vector stores).  A clear bit means every wave of k_conv1_wgrad32 skips the step, so its
+// dz1 values are neither needed there nor (when the mask is given to the conv2 backward) stored.
+__device__ __forceinline__ void c1_steps(const uint32_t* rm, uint32_t* out, uint8_t* need, int need_ld, int b, int lane) {
+  bool nd[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int s = lane + 64 * h;
+    const bool valid = s < 100;
+    const int ss = valid ? s : 0, oh = ss / 5, t = ss - 5 * oh;
+    nd[h] = valid && ((((rm[oh] | rm[oh + 1]) >> (4 * t)) & 0x1Fu) != 0u);
+    if (need && valid) need[(size_t)s * need_ld + b] = nd[h] ? 1 : 0;
+  }
+  const unsigned long long m0 = __builtin_amdgcn_ballot_w64(nd[0]), m1 = __builtin_amdgcn_ballot_w64(nd[1]);
+  if (lane < 4) {
+    const unsigned long long m = lane < 2 ? m0 : m1;
+    out[lane] = (uint32_t)(m >> (32 * (lane & 1)));
+  }
+}
+// is step st (0..99) of the mask (lo = bits 0..63, hi = 64..127) set
+__device__ __forceinline__ bool c1_step_set(unsigned long long lo, unsigned long long hi, int st) {
+  return ((st < 64 ? lo >> st : hi >> (st - 64)) & 1ull) != 0ull;
 }
 
 // a sample's row flags, one wave's share (waves 0, 1: conv2 rows p = tid; wave 2: conv3 rows p = tid - 128), as two
@@ -2535,6 +2600,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
 #endif
     if (lists) {
       if (wave < 3) c1_flags(rm, cl + wave * 2, wave, tid);
+      else if (L.steps) c1_steps(rm, L.steps + (size_t)b * 4, L.need, L.need_ld, b, lane);
       __syncthreads();
       c1_lists_flush(cl, 1, blockIdx.x, gridDim.x, L, wave, tid, B, cl + 6);
     }
@@ -2560,6 +2626,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
     if (lists && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
     c1_fwd_sample(fr, ob2, nt, rp, g, col, wf, bias, skip, a1, b);
     if (lists && wave < 3) c1_flags(rm + (it % 3) * kC1RmDw, cl + it * 6 + wave * 2, wave, tid);
+    if (lists && wave == 3 && L.steps) c1_steps(rm + (it % 3) * kC1RmDw, L.steps + (size_t)b * 4, L.need, L.need_ld, b, lane);
     if (nb < B) {
       c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);
       if (lists) c1_mark(rm + ((it + 1) % 3) * kC1RmDw, pf);
@@ -2574,8 +2641,9 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
 
 // weight gradient over sample chunk z (SC samples): slab[z][m][oc] = chain over r = (b, oh, ow) ascending of
 // x[r][m] dz1[r][oc] (steps whose frame values are all 0 skipped when skip != 0, exactly as in the forward; exact for
-// finite dz1), m = (kh, kw, c) HWIO; bias slab[z][256][oc] = ((C0 + C1) + C2) + C3 with Cq the chain over (b, rs)
-// ascending of dz1[b][4 rs + q][oc] (the four lane groups' chains of the MFMA B operand).  One block per
+// finite dz1), m = (kh, kw, c) HWIO; bias slab[z][256][oc] = the chunk's share of the conv2 backward's bias partials
+// (PConv2DgradPx::pb) as 16 chains combined in order, so only the dz1 rows of set steps (c1_steps: the rows
+// some wave multiplies) are fetched - 27 % of them at C3 - when the forward's step masks are given.  One block per
 // chunk, 8 waves: waves 0..3 cover output channels 0..15, waves 4..7 channels 16..31 (round 6: before, one block per
 // (chunk, channel half) - both blocks fetched the chunk's frames, 29 of the launch's 110 MB).  Wave w owns kh = 2 (w % 4),
 // 2 (w % 4) + 1: lane row rho = (kh low bit, h, c), tile t = kw - 4 h, so one LDS dword (pixels 4 ow + 4 h .. + 3 of image
@@ -2590,7 +2658,8 @@ constexpr int kC1WgradPf = (kC1Chunks + kC1DzChunks + kC1WgradThreads - 1) / kC1
 constexpr size_t kC1WgradLds = (size_t)4 * kC1WgSlotDw * 4 + (size_t)400 * 32 * 4;          // 79,488 B
 __host__ __device__ constexpr int c1_wgrad_blocks(int nz) { return nz; }
 __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint8_t* const* table, const float* dz1, int B, int nz,
-                                                                       float* slab, int skip) {
+                                                                       float* slab, int skip, const uint32_t* steps,
+                                                                       const float* pb) {
   extern __shared__ __attribute__((aligned(16))) uint32_t c1w[];   // frames [4][1768] dwords, then dz [2 halves][400][16] f32
   float* dzs = reinterpret_cast<float*>(c1w + 4 * kC1WgSlotDw);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2605,11 +2674,35 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
   // dz1 in LDS as two [400][16] channel halves: a step's reads (rows r, r + 1 on lane groups g, g + 1; 16 channels each) are
   // 32 consecutive dwords - conflict-free (a [400][32] image puts both rows on the same 16 banks: 2-way)
 
+  // conv1's bias: this chunk's share of the partials pb (rows i = g16 * 400 + position, NR of them, R per chunk), 16
+  // chains per channel (chain jb over rows i0 + jb, i0 + jb + 16, ..), combined in jb order at the end.
+  // Issued first, four loads in flight per thread, so the chain waits for them only.
+  const int boc = tid & 31, bjb = tid >> 5;
+  float bt = 0.0f;
+  {
+    const int NR = ((B + 15) >> 4) * 400, R = (NR + nz - 1) / nz, i0 = z * R, i1 = min(NR, i0 + R);
+    for (int i = i0 + bjb; i < i1; i += 64) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i + 16 * u < i1 ? pb[(size_t)(i + 16 * u) * 32 + boc] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + 16 * u < i1) bt = __fadd_rn(bt, v[u]);
+    }
+  }
   uint4 pf[kC1WgradPf];
   auto prefetch = [&](int b, uint4 (&pf)[kC1WgradPf]) {
     const C1Ptrs f = c1_ptrs(table, b);
     const uint64_t zp = (uint64_t)(gbyte*)q32_zero4;
     const uint64_t dzb = (uint64_t)(dz1 + (size_t)b * 400 * 32);
+    // the sample's step mask (scalar loads; null: every step): a dz1 chunk of a clear step is not fetched - its LDS rows
+    // get the zero page, and no wave multiplies them (c1_steps)
+    unsigned long long lo = ~0ull, hi = ~0ull;
+    if (steps) {
+      cu32* sp = (cu32*)(steps + (size_t)b * 4);
+      lo = (unsigned long long)sp[0] | ((unsigned long long)sp[1] << 32);
+      hi = (unsigned long long)sp[2] | ((unsigned long long)sp[3] << 32);
+    }
 #pragma unroll
     for (int j = 0; j < kC1WgradPf; ++j) {   // one unconditional 16-byte load per j: a frame chunk, a dz1 chunk or the zero page
       const int q = tid + kC1WgradThreads * j;
@@ -2618,7 +2711,7 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
       const int e = isd ? q - kC1Chunks : 0;
       const uint64_t fp = (uint64_t)c1_slot(f, slot);
       const uint64_t fa = fp ? fp + (uint64_t)(pos * 16) : zp;
-      const uint64_t da = dzb + (uint64_t)e * 16;
+      const uint64_t da = c1_step_set(lo, hi, e >> 5) ? dzb + (uint64_t)e * 16 : zp;
       const u32x4v v = *(gu4*)(isf ? fa : (isd ? da : zp));
       pf[j] = uint4{v.x, v.y, v.z, v.w};
     }
@@ -2643,7 +2736,6 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = zero4();
-  float bsum = 0.0f;   // lane (oc, q): chain Cq of its B-operand values
   prefetch(b0, pf);
 #pragma unroll
   for (int bl = 0; bl < QLX_F32_WGRAD_CHUNK_CONV1; ++bl) {
@@ -2679,7 +2771,6 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
         if (nz[j])
 #pragma unroll
           for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ubyte(px[j], t), bv[j], acc[t], 0, 0, 0);
-        bsum = __fadd_rn(bsum, bv[j]);   // (every wave; wave wq = 0's is stored)
       }
     };
     rd(0, bA, xA);
@@ -2691,10 +2782,6 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
     }
   }
   float* out = slab + (size_t)z * 257 * 32;
-  if (wq == 0) {   // ((C0 + C1) + C2) + C3 in row 256
-    const float c1 = __shfl(bsum, lane + 16), c2 = __shfl(bsum, lane + 32), c3 = __shfl(bsum, lane + 48);
-    if (g == 0) out[256 * 32 + bo] = __fadd_rn(__fadd_rn(__fadd_rn(bsum, c1), c2), c3);
-  }
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -2702,6 +2789,16 @@ __global__ __launch_bounds__(kC1WgradThreads, 2) void k_conv1_wgrad32(const uint
       const int rho = 4 * g + i, kh = 2 * wq + (rho >> 3), kw = 4 * ((rho >> 2) & 1) + t, c = rho & 3;
       out[(size_t)((kh * 8 + kw) * 4 + c) * 32 + bo] = acc[t][i];
     }
+  // bias row 256: the 16 chains in order, through the dz1 image (every wave is past its last step)
+  __syncthreads();
+  dzs[bjb * 32 + boc] = bt;
+  __syncthreads();
+  if (tid < 32) {
+    float sb = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sb = __fadd_rn(sb, dzs[j * 32 + tid]);
+    out[256 * 32 + tid] = sb;
+  }
 }
 
 #endif  // QLX_Q32_POLICIES_ONLY

@@ -187,6 +187,13 @@ int main(int argc, char** argv) {
   replay(PConv2DgradPx<32, 64, 2, 2>{Grid{(B + 31) / 32, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px");
   replay(PConv2DgradPx<64, 64, 2, 2>{Grid{(B + 63) / 64, 2, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px 64");
   replay(PConv2DgradPx<64, 128, 2, 2>{Grid{(B + 63) / 64, 1, 100}, dz2, w1, a1, dz1, B}, "conv2_dgrad px 64 x 128");
+  {  // the product form: conv1 bias partials and the step bytes of the smallest workspace (need_ld = B rounded up to 64)
+    const int need_ld = (B + 63) / 64 * 64;
+    PConv2DgradPx<64, 64, 2, 2> P{Grid{(B + 63) / 64, 2, 100}, dz2, w1, a1, dz1, B, buf<float>((size_t)(B + 15) / 16 * 400 * 32)};
+    P.need = buf<uint8_t>((size_t)100 * need_ld);
+    P.need_ld = need_ld;
+    replay(P, "conv2_dgrad px 64 pb need");
+  }
   check_groups<PConv2DgradPxG<>>(100, 4, "conv2 groups");
   replay(PConv2DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 2, 81}, dz2, w1, a1, dz1, B}}, "conv2_dgrad pxg");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");

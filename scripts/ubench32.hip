@@ -535,7 +535,7 @@ int main(int argc, char** argv) {
       for (int skip = 0; skip < 2; ++skip) {
         const uint8_t* const* t = zero ? ztab : table;
         const double uf = time_us([&] { hipLaunchKernelGGL(k_conv1_fwd32<0>, dim3(G), dim3(256), 2 * kC1Frames, 0, t, B, W0, W0 + 8192, a1, skip, C1Lists{}); });
-        const double uw = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(c1_wgrad_blocks(nz)), dim3(kC1WgradThreads), lds, 0, t, dz1, B, nz, slab, skip); });
+        const double uw = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(c1_wgrad_blocks(nz)), dim3(kC1WgradThreads), lds, 0, t, dz1, B, nz, slab, skip, nullptr, dz1); });
         printf("conv1 B=%d frames %-5s skip %d: forward %8.2f us  weight gradient %8.2f us\n", B, zero ? "zero" : "live", skip, uf, uw);
       }
     for (int nb : {1024, 8192}) {
@@ -601,7 +601,7 @@ int main(int argc, char** argv) {
     {
       const int nz = B / 4, lds = (int)kC1WgradLds;
       CK(hipFuncSetAttribute((const void*)k_conv1_wgrad32, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(c1_wgrad_blocks(nz)), dim3(kC1WgradThreads), lds, 0, table, dz1, B, nz, slab, 1); });
+      const double us = time_us([&] { hipLaunchKernelGGL(k_conv1_wgrad32, dim3(c1_wgrad_blocks(nz)), dim3(kC1WgradThreads), lds, 0, table, dz1, B, nz, slab, 1, nullptr, dz1); });
       const double f = 2.0 * B * 400 * 256 * 32;
       printf("%-34s blocks %6d lds %6d  %9.2f us  %7.2f TF  %5.1f %%\n", "conv1_wgrad (k_conv1_wgrad32)", 2 * nz, lds, us,
              f / us / 1e6, f / us / 1e6 / 157.3 * 100);
