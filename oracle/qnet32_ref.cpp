@@ -224,6 +224,99 @@ static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const 
   for (int oc = 0; oc < c.OC; ++oc) db[oc] = combine((size_t)KK * c.OC + oc);
 }
 
+// conv2 weight gradient, compacted (round 6, PConvWgrad CMP): per 16-sample chunk the chain runs over the chunk's
+// non-background rows (b, oh, ow) ascending (bg[b][p]: the forward's classification - all frame pixels of the position's
+// 20 x 20 receptive field 0), the bias chains Cq over the compacted row index mod 4; a background row's im2col row is
+// u[m] = relu(b0[m % 32]) (m < 512), so the chunk's background share is u[m] S[oc], added per chunk before the two-level
+// combine: part[z][m][oc] = fmaf(u[m], S_z[oc], chain) (u = 1 for the bias row).  S_z = ((T0 + T1) + T2) + T3, Tq = chain
+// over p in [21 q, min(81, 21 q + 21)) of Pbg[z][p][oc] = (Q0 + Q1) + (Q2 + Q3), Qg = ((e0 + e1) + e2) + e3 over samples
+// 16 z + 4 g .. + 3 of e = bg ? dz : 0 (0 past B) - the conv3 backward-data epilogue's sums (PConv3DgradPx::pbg, SideBgSum).
+static void conv2_wgrad_cmp(const Cfg& c, const float* in, const float* dz, int B, const uint8_t* bg, const float* b0, float* dW,
+                            float* db) {
+  constexpr int SC = 16;
+  const int KK = c.K * c.K * c.C, P = c.OH * c.OW, nz = (B + SC - 1) / SC;
+  std::vector<float> part((size_t)nz * (KK + 1) * c.OC, 0.0f);
+#pragma omp parallel for schedule(dynamic)
+  for (int z = 0; z < nz; ++z) {
+    float* Pz = part.data() + (size_t)z * (KK + 1) * c.OC;
+    std::vector<float> Cq((size_t)4 * c.OC, 0.0f);
+    int kc = 0;   // compacted row index
+    for (int b = z * SC; b < std::min(B, (z + 1) * SC); ++b)
+      for (int p = 0; p < P; ++p) {
+        if (bg[(size_t)b * P + p]) continue;
+        const int oh = p / c.OW, ow = p - oh * c.OW;
+        const float* d = dz + ((size_t)b * P + p) * c.OC;
+        for (int oc = 0; oc < c.OC; ++oc) Cq[(size_t)(kc % 4) * c.OC + oc] = Cq[(size_t)(kc % 4) * c.OC + oc] + d[oc];
+        ++kc;
+        for (int kh = 0; kh < c.K; ++kh)
+          for (int kw = 0; kw < c.K; ++kw)
+            for (int ch = 0; ch < c.C; ++ch) {
+              const float v = in[(((size_t)b * c.H + oh * c.S + kh) * c.W + ow * c.S + kw) * c.C + ch];
+              if (v == 0.0f) continue;   // fmaf(0, d, acc) == acc
+              float* pr = Pz + ((size_t)(kh * c.K + kw) * c.C + ch) * c.OC;
+              for (int oc = 0; oc < c.OC; ++oc) pr[oc] = fma32(v, d[oc], pr[oc]);
+            }
+      }
+    for (int oc = 0; oc < c.OC; ++oc)
+      Pz[(size_t)KK * c.OC + oc] = ((Cq[oc] + Cq[c.OC + oc]) + Cq[2 * c.OC + oc]) + Cq[3 * c.OC + oc];
+    // the chunk's background rows: Pbg, S_z, then u[m] S_z[oc] into every row of the partial
+    std::vector<float> pbg((size_t)P * c.OC);
+    for (int p = 0; p < P; ++p)
+      for (int oc = 0; oc < c.OC; ++oc) {
+        float Q[4];
+        for (int gq = 0; gq < 4; ++gq) {
+          float e[4];
+          for (int k = 0; k < 4; ++k) {
+            const int b = SC * z + 4 * gq + k;
+            e[k] = b < B && bg[(size_t)b * P + p] ? dz[((size_t)b * P + p) * c.OC + oc] : 0.0f;
+          }
+          Q[gq] = ((e[0] + e[1]) + e[2]) + e[3];
+        }
+        pbg[(size_t)p * c.OC + oc] = (Q[0] + Q[1]) + (Q[2] + Q[3]);
+      }
+    for (int oc = 0; oc < c.OC; ++oc) {
+      float T[4];
+      for (int q = 0; q < 4; ++q) {
+        float t = 0.0f;
+        for (int p = 21 * q; p < std::min(P, 21 * q + 21); ++p) t = t + pbg[(size_t)p * c.OC + oc];
+        T[q] = t;
+      }
+      const float S = ((T[0] + T[1]) + T[2]) + T[3];
+      for (int m = 0; m <= KK; ++m) {
+        const float u = m < KK ? (b0[m % c.C] > 0.0f ? b0[m % c.C] : 0.0f) : 1.0f;
+        Pz[(size_t)m * c.OC + oc] = fma32(u, S, Pz[(size_t)m * c.OC + oc]);
+      }
+    }
+  }
+  auto combine = [&](size_t i) {   // as conv_wgrad
+    float t = 0.0f;
+    for (int q = 0; q * 16 < nz; ++q) {
+      float sq = 0.0f;
+      for (int z = 16 * q; z < std::min(nz, 16 * q + 16); ++z) sq = sq + part[(size_t)z * (KK + 1) * c.OC + i];
+      t = t + sq;
+    }
+    return t;
+  };
+  for (int i = 0; i < KK * c.OC; ++i) dW[i] = combine(i);
+  for (int oc = 0; oc < c.OC; ++oc) db[oc] = combine((size_t)KK * c.OC + oc);
+}
+
+// conv2 background rows of each sample (c1_flags): position (i, j) of the 9 x 9 grid whose frame pixels [8 i, 8 i + 20) x
+// [8 j, 8 j + 20), all four channels, are 0
+static std::vector<uint8_t> conv2_background(const uint8_t* x8, int B) {
+  std::vector<uint8_t> bg((size_t)B * 81);
+  for (int b = 0; b < B; ++b)
+    for (int i = 0; i < 9; ++i)
+      for (int j = 0; j < 9; ++j) {
+        bool any = false;
+        for (int y = 8 * i; y < 8 * i + 20 && !any; ++y)
+          for (int x = 8 * j; x < 8 * j + 20 && !any; ++x)
+            for (int ch = 0; ch < 4; ++ch) any |= x8[(((size_t)b * 84 + y) * 84 + x) * 4 + ch] != 0;
+        bg[(size_t)b * 81 + i * 9 + j] = any ? 0 : 1;
+      }
+  return bg;
+}
+
 // conv backward-data: din[b][ih][iw][c] = mask(a_in) * chain over the valid (kh, kw, oc) of dz[..][oc] W[kh][kw][c][oc]
 static void conv_dgrad(const Cfg& c, const float* dz, int B, const float* W, const float* a_in, float* din) {
   // W transposed to [kh][kw][oc][c] so the per-c chains run along contiguous memory
@@ -330,7 +423,8 @@ float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* acti
   std::vector<float> dz2((size_t)B * 81 * 64), dz1((size_t)B * 400 * 32);
   conv_wgrad(kC3, a.a2.data(), nullptr, dz3.data(), B, kSC3, g.g[4].data(), g.g[5].data());
   conv_dgrad(kC3, dz3.data(), B, q.w[4].data(), a.a2.data(), dz2.data());
-  conv_wgrad(kC2, a.a1.data(), nullptr, dz2.data(), B, kSC2, g.g[2].data(), g.g[3].data());
+  static_assert(kSC2 == 16, "conv2 weight gradient: 16-sample chunks");
+  conv2_wgrad_cmp(kC2, a.a1.data(), dz2.data(), B, conv2_background(x8, B).data(), q.w[1].data(), g.g[2].data(), g.g[3].data());
   conv_dgrad(kC2, dz2.data(), B, q.w[2].data(), a.a1.data(), dz1.data());
   const Cfg c1 = {84, 84, 4, 8, 4, 20, 20, 32};
   // conv1's bias partials as the conv2 backward-data epilogue forms them (PConv2DgradPx::pb): per 16-sample group and

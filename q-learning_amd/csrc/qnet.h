@@ -38,6 +38,8 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float *fdz1 = nullptr, *fdz2 = nullptr, *fdz3 = nullptr, *fdz4 = nullptr;
   float *fslab1 = nullptr, *fslab2 = nullptr, *fslab3 = nullptr;
   float* fpb1 = nullptr;    // conv1 bias partials of the conv2 backward [ceil(B / 16)][400][32]
+  float* fpbg2 = nullptr;   // conv2 background-row dz2 partials of the conv3 backward [ceil(B / 16)][81][64]
+  float* fs2 = nullptr;     // their per-chunk sums [ceil(B / 16)][64] (SideBgSum)
   float* fpart = nullptr;   // clip_by_norm segment partials
   // background rows of the conv2 / conv3 forward (qnet32_kernels.h C1Lists): row lists of the forward chunk, the list
   // counters of two forwards (double-buffered by forward parity), the constant rows relu(b0) / c2 / c3
@@ -47,6 +49,8 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   uint32_t* fsteps = nullptr;   // the forward chunk's conv1 step masks [fchunk][4] (written when the row lists are)
   uint8_t* fneed = nullptr;     // the same bits as bytes [100][fneed_ld] (step-major)
   int fneed_ld = 0;
+  uint32_t* frows2 = nullptr;   // the forward chunk's conv2 non-background row bits [fchunk][4]
+  uint8_t* fbg2 = nullptr;      // its conv2 background rows as bytes [81][fneed_ld]
   int fparity = 0;
   int frl_cap = 0;   // samples the row lists hold
   int fchunk = 0;

@@ -252,6 +252,10 @@ struct WRed {
   int nb[3];      // blocks of the segment
   float* gw[3];   // W gradient
   float* gb[3];   // b gradient
+  // segment 1 (conv2, compacted weight gradient): each chunk's partial gets u[m] S[z][n] first (fmaf; u = relu(b0) of
+  // channel m % 32 for m < 512, 1 for the bias row) - the chunk's background rows (PConvWgrad CMP)
+  const float* s2;
+  const float* u2;
 };
 __host__ __device__ inline int wred_waves(int nz) {
   const int ng = (nz + kWGroup - 1) / kWGroup;
@@ -286,10 +290,18 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred
   const int nz = R.nz[L], ng = (nz + kWGroup - 1) / kWGroup;
   const float* p = R.slab[L] + (live ? e + o : 0);
   float* gsub = gs + sub * ng * 64;   // (16 / W) * ng <= kWGroupsMax slices of 64
+  const bool bg = L == 1 && R.s2 != nullptr;   // (block-uniform)
+  const int oc = R.oc[L], me = (e + o) / oc, ne = (e + o) - me * oc;
+  const float um = bg && live ? (me < 512 ? R.u2[me & 31] : 1.0f) : 0.0f;
   for (int q = g0; q < ng; q += W) {
     float v[kWGroup];
 #pragma unroll
     for (int j = 0; j < kWGroup; ++j) v[j] = q * kWGroup + j < nz ? p[(size_t)(q * kWGroup + j) * stride] : 0.0f;
+    if (bg) {
+#pragma unroll
+      for (int j = 0; j < kWGroup; ++j)
+        if (q * kWGroup + j < nz) v[j] = fmaf(um, R.s2[(size_t)(q * kWGroup + j) * 64 + ne], v[j]);
+    }
     float t = 0.0f;
 #pragma unroll
     for (int j = 0; j < kWGroup; ++j) t = __fadd_rn(t, v[j]);   // + 0 past the last chunk leaves t unchanged
@@ -299,7 +311,7 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred
   if (g0 != 0 || !live) return;
   float t = 0.0f;
   for (int q = 0; q < ng; ++q) t = __fadd_rn(t, gsub[q * 64 + o]);
-  const int oc = R.oc[L], m = (e + o) / oc, n = (e + o) - m * oc;
+  const int m = me, n = ne;
   const int M = R.count[L] / oc - 1;
   if (m == M) R.gb[L][n] = t;
   else R.gw[L][(size_t)m * oc + n] = t;
@@ -564,7 +576,8 @@ constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2
 // conv3's offset table after the images (3 blocks per CU: pair 72.1 us; in the images' pads, 4 per CU: 76.1 us, held to 3
 // by a 44 KB LDS request: 73.1 us - gpurun_out/w22, w31); conv2's in the pads (4 blocks per CU: pair 99.6 -> 96.8 us)
 using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4, 16, false>;
-using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4>;
+using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4, 16, true, true>;   // (compacted)
+static_assert(kSC2 == 16, "conv2 weight-gradient chunks are the conv3 backward's 16-row fragments (pbg)");
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
 static_assert((1605632 + kNormSeg - 1) / kNormSeg <= kNormSegMax, "norm partials per variable");
@@ -626,6 +639,7 @@ void f32_workspace(qlx_model* m, int B) {
   const size_t o_rcnt = take(2 * 2 * kListSlots * kCntStride * 8), o_bgc = take(160 * 4), o_steps = take((size_t)C * 4 * 4);
   const int need_ld = (C + 63) / 64 * 64;   // (the conv2 backward-data tiles read 64-row blocks of it)
   const size_t o_need = take((size_t)100 * need_ld);
+  const size_t o_rows2 = take((size_t)C * 4 * 4), o_bg2 = take((size_t)81 * need_ld);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -643,6 +657,8 @@ void f32_workspace(qlx_model* m, int B) {
   w.fsteps = (uint32_t*)(base + o_steps);
   w.fneed = (uint8_t*)(base + o_need);
   w.fneed_ld = need_ld;
+  w.frows2 = (uint32_t*)(base + o_rows2);
+  w.fbg2 = (uint8_t*)(base + o_bg2);
   QLX_HIP(hipMemset(w.frcnt, 0, 2 * 2 * kListSlots * kCntStride * 8));
   w.frl_cap = frl_cap;
   w.fparity = 0;
@@ -665,6 +681,7 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   const size_t o_s2 = take((size_t)((B + kSC2 - 1) / kSC2) * 513 * 64 * 4);
   const size_t o_s3 = take((size_t)((B + kSC3 - 1) / kSC3) * 577 * 64 * 4);
   const size_t o_pb = take((size_t)((B + 15) / 16) * 400 * 32 * 4);
+  const size_t o_pbg = take((size_t)((B + 15) / 16) * 81 * 64 * 4), o_bgs = take((size_t)((B + 15) / 16) * 64 * 4);
   void* p = nullptr;
   QLX_HIP(hipMalloc(&p, off));
   w.fgrad = p;
@@ -673,6 +690,8 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   w.fdz4 = (float*)(base + o_dz4);
   w.fslab1 = (float*)(base + o_s1); w.fslab2 = (float*)(base + o_s2); w.fslab3 = (float*)(base + o_s3);
   w.fpb1 = (float*)(base + o_pb);
+  w.fpbg2 = (float*)(base + o_pbg);
+  w.fs2 = (float*)(base + o_bgs);
   w.fgrad_batch = B;
 }
 
@@ -788,7 +807,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
     const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1),
-                    w.fbgc, w.fsteps, w.fneed, w.fneed_ld};
+                    w.fbgc, w.fsteps, w.fneed, w.fneed_ld, w.frows2, w.fbg2};
     if (lists) w.fparity ^= 1;
     {
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
@@ -959,18 +978,21 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     // 64 x 64 pixel tiles on the stream core: pair 73.2 vs 75.0 us in place for 32 x 64 (gpurun_out/w3)
     using PD3 = PConv3DgradPx<64, 64, 2, 2>;
     PD3 Pd{Grid{(B + PD3::BM - 1) / PD3::BM, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
+    Pd.pbg = w.fpbg2;   // conv2's background-row dz2 sums (the compacted conv2 weight gradient)
+    Pd.bg2 = w.fbg2;
+    Pd.bg2_ld = w.fneed_ld;
     
     launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
-    PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
+    PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B, w.frows2};
     PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B, QLX_PB_OFF ? nullptr : w.fpb1};
     if (QLX_DZ1_SKIP && c1_sparse_dz(m)) {   // dz1 rows of clear conv1 steps are neither stored here nor fetched by the conv1 weight gradient
       Pd.need = w.fneed;
       Pd.need_ld = w.fneed_ld;
     }
 
-    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    launch_pair(m, Pw, Pd, SideBgSum{w.fpbg2, w.fs2, z2}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
     constexpr size_t lds = kC1WgradLds;   // 79,488 B
@@ -990,6 +1012,8 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     R.slab[0] = w.fslab3; R.nz[0] = z3; R.count[0] = 577 * 64; R.oc[0] = 64; R.gw[0] = G + voff(4); R.gb[0] = G + voff(5);
     R.slab[1] = w.fslab2; R.nz[1] = z2; R.count[1] = 513 * 64; R.oc[1] = 64; R.gw[1] = G + voff(2); R.gb[1] = G + voff(3);
     R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
+    R.s2 = w.fs2;
+    R.u2 = w.fbgc;   // relu(0 + b0), written by the training forward's conv1
     QLX_CHECK(std::max({z1, z2, z3}) <= kWGroup * kWGroupsMax, QLX_E_INVALID, "too many weight-gradient chunks");
     int nred = 0;
     for (int L = 0; L < 3; ++L) {

@@ -802,7 +802,9 @@ struct PairStreams {
 // and adds its row offset - no per-slab division or scalar offset arithmetic.  A thread stages 4 consecutive rows (a float4)
 // of one k; the 64 lanes of a wave instruction cover 4 consecutive k (16 lanes each): wave w stages k = 4 w + g and
 // 16 + 4 w + g.  (Measured slower and removed: the same offsets generated per slab on the scalar unit, 4 per wave load.)
-template <int T, bool PADS = true>
+// (SHIFT / MASK / MUL: an entry packs more than one offset - the lane's byte offset is ((entry >> SHIFT) & MASK) * MUL;
+// kOob must stay past the buffer's end under that map)
+template <int T, bool PADS = true, int SHIFT = 0, uint32_t MASK = 0xFFFFFFFFu, uint32_t MUL = 1u>
 struct TableK4Stream {
   static_assert(T == 256, "table gather stream: four waves");
   using O = Opnd<64, true, 16>;
@@ -828,7 +830,7 @@ struct TableK4Stream {
   }
   __device__ void load(int kbase, Regs& rg) const {
 #pragma unroll
-    for (int i = 0; i < N; ++i) rg[i] = buf_ld4(rs, vo + tbl[slot(kbase + k0 + 16 * i + g)], 0u);
+    for (int i = 0; i < N; ++i) rg[i] = buf_ld4(rs, vo + ((tbl[slot(kbase + k0 + 16 * i + g)] >> SHIFT) & MASK) * MUL, 0u);
   }
   __device__ void store(float* t, const Regs& rg) const {
 #pragma unroll
@@ -1094,6 +1096,30 @@ __global__ __launch_bounds__(threads_of<P>()) void k_gemm32_side(const P p, cons
   if (b < ns) { side.run(b, lds); return; }
   body(p, block_order<P>(b - ns, (int)gridDim.x - ns), lds);
 }
+
+// conv2's background-row dz sums per sample chunk z (PConvWgrad CMP, SC = 16): S[z][oc] = ((T0 + T1) + T2) + T3, Tq =
+// chain over p in [21 q, min(81, 21 q + 21)) ascending of pbg[z][p][oc] (the conv3 backward-data's per-chunk partials).
+// Leading blocks of the conv2 backward launch, one per chunk.
+struct SideBgSum {
+  static constexpr size_t LDS = 4 * 64 * sizeof(float);
+  const float* pbg;   // [nz][81][64]
+  float* S;           // [nz][64]
+  int nz;
+  __host__ __device__ int blocks() const { return nz; }
+  __device__ void run(int z, float* lds) const {
+    const int oc = threadIdx.x & 63, q = threadIdx.x >> 6, p0 = 21 * q, n = q < 3 ? 21 : 18;
+    float v[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) v[i] = i < n ? pbg[((size_t)z * 81 + p0 + i) * 64 + oc] : 0.0f;
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 21; ++i)
+      if (i < n) t = __fadd_rn(t, v[i]);
+    lds[q * 64 + oc] = t;
+    __syncthreads();
+    if (q == 0) S[(size_t)z * 64 + oc] = __fadd_rn(__fadd_rn(__fadd_rn(lds[oc], lds[64 + oc]), lds[128 + oc]), lds[192 + oc]);
+  }
+};
 
 struct NoSide {
   static constexpr size_t LDS = 0;
@@ -1660,6 +1686,33 @@ __host__ __device__ inline int px3_order(int z) { return z < 5 ? z + 2 : (z == 5
 // ... and of the 10 class rows of conv2 dgrad (valid th: 2 for i 1..8, 1 for 0 and 9)
 __host__ __device__ inline int px2_order(int z) { return z < 8 ? z + 1 : (z == 8 ? 0 : 9); }
 
+#ifndef QLX_PB_XCH
+#define QLX_PB_XCH 1   // conv1 bias partials: lane exchanges by v_permlane16/32_swap (1) or ds_bpermute (0)
+#endif
+// (Q0 + Q1) + (Q2 + Q3) of a 16-row MFMA fragment column, Qg = ((d0 + d1) + d2) + d3 of lane group g's four rows, in every
+// lane (PConv2DgradPx::pb)
+#ifndef QLX_Q32_POLICIES_ONLY
+__device__ __forceinline__ float pb_sum16(const float (&d)[4]) {
+  float s = __fadd_rn(__fadd_rn(__fadd_rn(d[0], d[1]), d[2]), d[3]);
+#if QLX_PB_XCH
+  // VALU lane swaps (gfx950): with both operands s, the pair holds the lower and the upper row's (half's) value in every
+  // lane, so both partners form the same sum (an fp32 sum of two does not depend on the order)
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  s = __fadd_rn(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __fadd_rn(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+#else
+  s = __fadd_rn(s, __shfl_xor(s, 16));
+  return __fadd_rn(s, __shfl_xor(s, 32));
+#endif
+}
+#else
+inline float pb_sum16(const float (&d)[4]) { return ((d[0] + d[1]) + d[2]) + d[3]; }   // (host address replay)
+#endif
+
+#ifndef QLX_BG2_POST
+#define QLX_BG2_POST 0
+#endif
 // conv3 backward-data, pixel-major: z = pixel (ih, iw) of the 9 x 9 grid; rows b; k = valid (kh, kw) x oc
 template <int BM_ = 32, int BN_ = 64, int WM_ = 2, int WN_ = 2, bool DIRECT = false>
 struct PConv3DgradPx {
@@ -1672,9 +1725,19 @@ struct PConv3DgradPx {
   const float* a2;
   float* dz2;
   int B;
+  // conv2's background-row dz2 sums per sample chunk (16 samples: one MFMA fragment's rows) and position (null: none):
+  // pbg[g16][p][oc] = (Q0 + Q1) + (Q2 + Q3), Qg = ((d0 + d1) + d2) + d3 over samples 16 g16 + 4 g .. + 3 of the stored dz2
+  // where position p of the sample is a background row (bg2, c1_flags), else 0 (PConvWgrad compacted, SideBgSum)
+  float* pbg = nullptr;
+  const uint8_t* bg2 = nullptr;
+  int bg2_ld = 0;
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   struct Px {
     int ih, iw, kh0, kw0, nkw, ntap;
+  };
+  struct Pre {
+    f32x4 m;       // a2 of the four rows (the ReLU mask)
+    uint32_t bg;   // their background bytes
   };
   __host__ __device__ static Px px(int z) {
     Px q;
@@ -1698,27 +1761,35 @@ struct PConv3DgradPx {
     const int t = s >> 1, kh = q.kh0 + t / q.nkw, kw = q.kw0 + t % q.nkw;
     return ld4(w2 + ((size_t)(kh * 3 + kw) * 64 + col) * 64 + (s & 1) * 32 + k);
   }
-  __device__ void epi(int z, int row, int col, f32x4 v) const {
+  __device__ void epi(int z, int row, int col, f32x4 v) const { epi_post(z, row, col, v, epi_pre(z, row, col)); }
+  __device__ Pre epi_pre(int z, int row, int col) const {
     const Px q = px(z);
+    Pre pr;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < B) {
-        const size_t o = ((size_t)((row + r) * 9 + q.ih) * 9 + q.iw) * 64 + col;
-        dz2[o] = a2[o] > 0.0f ? v[r] : 0.0f;
-      }
+    for (int r = 0; r < 4; ++r) pr.m[r] = a2[((size_t)((row + r < B ? row + r : 0) * 9 + q.ih) * 9 + q.iw) * 64 + col];
+    // (row is a multiple of 4 and row + 3 < bg2_ld: the four samples' bytes are one aligned dword)
+#if !QLX_BG2_POST
+    pr.bg = pbg ? *reinterpret_cast<const uint32_t*>(bg2 + (size_t)(q.ih * 9 + q.iw) * bg2_ld + row) : 0u;
+#endif
+    return pr;
   }
-  __device__ f32x4 epi_pre(int z, int row, int col) const {
+  __device__ void epi_post(int z, int row, int col, f32x4 v, const Pre& pr0) const {
     const Px q = px(z);
-    f32x4 m;
+    Pre pr = pr0;
+#if QLX_BG2_POST   // (the background bytes loaded in the epilogue: no register held across the slab loop)
+    pr.bg = pbg ? *reinterpret_cast<const uint32_t*>(bg2 + (size_t)(q.ih * 9 + q.iw) * bg2_ld + row) : 0u;
+#endif
+    float d[4], e[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) m[r] = a2[((size_t)((row + r < B ? row + r : 0) * 9 + q.ih) * 9 + q.iw) * 64 + col];
-    return m;
-  }
-  __device__ void epi_post(int z, int row, int col, f32x4 v, f32x4 m) const {
-    const Px q = px(z);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < B) dz2[((size_t)((row + r) * 9 + q.ih) * 9 + q.iw) * 64 + col] = m[r] > 0.0f ? v[r] : 0.0f;
+    for (int r = 0; r < 4; ++r) {
+      d[r] = row + r < B && pr.m[r] > 0.0f ? v[r] : 0.0f;
+      e[r] = ((pr.bg >> (8 * r)) & 0xFFu) != 0u ? d[r] : 0.0f;
+      if (row + r < B) dz2[((size_t)((row + r) * 9 + q.ih) * 9 + q.iw) * 64 + col] = d[r];
+    }
+    if (pbg) {   // (uniform: every lane of the wave takes part in the exchanges)
+      const float s = pb_sum16(e);
+      if ((row & 15) == 0 && row < B) pbg[((size_t)(row >> 4) * 81 + q.ih * 9 + q.iw) * 64 + col] = s;
+    }
   }
   // streams (gemm_body_s, gemm_body_chain): dz3 rows of the tile's samples (rows past B read zeros), W2 rows of the tile's
   // channels; a slab's pixel tap (kh, kw) and oc half are wave-uniform offsets (per sub-tile z in a chained group)
@@ -1757,29 +1828,6 @@ struct PConv3DgradPx {
 // conv2 backward-data, pixel-major over the class grid: z = (i, j) of 10 x 10; rows b; cols (py, px, c) = 128 (the four
 // output parity classes share the A operand: dz2[b][i - th][j - tw]); k = valid (th, tw) x oc, which is the valid
 // (kh = py + 2 th, kw = px + 2 tw, oc) lexicographic order of every class
-#ifndef QLX_PB_XCH
-#define QLX_PB_XCH 1   // conv1 bias partials: lane exchanges by v_permlane16/32_swap (1) or ds_bpermute (0)
-#endif
-// (Q0 + Q1) + (Q2 + Q3) of a 16-row MFMA fragment column, Qg = ((d0 + d1) + d2) + d3 of lane group g's four rows, in every
-// lane (PConv2DgradPx::pb)
-#ifndef QLX_Q32_POLICIES_ONLY
-__device__ __forceinline__ float pb_sum16(const float (&d)[4]) {
-  float s = __fadd_rn(__fadd_rn(__fadd_rn(d[0], d[1]), d[2]), d[3]);
-#if QLX_PB_XCH
-  // VALU lane swaps (gfx950): with both operands s, the pair holds the lower and the upper row's (half's) value in every
-  // lane, so both partners form the same sum (an fp32 sum of two does not depend on the order)
-  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  s = __fadd_rn(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
-  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  return __fadd_rn(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
-#else
-  s = __fadd_rn(s, __shfl_xor(s, 16));
-  return __fadd_rn(s, __shfl_xor(s, 32));
-#endif
-}
-#else
-inline float pb_sum16(const float (&d)[4]) { return ((d[0] + d[1]) + d[2]) + d[3]; }   // (host address replay)
-#endif
 template <int BM_ = 32, int BN_ = 128, int WM_ = 2, int WN_ = 2, bool DIRECT = false>
 struct PConv2DgradPx {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
@@ -2027,8 +2075,14 @@ using PConv2DgradS = PConv2DgradT<64, 32, 4, 1>;
 
 // conv2 / conv3 weight gradient over sample chunk z (samples [z SC, min(B, (z + 1) SC))): rows m = (kh, kw, c),
 // cols oc, r = (b, oh, ow) ascending; partial slab[z][M + 1][OC] (row M = bias partial)
+// CMP (round 6, conv2): the reduction runs over the chunk's non-background rows only (rows: the forward's row flags,
+// c1_flags), in order; a background row's im2col row is the constant u (relu(b0) per channel, the forward's xbg), so
+// its share u[m] dz[r][oc] is taken as u[m] S[oc] with S the chunk's background-row dz sum (SideBgSum), in the
+// weight-gradient reduction (k_wreduce32): slab[z][m][oc] + u[m] S[z][oc] per chunk.  The table entries
+// pack the im2col row offset from the chunk's first sample (bits 0..19) and the chunk row r (bits 20..31), which
+// addresses the dz row: one table for both streams.
 template <int H, int W, int C, int KS, int S, int OH, int OW, int OC, int SC, int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2,
-          int MF_ = 16, bool TPADS = true>
+          int MF_ = 16, bool TPADS = true, bool CMP = false>
 struct PConvWgrad {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
   static constexpr bool LOAD_FENCE = false;   // (with the conv2 backward data's: conv2 pair 101.3 -> 99.8 us, w18)
@@ -2040,12 +2094,24 @@ struct PConvWgrad {
   const float* dz;   // [B][OH][OW][OC]
   float* slab;
   int B;
+  const uint32_t* rows = nullptr;   // CMP: the samples' non-background row bits [B][4]
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int rows_in(int z) const {
     const int b0 = z * SC, b1 = b0 + SC < B ? b0 + SC : B;
     return (b1 - b0) * P;
   }
-  __host__ __device__ int nslabs(int z) const { return (rows_in(z) + BK - 1) / BK; }
+  static_assert(!CMP || (P <= 96 && SC * P <= 4096 && (size_t)SC * H * W * C * 4 <= 0xFFFFFu - 4 * KS * W * C),
+                "compacted weight gradient: packed table entries");
+  __host__ __device__ int kept_in(int z) const {   // CMP: the chunk's non-background rows
+    int n = 0;
+    for (int bl = 0; bl < SC; ++bl) {
+      const int b = z * SC + bl;
+      if (b < B) n += __builtin_popcount(rows[(size_t)b * 4]) + __builtin_popcount(rows[(size_t)b * 4 + 1]) +
+                      __builtin_popcount(rows[(size_t)b * 4 + 2]);
+    }
+    return n;
+  }
+  __host__ __device__ int nslabs(int z) const { return ((CMP ? kept_in(z) : rows_in(z)) + BK - 1) / BK; }
   __device__ f32x4 ldA(int z, int s, int row, int k) const {
     const int r0 = s * BK + k;
     const bool ok = r0 < rows_in(z);
@@ -2099,11 +2165,57 @@ struct PConvWgrad {
       b.store(bs, x.b);
     }
   };
+  // CMP: both operands through one table of the chunk's non-background rows (entry = A offset | r << 20; all ones past them)
+  using TA = TableK4Stream<T, TPADS, 0, 0xFFFFFu, 1u>;
+  using TB = TableK4Stream<T, TPADS, 20, 0xFFFu, (uint32_t)OC * 4u>;
+  struct StreamsCmp {
+    TA a;
+    TB b;
+    int z;
+    const uint32_t* rows;
+    int B;
+    struct Regs {
+      typename TA::Regs a;
+      typename TB::Regs b;
+    };
+    __device__ void prepare(float* lds, int ns) {
+      uint32_t* t = reinterpret_cast<uint32_t*>(lds);
+      int run = 0;   // kept rows of the samples before bl (uniform)
+      for (int bl = 0; bl < SC; ++bl) {
+        const int b = z * SC + bl;
+        if (b >= B) break;
+        const uint32_t w0 = rows[(size_t)b * 4], w1 = rows[(size_t)b * 4 + 1], w2 = rows[(size_t)b * 4 + 2];
+        for (int pp = a.tid; pp < P; pp += T) {
+          const uint32_t w = pp < 32 ? w0 : (pp < 64 ? w1 : w2), bit = 1u << (pp & 31);
+          if (w & bit) {
+            const int below = (pp >= 32 ? __builtin_popcount(w0) : 0) + (pp >= 64 ? __builtin_popcount(w1) : 0) +
+                              __builtin_popcount(w & (bit - 1u));
+            const int oh = pp / OW, ow = pp - oh * OW;
+            const uint32_t ao = (uint32_t)(((bl * H + oh * S) * W + ow * S) * C) * 4u;
+            t[TA::slot(run + below)] = ao | ((uint32_t)(bl * P + pp) << 20);
+          }
+        }
+        run += __builtin_popcount(w0) + __builtin_popcount(w1) + __builtin_popcount(w2);
+      }
+      for (int r = run + a.tid; r < ns * BK; r += T) t[TA::slot(r)] = 0xFFFFFFFFu;   // past both buffers under both maps
+      a.tbl = t;
+      b.tbl = t;
+    }
+    __device__ void load(int s, Regs& x) const {
+      a.load(s * BK, x.a);
+      b.load(s * BK, x.b);
+    }
+    __device__ void store(float* as, float* bs, const Regs& x) const {
+      a.store(as, x.a);
+      b.store(bs, x.b);
+    }
+  };
   // (the table stream stages 64-row tiles on four waves: other tile shapes keep the ldA / ldB core)
   // (in place against the ldA / ldB core: 262.3K vs 263.0K env-steps/s, conv2 pair 102.0 vs 102.2 us - neutral; kept as the
   // one path: the weight-gradient tiles then issue no per-slab address arithmetic)
   static constexpr bool STREAMED = BM_ == 64 && MF_ == 16 && WM_ * WN_ == 4;
-  using Streams = std::conditional_t<STREAMED, StreamsImpl, void>;
+  static_assert(!CMP || STREAMED, "compacted weight gradient: streamed tiles");
+  using Streams = std::conditional_t<STREAMED, std::conditional_t<CMP, StreamsCmp, StreamsImpl>, void>;
   static_assert(!TPADS || KMAX <= 4 * 32 * 16, "weight-gradient chunk: the offset table lives in the four images' pads");
   // TableK4Stream::slot() places the table in the pad columns 64..79 of four 64-row KMAJ images (A and B, two buffers):
   // a B tile of another width would put it into B's live data
@@ -2113,11 +2225,19 @@ struct PConvWgrad {
   __device__ ST streams(int z, int row0, int col0, int tid) const {
     ST st;
     st.z = z;
-    st.rows = rows_in(z);
     const int m = row0 + (tid & 15) * 4, tap = m / C, c = m - tap * C, kh = tap / KS, kw = tap - kh * KS;
-    st.a.init(in, (uint32_t)B * H * W * C * 4u, tid, (uint32_t)((kh * W + kw) * C + c) * 4u);
-    st.b.init(dz + (size_t)z * SC * P * OC, (uint32_t)st.rows * OC * 4u, tid,
-              [col0](int r, int k) { return (uint32_t)(k * OC + col0 + r) * 4u; });
+    if constexpr (CMP) {
+      st.rows = rows;
+      st.B = B;
+      const int nb = B - z * SC < SC ? B - z * SC : SC;   // the chunk's samples: its A and dz rows end the buffers
+      st.a.init(in + (size_t)z * SC * H * W * C, (uint32_t)nb * H * W * C * 4u, tid, (uint32_t)((kh * W + kw) * C + c) * 4u);
+      st.b.init(dz + (size_t)z * SC * P * OC, (uint32_t)nb * P * OC * 4u, tid, (uint32_t)(col0 + (tid & 15) * 4) * 4u);
+    } else {
+      st.rows = rows_in(z);
+      st.a.init(in, (uint32_t)B * H * W * C * 4u, tid, (uint32_t)((kh * W + kw) * C + c) * 4u);
+      st.b.init(dz + (size_t)z * SC * P * OC, (uint32_t)st.rows * OC * 4u, tid,
+                [col0](int r, int k) { return (uint32_t)(k * OC + col0 + r) * 4u; });
+    }
     return st;
   }
 };
@@ -2294,6 +2414,10 @@ struct C1Lists {
   uint32_t* steps;                // null, or the samples' conv1 step masks [n][4] (c1_steps)
   uint8_t* need;                  // null, or the same bits as bytes [100][need_ld] (step-major: PConv2DgradPx::need)
   int need_ld;
+  // null, or the samples' conv2 row flags (the row lists' classification, also without lists): rows2[n][4] the
+  // non-background bits (words 0, 1: rows 0..63, word 2: rows 64..80), bg2[81][need_ld] background as bytes (row-major)
+  uint32_t* rows2;
+  uint8_t* bg2;
 };
 constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
 
@@ -2346,7 +2470,7 @@ __device__ __forceinline__ bool c1_step_set(unsigned long long lo, unsigned long
 // ballots (non-background / background rows) stored in LDS at the end of the sample's iteration; the list entries are
 // claimed and written once per wave after the block's last sample (c1_lists_flush), so no atomic's round trip is waited
 // for inside the sample loop
-__device__ __forceinline__ void c1_flags(const uint32_t* rm, unsigned long long* cl, int wave, int) {
+__device__ __forceinline__ void c1_flags(const uint32_t* rm, unsigned long long* cl, int wave, const C1Lists& L, int b) {
   const int tid = c1_opaque_tid();
   const int R = wave < 2 ? 81 : 49, p = wave < 2 ? tid : tid - 128;
   const bool valid = p < R;
@@ -2369,6 +2493,12 @@ __device__ __forceinline__ void c1_flags(const uint32_t* rm, unsigned long long*
   if ((tid & 63) == 0) {
     cl[0] = bn;
     cl[1] = bb;
+  }
+  if (wave < 2 && L.rows2) {   // (vector stores: lanes 0, 1 of waves 0, 1)
+    const int lane = tid & 63;
+    if (lane < 2 && (wave == 0 || lane == 0)) L.rows2[(size_t)b * 4 + 2 * wave + lane] = (uint32_t)(bn >> (32 * lane));
+    if (wave == 1 && lane == 1) L.rows2[(size_t)b * 4 + 3] = 0u;
+    if (valid) L.bg2[(size_t)p * L.need_ld + b] = nonbg ? 0 : 1;
   }
 }
 // cl: [iteration][3 waves][2]; the block's samples b0, b0 + G, .. (nit of them)
@@ -2524,9 +2654,10 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
   uint32_t* rm = c1w + (ONE ? 1 : 2) * 4 * kC1SlotDw;
   unsigned long long* cl = reinterpret_cast<unsigned long long*>(rm + 3 * kC1RmDw);   // [iteration][3][2] (c1_flags)
   const bool lists = L.rl2 != nullptr;
+  const bool marks = lists || L.rows2 != nullptr;   // the samples' row classification (lists, row flags, step masks)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (lists) {
+  if (marks) {
     if (blockIdx.x == 0 && tid < 2 * kListSlots) L.cnt_next[tid * kCntStride] = 0ull;
     if (blockIdx.x == 0 && tid < 32) L.xbg[tid] = relu(0.0f + b0[tid]);   // conv2's constant input row
     if (tid < 3 * kC1RmDw) rm[tid] = 0u;
@@ -2571,7 +2702,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
       if (q < kC1Chunks) {
         const int bx = q / 84, rem = q - bx * 84, slot = rem / 21, by = rem - slot * 21;
         c1_put(c1w, slot * 441 + bx * 21 + by, pf[j]);
-        if (lists && (pf[j].x | pf[j].y | pf[j].z | pf[j].w) != 0u) atomicOr(&rm[bx], 1u << by);
+        if (marks && (pf[j].x | pf[j].y | pf[j].z | pf[j].w) != 0u) atomicOr(&rm[bx], 1u << by);
       }
     };
     issue(0);
@@ -2593,16 +2724,18 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
       uint4 pf[7];
       c1_prefetch(c1_ptrs(table, b), pf);
       c1_stage(c1w, pf);
-      if (lists) c1_mark(rm, pf);
+      if (marks) c1_mark(rm, pf);
     }
     __syncthreads();
     c1_fwd_sample(c1w, ob2, nt, rp, g, col, wf, bias, skip, a1, b);
 #endif
-    if (lists) {
-      if (wave < 3) c1_flags(rm, cl + wave * 2, wave, tid);
+    if (marks) {
+      if (wave < 3) c1_flags(rm, cl + wave * 2, wave, L, b);
       else if (L.steps) c1_steps(rm, L.steps + (size_t)b * 4, L.need, L.need_ld, b, lane);
-      __syncthreads();
-      c1_lists_flush(cl, 1, blockIdx.x, gridDim.x, L, wave, tid, B, cl + 6);
+      if (lists) {
+        __syncthreads();
+        c1_lists_flush(cl, 1, blockIdx.x, gridDim.x, L, wave, tid, B, cl + 6);
+      }
     }
     return;
   }
@@ -2611,7 +2744,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
   // frame pointers one sample ahead of the frames (scalar registers)
   C1Ptrs nxt = c1_ptrs(table, b + (int)gridDim.x < B ? b + (int)gridDim.x : b);
   c1_stage(c1w, pf);
-  if (lists) c1_mark(rm, pf);
+  if (marks) c1_mark(rm, pf);
   __syncthreads();
   for (int it = 0; b < B; b += gridDim.x, ++it) {
     const uint32_t* fr = c1w + (it & 1) * (4 * kC1SlotDw);
@@ -2623,13 +2756,13 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
     // row masks: buffer it % 3 holds sample b's (complete since the last barrier, read by c1_flags at the end of this
     // iteration); (it + 1) % 3 gets the next sample's at the end of this iteration; (it + 2) % 3, read at the end of
     // it - 1, is cleared for it + 1
-    if (lists && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
+    if (marks && wave == 3 && tid - 192 < kC1RmDw) rm[((it + 2) % 3) * kC1RmDw + tid - 192] = 0u;
     c1_fwd_sample(fr, ob2, nt, rp, g, col, wf, bias, skip, a1, b);
-    if (lists && wave < 3) c1_flags(rm + (it % 3) * kC1RmDw, cl + it * 6 + wave * 2, wave, tid);
-    if (lists && wave == 3 && L.steps) c1_steps(rm + (it % 3) * kC1RmDw, L.steps + (size_t)b * 4, L.need, L.need_ld, b, lane);
+    if (marks && wave < 3) c1_flags(rm + (it % 3) * kC1RmDw, cl + it * 6 + wave * 2, wave, L, b);
+    if (marks && wave == 3 && L.steps) c1_steps(rm + (it % 3) * kC1RmDw, L.steps + (size_t)b * 4, L.need, L.need_ld, b, lane);
     if (nb < B) {
       c1_stage(c1w + ((it + 1) & 1) * (4 * kC1SlotDw), pf);
-      if (lists) c1_mark(rm + ((it + 1) % 3) * kC1RmDw, pf);
+      if (marks) c1_mark(rm + ((it + 1) % 3) * kC1RmDw, pf);
     }
     __syncthreads();
   }

@@ -197,6 +197,20 @@ int main(int argc, char** argv) {
   check_groups<PConv2DgradPxG<>>(100, 4, "conv2 groups");
   replay(PConv2DgradPxG<64, 64, 2, 2>{{Grid{(B + 63) / 64, 2, 81}, dz2, w1, a1, dz1, B}}, "conv2_dgrad pxg");
   replay(PConv2Wgrad{grid(512, 64, 64, 64, z2), a1, dz2, s2, B}, "conv2_wgrad");
+  {  // the compacted form (the product's): non-background row bits, a varying share per sample (all, none, every k-th)
+    uint32_t* rows = buf<uint32_t>((size_t)B * 4);
+    for (int b = 0; b < B; ++b)
+      for (int p = 0; p < 81; ++p)
+        if (b % 5 == 0 || (b % 5 != 1 && (p * 7 + b) % (2 + b % 3) == 0)) rows[(size_t)b * 4 + p / 32] |= 1u << (p % 32);
+    using PW2C = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4, 16, true, true>;
+    replay(PW2C{grid(512, 64, 64, 64, z2), a1, dz2, s2, B, rows}, "conv2_wgrad compacted");
+    const int need_ld = (B + 63) / 64 * 64;
+    PConv3DgradPx<64, 64, 2, 2> P3{Grid{(B + 63) / 64, 1, 81}, dz3, w2, a2, dz2, B};
+    P3.pbg = buf<float>((size_t)(B + 15) / 16 * 81 * 64);
+    P3.bg2 = buf<uint8_t>((size_t)81 * need_ld);
+    P3.bg2_ld = need_ld;
+    replay(P3, "conv3_dgrad px 64 pbg");
+  }
   printf("B %d n %d: %ld operand loads replayed, all in bounds\n", B, n, checks);
   return 0;
 }
