@@ -205,6 +205,7 @@ void orc_qnet32_forward(void* h, const uint8_t* x, int B, float* q, float* a1, f
   if (a3) std::memcpy(a3, a.a3.data(), a.a3.size() * 4);
   if (a4) std::memcpy(a4, a.a4.data(), a.a4.size() * 4);
 }
+void orc_qnet32_set_dense(int dense) { qnet32_set_dense(dense != 0); }
 float orc_qnet32_train(void* h, const uint8_t* x, const uint8_t* actions, const float* y, int B, float* grads_out,
                        float* norms_out) {
   QNet* q = (QNet*)h;

@@ -231,10 +231,12 @@ static void conv_wgrad(const Cfg& c, const float* in, const uint8_t* in8, const 
 // combine: part[z][m][oc] = fmaf(u[m], S_z[oc], chain) (u = 1 for the bias row).  S_z = ((T0 + T1) + T2) + T3, Tq = chain
 // over p in [21 q, min(81, 21 q + 21)) of Pbg[z][p][oc] = (Q0 + Q1) + (Q2 + Q3), Qg = ((e0 + e1) + e2) + e3 over samples
 // 16 z + 4 g .. + 3 of e = bg ? dz : 0 (0 past B) - the conv3 backward-data epilogue's sums (PConv3DgradPx::pbg, SideBgSum).
-static void conv2_wgrad_cmp(const Cfg& c, const float* in, const float* dz, int B, const uint8_t* bg, const float* b0, float* dW,
-                            float* db) {
+// (conv3 likewise: rows (b, oh, ow) of the 7 x 7 grid, u = the constant conv2 output row c2 at channel m % 64, S from
+// the fc1 backward-data epilogue's sums over the 49 positions, Q = 13)
+static void conv_wgrad_cmp(const Cfg& c, const float* in, const float* dz, int B, const uint8_t* bg, const float* uc, float* dW,
+                           float* db) {
   constexpr int SC = 16;
-  const int KK = c.K * c.K * c.C, P = c.OH * c.OW, nz = (B + SC - 1) / SC;
+  const int KK = c.K * c.K * c.C, P = c.OH * c.OW, nz = (B + SC - 1) / SC;   // (P <= 81)
   std::vector<float> part((size_t)nz * (KK + 1) * c.OC, 0.0f);
 #pragma omp parallel for schedule(dynamic)
   for (int z = 0; z < nz; ++z) {
@@ -276,14 +278,15 @@ static void conv2_wgrad_cmp(const Cfg& c, const float* in, const float* dz, int 
       }
     for (int oc = 0; oc < c.OC; ++oc) {
       float T[4];
+      const int Q = (P + 3) / 4;
       for (int q = 0; q < 4; ++q) {
         float t = 0.0f;
-        for (int p = 21 * q; p < std::min(P, 21 * q + 21); ++p) t = t + pbg[(size_t)p * c.OC + oc];
+        for (int p = Q * q; p < std::min(P, Q * q + Q); ++p) t = t + pbg[(size_t)p * c.OC + oc];
         T[q] = t;
       }
       const float S = ((T[0] + T[1]) + T[2]) + T[3];
       for (int m = 0; m <= KK; ++m) {
-        const float u = m < KK ? (b0[m % c.C] > 0.0f ? b0[m % c.C] : 0.0f) : 1.0f;
+        const float u = m < KK ? uc[m % c.C] : 1.0f;
         Pz[(size_t)m * c.OC + oc] = fma32(u, S, Pz[(size_t)m * c.OC + oc]);
       }
     }
@@ -301,18 +304,21 @@ static void conv2_wgrad_cmp(const Cfg& c, const float* in, const float* dz, int 
   for (int oc = 0; oc < c.OC; ++oc) db[oc] = combine((size_t)KK * c.OC + oc);
 }
 
-// conv2 background rows of each sample (c1_flags): position (i, j) of the 9 x 9 grid whose frame pixels [8 i, 8 i + 20) x
-// [8 j, 8 j + 20), all four channels, are 0
-static std::vector<uint8_t> conv2_background(const uint8_t* x8, int B) {
-  std::vector<uint8_t> bg((size_t)B * 81);
+static bool g_dense = false;
+void qnet32_set_dense(bool dense) { g_dense = dense; }
+
+// background rows of each sample (c1_flags): position (i, j) of the n x n grid (conv2: 9, field 20; conv3: 7, field 36)
+// whose frame pixels [8 i, 8 i + field) x [8 j, 8 j + field), all four channels, are 0
+static std::vector<uint8_t> background(const uint8_t* x8, int B, int n, int field) {
+  std::vector<uint8_t> bg((size_t)B * n * n);
   for (int b = 0; b < B; ++b)
-    for (int i = 0; i < 9; ++i)
-      for (int j = 0; j < 9; ++j) {
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
         bool any = false;
-        for (int y = 8 * i; y < 8 * i + 20 && !any; ++y)
-          for (int x = 8 * j; x < 8 * j + 20 && !any; ++x)
+        for (int y = 8 * i; y < 8 * i + field && !any; ++y)
+          for (int x = 8 * j; x < 8 * j + field && !any; ++x)
             for (int ch = 0; ch < 4; ++ch) any |= x8[(((size_t)b * 84 + y) * 84 + x) * 4 + ch] != 0;
-        bg[(size_t)b * 81 + i * 9 + j] = any ? 0 : 1;
+        bg[((size_t)b * n + i) * n + j] = any ? 0 : 1;
       }
   return bg;
 }
@@ -421,10 +427,29 @@ float qnet32_loss_backward(const QNet& q, const uint8_t* x8, const uint8_t* acti
   }
   // conv3, conv2, conv1
   std::vector<float> dz2((size_t)B * 81 * 64), dz1((size_t)B * 400 * 32);
-  conv_wgrad(kC3, a.a2.data(), nullptr, dz3.data(), B, kSC3, g.g[4].data(), g.g[5].data());
+  static_assert(kSC3 == 16, "conv3 weight gradient: 16-sample chunks");
+  const std::vector<uint8_t> bg2 = background(x8, B, 9, 20), bg3 = background(x8, B, 7, 36);
+  if (g_dense) {
+    conv_wgrad(kC3, a.a2.data(), nullptr, dz3.data(), B, kSC3, g.g[4].data(), g.g[5].data());
+  } else {
+    // u = c2: a2 at a conv2 background position (every such position holds it; none - no conv3 background row either)
+    std::vector<float> c2(64, 0.0f);
+    for (size_t r = 0; r < bg2.size(); ++r)
+      if (bg2[r]) {
+        std::memcpy(c2.data(), a.a2.data() + r * 64, 64 * 4);
+        break;
+      }
+    conv_wgrad_cmp(kC3, a.a2.data(), dz3.data(), B, bg3.data(), c2.data(), g.g[4].data(), g.g[5].data());
+  }
   conv_dgrad(kC3, dz3.data(), B, q.w[4].data(), a.a2.data(), dz2.data());
   static_assert(kSC2 == 16, "conv2 weight gradient: 16-sample chunks");
-  conv2_wgrad_cmp(kC2, a.a1.data(), dz2.data(), B, conv2_background(x8, B).data(), q.w[1].data(), g.g[2].data(), g.g[3].data());
+  if (g_dense) {
+    conv_wgrad(kC2, a.a1.data(), nullptr, dz2.data(), B, kSC2, g.g[2].data(), g.g[3].data());
+  } else {
+    std::vector<float> u1(32);   // relu(0 + b0)
+    for (int ch = 0; ch < 32; ++ch) u1[ch] = q.w[1][ch] > 0.0f ? q.w[1][ch] : 0.0f;
+    conv_wgrad_cmp(kC2, a.a1.data(), dz2.data(), B, bg2.data(), u1.data(), g.g[2].data(), g.g[3].data());
+  }
   conv_dgrad(kC2, dz2.data(), B, q.w[2].data(), a.a1.data(), dz1.data());
   const Cfg c1 = {84, 84, 4, 8, 4, 20, 20, 32};
   // conv1's bias partials as the conv2 backward-data epilogue forms them (PConv2DgradPx::pb): per 16-sample group and

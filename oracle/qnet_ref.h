@@ -57,6 +57,9 @@ void qnet32_forward(const QNet& q, const uint8_t* x, int B, Acts& acts);
 float qnet32_loss_backward(const QNet& q, const uint8_t* x, const uint8_t* actions, const float* y, int B,
                            const Acts& acts, Grads& grads, const float* weights = nullptr, float* td_abs = nullptr);
 void qnet32_apply_adam(QNet& q, const Grads& grads, float* norms_out /*[10] or null*/);
+// the product's dense-frame path (QLX_F32_BG=0): the conv weight gradients over every row (no background-row
+// compaction); process-wide, default off
+void qnet32_set_dense(bool dense);
 
 // reference helpers
 int argmax_first(const float* q, int n);

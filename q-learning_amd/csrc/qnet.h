@@ -40,6 +40,8 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   float* fpb1 = nullptr;    // conv1 bias partials of the conv2 backward [ceil(B / 16)][400][32]
   float* fpbg2 = nullptr;   // conv2 background-row dz2 partials of the conv3 backward [ceil(B / 16)][81][64]
   float* fs2 = nullptr;     // their per-chunk sums [ceil(B / 16)][64] (SideBgSum)
+  float* fpbg3 = nullptr;   // conv3 background-row dz3 partials of the fc1 backward [ceil(B / 16)][49][64]
+  float* fs3 = nullptr;     // their per-chunk sums [ceil(B / 16)][64]
   float* fpart = nullptr;   // clip_by_norm segment partials
   // background rows of the conv2 / conv3 forward (qnet32_kernels.h C1Lists): row lists of the forward chunk, the list
   // counters of two forwards (double-buffered by forward parity), the constant rows relu(b0) / c2 / c3
@@ -51,6 +53,8 @@ struct ModelWs {   // per-batch workspace (activations are bf16, heads fp32)
   int fneed_ld = 0;
   uint32_t* frows2 = nullptr;   // the forward chunk's conv2 non-background row bits [fchunk][4]
   uint8_t* fbg2 = nullptr;      // its conv2 background rows as bytes [81][fneed_ld]
+  uint32_t* frows3 = nullptr;   // the same for conv3 [fchunk][4], [49][fneed_ld]
+  uint8_t* fbg3 = nullptr;
   int fparity = 0;
   int frl_cap = 0;   // samples the row lists hold
   int fchunk = 0;

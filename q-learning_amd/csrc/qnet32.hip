@@ -252,10 +252,11 @@ struct WRed {
   int nb[3];      // blocks of the segment
   float* gw[3];   // W gradient
   float* gb[3];   // b gradient
-  // segment 1 (conv2, compacted weight gradient): each chunk's partial gets u[m] S[z][n] first (fmaf; u = relu(b0) of
-  // channel m % 32 for m < 512, 1 for the bias row) - the chunk's background rows (PConvWgrad CMP)
-  const float* s2;
-  const float* u2;
+  // segments 0, 1 (conv3, conv2: compacted weight gradients; null: none): each chunk's partial gets u[m] S[z][n] first
+  // (fmaf; u[m] = the layer's constant input row at channel m % C - conv2: relu(b0), C = 32; conv3: c2, C = 64 - and 1
+  // for the bias row): the chunk's background rows (PConvWgrad CMP)
+  const float* sbg[2];
+  const float* ubg[2];
 };
 __host__ __device__ inline int wred_waves(int nz) {
   const int ng = (nz + kWGroup - 1) / kWGroup;
@@ -290,9 +291,11 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred
   const int nz = R.nz[L], ng = (nz + kWGroup - 1) / kWGroup;
   const float* p = R.slab[L] + (live ? e + o : 0);
   float* gsub = gs + sub * ng * 64;   // (16 / W) * ng <= kWGroupsMax slices of 64
-  const bool bg = L == 1 && R.s2 != nullptr;   // (block-uniform)
+  const float* sbg = L < 2 ? R.sbg[L] : nullptr;   // (block-uniform)
+  const bool bg = sbg != nullptr;
   const int oc = R.oc[L], me = (e + o) / oc, ne = (e + o) - me * oc;
-  const float um = bg && live ? (me < 512 ? R.u2[me & 31] : 1.0f) : 0.0f;
+  const int Mr = R.count[L] / oc - 1, uc = L == 0 ? 64 : 32;
+  const float um = bg && live ? (me < Mr ? R.ubg[L][me % uc] : 1.0f) : 0.0f;
   for (int q = g0; q < ng; q += W) {
     float v[kWGroup];
 #pragma unroll
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(1024) void k_wreduce32(WRed R, NormArgs N, int nred
     if (bg) {
 #pragma unroll
       for (int j = 0; j < kWGroup; ++j)
-        if (q * kWGroup + j < nz) v[j] = fmaf(um, R.s2[(size_t)(q * kWGroup + j) * 64 + ne], v[j]);
+        if (q * kWGroup + j < nz) v[j] = fmaf(um, sbg[(size_t)(q * kWGroup + j) * 64 + ne], v[j]);
     }
     float t = 0.0f;
 #pragma unroll
@@ -575,8 +578,11 @@ constexpr int kSC1 = QLX_F32_WGRAD_CHUNK_CONV1, kSC2 = QLX_F32_WGRAD_CHUNK_CONV2
 // 102.2 -> 101.2 us in place against 2 x 2 (4 x 1: no change; gpurun_out/w14)
 // conv3's offset table after the images (3 blocks per CU: pair 72.1 us; in the images' pads, 4 per CU: 76.1 us, held to 3
 // by a 44 KB LDS request: 73.1 us - gpurun_out/w22, w31); conv2's in the pads (4 blocks per CU: pair 99.6 -> 96.8 us)
-using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4, 16, false>;
+using PConv3Wgrad = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4, 16, false, true>;   // (compacted)
+using PConv3WgradD = PConvWgrad<9, 9, 64, 3, 1, 7, 7, 64, kSC3, 64, 64, 1, 4, 16, false>;         // (every row: QLX_F32_BG=0)
+static_assert(kSC3 == 16, "conv3 weight-gradient chunks are the fc1 backward's 16-row fragments (pbg)");
 using PConv2Wgrad = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4, 16, true, true>;   // (compacted)
+using PConv2WgradD = PConvWgrad<20, 20, 32, 4, 2, 9, 9, 64, kSC2, 64, 64, 1, 4>;                  // (every row: QLX_F32_BG=0)
 static_assert(kSC2 == 16, "conv2 weight-gradient chunks are the conv3 backward's 16-row fragments (pbg)");
 
 static int segs_of(int v) { return (kVarSize[v] + kNormSeg - 1) / kNormSeg; }
@@ -640,6 +646,7 @@ void f32_workspace(qlx_model* m, int B) {
   const int need_ld = (C + 63) / 64 * 64;   // (the conv2 backward-data tiles read 64-row blocks of it)
   const size_t o_need = take((size_t)100 * need_ld);
   const size_t o_rows2 = take((size_t)C * 4 * 4), o_bg2 = take((size_t)81 * need_ld);
+  const size_t o_rows3 = take((size_t)C * 4 * 4), o_bg3 = take((size_t)49 * need_ld);
   QLX_HIP(hipMalloc(&m->ws, off));
   char* base = (char*)m->ws;
   w.frames = (uint8_t*)(base + o_frames);
@@ -659,6 +666,8 @@ void f32_workspace(qlx_model* m, int B) {
   w.fneed_ld = need_ld;
   w.frows2 = (uint32_t*)(base + o_rows2);
   w.fbg2 = (uint8_t*)(base + o_bg2);
+  w.frows3 = (uint32_t*)(base + o_rows3);
+  w.fbg3 = (uint8_t*)(base + o_bg3);
   QLX_HIP(hipMemset(w.frcnt, 0, 2 * 2 * kListSlots * kCntStride * 8));
   w.frl_cap = frl_cap;
   w.fparity = 0;
@@ -682,6 +691,7 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   const size_t o_s3 = take((size_t)((B + kSC3 - 1) / kSC3) * 577 * 64 * 4);
   const size_t o_pb = take((size_t)((B + 15) / 16) * 400 * 32 * 4);
   const size_t o_pbg = take((size_t)((B + 15) / 16) * 81 * 64 * 4), o_bgs = take((size_t)((B + 15) / 16) * 64 * 4);
+  const size_t o_pbg3 = take((size_t)((B + 15) / 16) * 49 * 64 * 4), o_bgs3 = take((size_t)((B + 15) / 16) * 64 * 4);
   void* p = nullptr;
   QLX_HIP(hipMalloc(&p, off));
   w.fgrad = p;
@@ -692,6 +702,8 @@ static void f32_grad_workspace(qlx_model* m, int B) {
   w.fpb1 = (float*)(base + o_pb);
   w.fpbg2 = (float*)(base + o_pbg);
   w.fs2 = (float*)(base + o_bgs);
+  w.fpbg3 = (float*)(base + o_pbg3);
+  w.fs3 = (float*)(base + o_bgs3);
   w.fgrad_batch = B;
 }
 
@@ -807,7 +819,7 @@ void f32_forward(qlx_model* m, const uint8_t* const* table, int B, hipStream_t s
     const int cap2 = per_slot * 81, cap3 = per_slot * 49;
     QLX_CHECK((size_t)kListSlots * cap2 <= w.frl_cap * 81, QLX_E_STATE, "row lists too small");
     const C1Lists L{lists ? w.frl2 : nullptr, w.frl3, cap2, cap3, cnt, w.frcnt + 2 * kListSlots * kCntStride * (w.fparity ^ 1),
-                    w.fbgc, w.fsteps, w.fneed, w.fneed_ld, w.frows2, w.fbg2};
+                    w.fbgc, w.fsteps, w.fneed, w.fneed_ld, w.frows2, w.fbg2, w.frows3, w.fbg3};
     if (lists) w.fparity ^= 1;
     {
       const char* sc = big ? "f32_conv1_fwd_big" : "f32_conv1_fwd";
@@ -919,6 +931,11 @@ void f32_backward_dense(qlx_model* m, int B, const uint8_t* actions, const float
   {  // dW3 + db3 and dz3 tiles in one grid, dW4 / db4 / loss as its leading blocks
     PFc1WgradS Pw{grid(3136, PFc1WgradS::BM, 512, PFc1WgradS::BN, 1), w.fa3, w.fdz4, G + voff(6), G + voff(7), B};
     PFc1DgradS Pd{grid(B, PFc1DgradS::BM, 3136, PFc1DgradS::BN, 1), w.fdz4, p + voff(6), w.fa3, w.fdz3, B};
+    if (bg_rows(m)) {   // conv3's background-row dz3 sums (the compacted conv3 weight gradient)
+      Pd.pbg = w.fpbg3;
+      Pd.bg = w.fbg3;
+      Pd.bg_ld = w.fneed_ld;
+    }
     SideFc2 S{w.fa4, actions, w.gs, w.hs, B, G + voff(8), G + voff(9), loss_dev};
     launch_pair(m, Pw, Pd, S, "f32_fc1_bwd", 2.0 * 2.0 * B * 512 * 3136, s);   // (3 blocks per CU: 72.8 vs 61.8 us, w23)
   }
@@ -974,25 +991,33 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
   // one-pixel conv3 tiles beat the balanced pixel groups (chained sub-tiles: scripts/ubench32.hip bwd, B = 1024: pair 84.4
   // vs 93.4 us; on the ldA / ldB core the groups had won, 97.1 vs 105.6 us); conv2 groups were slower on both cores
   {  // conv3: dz2 pixel tiles + weight-gradient chunk tiles
-    PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
+    PConv3Wgrad Pw{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B, w.frows3};
+    PConv3WgradD Pw_dense{grid(576, 64, 64, 64, z3), w.fa2, w.fdz3, w.fslab3, B};
     // 64 x 64 pixel tiles on the stream core: pair 73.2 vs 75.0 us in place for 32 x 64 (gpurun_out/w3)
     using PD3 = PConv3DgradPx<64, 64, 2, 2>;
     PD3 Pd{Grid{(B + PD3::BM - 1) / PD3::BM, 1, 81}, w.fdz3, p + voff(4), w.fa2, w.fdz2, B};
-    Pd.pbg = w.fpbg2;   // conv2's background-row dz2 sums (the compacted conv2 weight gradient)
-    Pd.bg2 = w.fbg2;
-    Pd.bg2_ld = w.fneed_ld;
+    if (bg_rows(m)) {   // conv2's background-row dz2 sums (the compacted conv2 weight gradient)
+      Pd.pbg = w.fpbg2;
+      Pd.bg2 = w.fbg2;
+      Pd.bg2_ld = w.fneed_ld;
+    }
     
-    launch_pair(m, Pw, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+    if (bg_rows(m)) launch_pair(m, Pw, Pd, SideBgSum<49>{w.fpbg3, w.fs3, z3}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
+    else launch_pair(m, Pw_dense, Pd, NoSide{}, "f32_conv3_bwd", 2.0 * 2.0 * B * 49 * 64 * 576, s);
   }
   {  // conv2: dz1 pixel tiles (all 4 parity classes) + weight-gradient chunk tiles
+    // the weight gradient over the non-background rows (their background share through SideBgSum and k_wreduce32), or
+    // over every row on the dense-frame path
     PConv2Wgrad Pw{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B, w.frows2};
+    PConv2WgradD Pw_dense{grid(512, 64, 64, 64, z2), w.fa1, w.fdz2, w.fslab2, B};
     PConv2DgradPx<64, 64, 2, 2> Pd{Grid{(B + 63) / 64, 2, 100}, w.fdz2, p + voff(2), w.fa1, w.fdz1, B, QLX_PB_OFF ? nullptr : w.fpb1};
     if (QLX_DZ1_SKIP && c1_sparse_dz(m)) {   // dz1 rows of clear conv1 steps are neither stored here nor fetched by the conv1 weight gradient
       Pd.need = w.fneed;
       Pd.need_ld = w.fneed_ld;
     }
 
-    launch_pair(m, Pw, Pd, SideBgSum{w.fpbg2, w.fs2, z2}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    if (bg_rows(m)) launch_pair(m, Pw, Pd, SideBgSum<81>{w.fpbg2, w.fs2, z2}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
+    else launch_pair(m, Pw_dense, Pd, NoSide{}, "f32_conv2_bwd", 2.0 * 2.0 * B * 81 * 64 * 512, s);
   }
   {
     constexpr size_t lds = kC1WgradLds;   // 79,488 B
@@ -1012,8 +1037,10 @@ void f32_backward_conv(qlx_model* m, const uint8_t* const* table, int B, hipStre
     R.slab[0] = w.fslab3; R.nz[0] = z3; R.count[0] = 577 * 64; R.oc[0] = 64; R.gw[0] = G + voff(4); R.gb[0] = G + voff(5);
     R.slab[1] = w.fslab2; R.nz[1] = z2; R.count[1] = 513 * 64; R.oc[1] = 64; R.gw[1] = G + voff(2); R.gb[1] = G + voff(3);
     R.slab[2] = w.fslab1; R.nz[2] = z1; R.count[2] = 257 * 32; R.oc[2] = 32; R.gw[2] = G + voff(0); R.gb[2] = G + voff(1);
-    R.s2 = w.fs2;
-    R.u2 = w.fbgc;   // relu(0 + b0), written by the training forward's conv1
+    R.sbg[0] = bg_rows(m) ? w.fs3 : nullptr;
+    R.ubg[0] = w.fbgc + 32;   // c2, written by the training forward's conv2 launch (ConstRows)
+    R.sbg[1] = bg_rows(m) ? w.fs2 : nullptr;
+    R.ubg[1] = w.fbgc;        // relu(0 + b0), written by the training forward's conv1
     QLX_CHECK(std::max({z1, z2, z3}) <= kWGroup * kWGroupsMax, QLX_E_INVALID, "too many weight-gradient chunks");
     int nred = 0;
     for (int L = 0; L < 3; ++L) {

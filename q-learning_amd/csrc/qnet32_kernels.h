@@ -1097,23 +1097,26 @@ __global__ __launch_bounds__(threads_of<P>()) void k_gemm32_side(const P p, cons
   body(p, block_order<P>(b - ns, (int)gridDim.x - ns), lds);
 }
 
-// conv2's background-row dz sums per sample chunk z (PConvWgrad CMP, SC = 16): S[z][oc] = ((T0 + T1) + T2) + T3, Tq =
-// chain over p in [21 q, min(81, 21 q + 21)) ascending of pbg[z][p][oc] (the conv3 backward-data's per-chunk partials).
-// Leading blocks of the conv2 backward launch, one per chunk.
+// A conv layer's background-row dz sums per sample chunk z (PConvWgrad CMP, SC = 16; conv2: P = 81, conv3: P = 49):
+// S[z][oc] = ((T0 + T1) + T2) + T3, Tq = chain over p in [Q q, min(P, Q q + Q)) ascending of pbg[z][p][oc], Q = ceil(P / 4)
+// (the per-chunk partials of the backward-data epilogue that produced dz).  Leading blocks of the layer's backward
+// launch, one per chunk.
+template <int P = 81>
 struct SideBgSum {
   static constexpr size_t LDS = 4 * 64 * sizeof(float);
-  const float* pbg;   // [nz][81][64]
+  static constexpr int Q = (P + 3) / 4;   // positions per chain
+  const float* pbg;   // [nz][P][64]
   float* S;           // [nz][64]
   int nz;
   __host__ __device__ int blocks() const { return nz; }
   __device__ void run(int z, float* lds) const {
-    const int oc = threadIdx.x & 63, q = threadIdx.x >> 6, p0 = 21 * q, n = q < 3 ? 21 : 18;
-    float v[21];
+    const int oc = threadIdx.x & 63, q = threadIdx.x >> 6, p0 = Q * q, n = q < 3 ? Q : P - 3 * Q;
+    float v[Q];
 #pragma unroll
-    for (int i = 0; i < 21; ++i) v[i] = i < n ? pbg[((size_t)z * 81 + p0 + i) * 64 + oc] : 0.0f;
+    for (int i = 0; i < Q; ++i) v[i] = i < n ? pbg[((size_t)z * P + p0 + i) * 64 + oc] : 0.0f;
     float t = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 21; ++i)
+    for (int i = 0; i < Q; ++i)
       if (i < n) t = __fadd_rn(t, v[i]);
     lds[q * 64 + oc] = t;
     __syncthreads();
@@ -1531,6 +1534,30 @@ using PFc1FwdB = PFc1FwdT<64, 128, 2, 2, 16, 1, kFc1Chains>;
 using PFc1FwdS = PFc1FwdT<32, 32, 2, 2, 16, kFc1Chains, 1>;   // (round 5, after the slab-loop fix: 64 x 32 / 32 x 64 38.4 / 38.9 us against 33.8)
 
 // fc1 backward-data: dz3 [B][3136] = (dz4 [B][512] W3^T) * (a3 > 0); k = n
+#ifndef QLX_PB_XCH
+#define QLX_PB_XCH 1   // conv1 bias partials: lane exchanges by v_permlane16/32_swap (1) or ds_bpermute (0)
+#endif
+// (Q0 + Q1) + (Q2 + Q3) of a 16-row MFMA fragment column, Qg = ((d0 + d1) + d2) + d3 of lane group g's four rows, in every
+// lane (PConv2DgradPx::pb)
+#ifndef QLX_Q32_POLICIES_ONLY
+__device__ __forceinline__ float pb_sum16(const float (&d)[4]) {
+  float s = __fadd_rn(__fadd_rn(__fadd_rn(d[0], d[1]), d[2]), d[3]);
+#if QLX_PB_XCH
+  // VALU lane swaps (gfx950): with both operands s, the pair holds the lower and the upper row's (half's) value in every
+  // lane, so both partners form the same sum (an fp32 sum of two does not depend on the order)
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  s = __fadd_rn(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __fadd_rn(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+#else
+  s = __fadd_rn(s, __shfl_xor(s, 16));
+  return __fadd_rn(s, __shfl_xor(s, 32));
+#endif
+}
+#else
+inline float pb_sum16(const float (&d)[4]) { return ((d[0] + d[1]) + d[2]) + d[3]; }   // (host address replay)
+#endif
+
 template <int BM_ = 64, int BN_ = 64, int WM_ = 2, int WN_ = 2, int MF_ = 16>
 struct PFc1DgradT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, MF = MF_;
@@ -1541,31 +1568,43 @@ struct PFc1DgradT {
   const float* a3;
   float* dz3;
   int M;
+  // conv3's background-row dz3 sums per 16-sample chunk and position, as PConv3DgradPx::pbg for conv2 (null: none):
+  // pbg[g16][p][c], column = 64 p + c, background bytes bg[49][bg_ld]
+  float* pbg = nullptr;
+  const uint8_t* bg = nullptr;
+  int bg_ld = 0;
+  struct Pre {
+    f32x4 m;
+    uint32_t bg;
+  };
   __host__ __device__ void decode(int lb, int& tm, int& tn, int& z) const { g.decode(lb, tm, tn, z); }
   __host__ __device__ int nslabs(int) const { return 512 / BK; }
   __device__ f32x4 ldA(int, int s, int row, int k) const {
     return ld4m(dz4 + (size_t)(row < M ? row : 0) * 512 + s * BK + k, row < M);
   }
   __device__ f32x4 ldB(int, int s, int col, int k) const { return ld4(w3 + (size_t)col * 512 + s * BK + k); }
-  __device__ void epi(int, int row, int col, f32x4 v) const {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < M) {
-        const size_t o = (size_t)(row + r) * 3136 + col;
-        dz3[o] = a3[o] > 0.0f ? v[r] : 0.0f;
-      }
-  }
+  __device__ void epi(int z, int row, int col, f32x4 v) const { epi_post(z, row, col, v, epi_pre(z, row, col)); }
   // the ReLU mask of the four rows, loaded before the slab loop (HasEpiPre; rows past M read row 0)
-  __device__ f32x4 epi_pre(int, int row, int col) const {
-    f32x4 m;
+  __device__ Pre epi_pre(int, int row, int col) const {
+    Pre pr;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) m[r] = a3[(size_t)(row + r < M ? row + r : 0) * 3136 + col];
-    return m;
+    for (int r = 0; r < 4; ++r) pr.m[r] = a3[(size_t)(row + r < M ? row + r : 0) * 3136 + col];
+    // (row is a multiple of 4 and row + 3 < bg_ld: the four samples' bytes are one aligned dword)
+    pr.bg = pbg ? *reinterpret_cast<const uint32_t*>(bg + (size_t)(col >> 6) * bg_ld + row) : 0u;
+    return pr;
   }
-  __device__ void epi_post(int, int row, int col, f32x4 v, f32x4 m) const {
+  __device__ void epi_post(int, int row, int col, f32x4 v, const Pre& pr) const {
+    float d[4], e[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (row + r < M) dz3[(size_t)(row + r) * 3136 + col] = m[r] > 0.0f ? v[r] : 0.0f;
+    for (int r = 0; r < 4; ++r) {
+      d[r] = row + r < M && pr.m[r] > 0.0f ? v[r] : 0.0f;
+      e[r] = ((pr.bg >> (8 * r)) & 0xFFu) != 0u ? d[r] : 0.0f;
+      if (row + r < M) dz3[(size_t)(row + r) * 3136 + col] = d[r];
+    }
+    if (pbg) {   // (uniform: every lane of the wave takes part in the exchanges)
+      const float s = pb_sum16(e);
+      if ((row & 15) == 0 && row < M) pbg[(size_t)(row >> 4) * 3136 + col] = s;
+    }
   }
   // streams (gemm_body_s): dz4 rows (rows past M read zeros), W3 rows (k = n contiguous)
   static constexpr int T = WM_ * WN_ * 64;
@@ -1686,29 +1725,6 @@ __host__ __device__ inline int px3_order(int z) { return z < 5 ? z + 2 : (z == 5
 // ... and of the 10 class rows of conv2 dgrad (valid th: 2 for i 1..8, 1 for 0 and 9)
 __host__ __device__ inline int px2_order(int z) { return z < 8 ? z + 1 : (z == 8 ? 0 : 9); }
 
-#ifndef QLX_PB_XCH
-#define QLX_PB_XCH 1   // conv1 bias partials: lane exchanges by v_permlane16/32_swap (1) or ds_bpermute (0)
-#endif
-// (Q0 + Q1) + (Q2 + Q3) of a 16-row MFMA fragment column, Qg = ((d0 + d1) + d2) + d3 of lane group g's four rows, in every
-// lane (PConv2DgradPx::pb)
-#ifndef QLX_Q32_POLICIES_ONLY
-__device__ __forceinline__ float pb_sum16(const float (&d)[4]) {
-  float s = __fadd_rn(__fadd_rn(__fadd_rn(d[0], d[1]), d[2]), d[3]);
-#if QLX_PB_XCH
-  // VALU lane swaps (gfx950): with both operands s, the pair holds the lower and the upper row's (half's) value in every
-  // lane, so both partners form the same sum (an fp32 sum of two does not depend on the order)
-  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  s = __fadd_rn(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
-  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  return __fadd_rn(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
-#else
-  s = __fadd_rn(s, __shfl_xor(s, 16));
-  return __fadd_rn(s, __shfl_xor(s, 32));
-#endif
-}
-#else
-inline float pb_sum16(const float (&d)[4]) { return ((d[0] + d[1]) + d[2]) + d[3]; }   // (host address replay)
-#endif
 
 #ifndef QLX_BG2_POST
 #define QLX_BG2_POST 0
@@ -2418,6 +2434,8 @@ struct C1Lists {
   // non-background bits (words 0, 1: rows 0..63, word 2: rows 64..80), bg2[81][need_ld] background as bytes (row-major)
   uint32_t* rows2;
   uint8_t* bg2;
+  uint32_t* rows3;                // the same for conv3's 49 rows: rows3[n][4] (words 0, 1), bg3[49][need_ld]
+  uint8_t* bg3;
 };
 constexpr int kC1RmDw = 24;       // one row-mask buffer (21 dwords + pad); three buffers after the frames in LDS
 
@@ -2499,6 +2517,11 @@ __device__ __forceinline__ void c1_flags(const uint32_t* rm, unsigned long long*
     if (lane < 2 && (wave == 0 || lane == 0)) L.rows2[(size_t)b * 4 + 2 * wave + lane] = (uint32_t)(bn >> (32 * lane));
     if (wave == 1 && lane == 1) L.rows2[(size_t)b * 4 + 3] = 0u;
     if (valid) L.bg2[(size_t)p * L.need_ld + b] = nonbg ? 0 : 1;
+  }
+  if (wave == 2 && L.rows3) {
+    const int lane = tid & 63;
+    if (lane < 4) L.rows3[(size_t)b * 4 + lane] = lane < 2 ? (uint32_t)(bn >> (32 * lane)) : 0u;
+    if (valid) L.bg3[(size_t)p * L.need_ld + b] = nonbg ? 0 : 1;
   }
 }
 // cl: [iteration][3 waves][2]; the block's samples b0, b0 + G, .. (nit of them)
@@ -2654,7 +2677,7 @@ __global__ __launch_bounds__(256, ONE ? QLX_C1_ONE_MINW : 2) void k_conv1_fwd32(
   uint32_t* rm = c1w + (ONE ? 1 : 2) * 4 * kC1SlotDw;
   unsigned long long* cl = reinterpret_cast<unsigned long long*>(rm + 3 * kC1RmDw);   // [iteration][3][2] (c1_flags)
   const bool lists = L.rl2 != nullptr;
-  const bool marks = lists || L.rows2 != nullptr;   // the samples' row classification (lists, row flags, step masks)
+  const bool marks = lists || L.rows2 != nullptr || L.rows3 != nullptr;   // the samples' row classification (lists, row flags, step masks)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (marks) {

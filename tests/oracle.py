@@ -133,6 +133,7 @@ def lib():
         L.orc_qnet_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
         L.orc_qnet_train.restype = f32
         L.orc_qnet32_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+        L.orc_qnet32_set_dense.argtypes = [i32]
         L.orc_qnet32_train.argtypes = [vp, vp, vp, vp, i32, vp, vp]
         L.orc_qnet32_train.restype = f32
         L.orc_qnet32_apply.argtypes = [vp, vp, f32, vp]

@@ -86,13 +86,26 @@ def case(tmp_path_factory):
     exp["q1"], acts = ref.forward(x1, acts=True)
     exp["a2"], exp["a3"] = acts[1].ravel(), acts[2].ravel()
     exp["q2"] = ref.forward(x2)
-    loss, grads, norms = ref.train(xt, at, yt)
-    exp["loss"], exp["norms"] = np.float32(loss), np.asarray(norms, np.float32)
-    for v in range(10):
-        exp[f"g{v}"] = grads[v]
-        for which in range(3):
-            exp[f"s{v}_{which}"] = ref.get(v, which)
-    return d, inp, exp
+    # the training step twice: the default chains (background-row compaction of the conv weight gradients) and the
+    # dense-frame path's (QLX_F32_BG=0: every row)
+    snap = {(v, which): ref.get(v, which) for v in range(10) for which in range(3)}
+    it0 = ref.iterations()
+    exps = {}
+    for dense in (False, True):
+        for (v, which), a in snap.items():
+            ref.set(v, a, which)
+        ref.set_iterations(it0)
+        O.lib().orc_qnet32_set_dense(int(dense))
+        e = dict(exp)
+        loss, grads, norms = ref.train(xt, at, yt)
+        e["loss"], e["norms"] = np.float32(loss), np.asarray(norms, np.float32)
+        for v in range(10):
+            e[f"g{v}"] = grads[v]
+            for which in range(3):
+                e[f"s{v}_{which}"] = ref.get(v, which)
+        exps[dense] = e
+    O.lib().orc_qnet32_set_dense(0)
+    return d, inp, exps
 
 
 @pytest.mark.parametrize("env", [{}, {"QLX_F32_BG": "0"}, {"QLX_F32_C1_SKIP": "0"},
@@ -100,7 +113,8 @@ def case(tmp_path_factory):
                                  {"QLX_F32_DENSE_OVERLAP": "1"}, {"QLX_F32_DENSE_OVERLAP": "0"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "default")
 def test_path_bit_exact(case, env):
-    d, inp, exp = case
+    d, inp, exps = case
+    exp = exps[env.get("QLX_F32_BG") == "0"]
     out = str(d / ("out_" + ("_".join(f"{k}{v}" for k, v in env.items()) or "default") + ".npz"))
     cenv = {k: v for k, v in os.environ.items() if not k.startswith("QLX_F32_") and k != "QLX_NUM_CUS"}
     cenv.update(env)
