@@ -412,10 +412,23 @@ class Run:
         avg_us = self.dom_us / max(self.dom_launches, 1)
         tflops = rate(self.dom_work, self.dom_us, 1e6)
         traffic, src = pmc_traffic(self.precision, self.dominant)
-        return {"kernel": self.dominant, "bound": "mfma", "achieved": round(tflops, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(tflops / peak, 4), "traffic": traffic, "traffic_unit": "HBM bytes/launch",
-                "traffic_source": src, "avg_us": round(avg_us, 2), "launches_timed": self.dom_launches,
-                "flops_per_launch": round(self.dom_work / max(self.dom_launches, 1))}
+        out = {"kernel": self.dominant, "bound": "mfma", "achieved": round(tflops, 2), "peak": peak, "unit": "TFLOP/s",
+               "frac": round(tflops / peak, 4), "traffic": traffic, "traffic_unit": "HBM bytes/launch",
+               "traffic_source": src, "avg_us": round(avg_us, 2), "launches_timed": self.dom_launches,
+               "flops_per_launch": round(self.dom_work / max(self.dom_launches, 1))}
+        if self.dominant in ZERO_STEP_SCOPES:
+            # a launch that does not issue part of its dense work: achieved = the issued FLOP (dense x (1 - share x the
+            # measured skipped fraction)) per launch / time; the dense-equivalent rate beside it
+            _, (half, key), share = zero_step_scope(self.dominant)
+            skip = self.skipped(half, key)
+            if skip is not None:
+                f = 1.0 - share * skip
+                out.update({"achieved": round(tflops * f, 2), "frac": round(tflops * f / peak, 4),
+                            "flops_per_launch": round(self.dom_work * f / max(self.dom_launches, 1)),
+                            "achieved_dense_equivalent": round(tflops, 2), "skipped_fraction": round(skip, 4),
+                            "skipped_share_of_launch": share,
+                            "flops_per_launch_dense": round(self.dom_work / max(self.dom_launches, 1))})
+        return out
 
     def report(self):
         """north_star's extra rates from the event-timed profile pass: per-layer MFMA utilisation, replay-sampling
@@ -427,14 +440,16 @@ class Run:
                 t = rate(c[k]["work"], c[k]["total_us_per_step"], 1e6)
                 if k in ZERO_STEP_SCOPES:
                     # part of the dense work is not issued: the MFMA utilisation is the issued work, dense FLOP x (1 - the
-                    # scope's measured skipped fraction), over the time; the dense-equivalent rate stays beside it
-                    note, (half, key) = ZERO_STEP_SCOPES[k]
+                    # scope's measured skipped fraction x the share of the launch's work it applies to), over the time;
+                    # the dense-equivalent rate stays beside it
+                    note, (half, key), share = zero_step_scope(k)
                     skip = self.skipped(half, key)
-                    issued = None if skip is None else t * (1.0 - skip)
+                    issued = None if skip is None else t * (1.0 - share * skip)
                     layers[k] = {"tflops_issued": None if issued is None else round(issued, 2),
                                  "mfma_frac": None if issued is None else round(issued / peak, 4),
                                  "skipped_fraction": None if skip is None else round(skip, 4),
                                  "skipped_fraction_source": f"skipped_fractions.{half}.{key}.mean",
+                                 "skipped_share_of_launch": share,
                                  "tflops_dense_equivalent": round(t, 2), "avg_us": round(c[k]["avg_us"], 2), "note": note}
                 else:
                     layers[k] = {"tflops": round(t, 2), "mfma_frac": round(t / peak, 4), "avg_us": round(c[k]["avg_us"], 2)}
@@ -482,7 +497,13 @@ _C1_NOTE = ("MFMA steps whose frame operands are all 0 are not issued (exact, DE
 _BG_NOTE = ("the background rows (receptive field all-zero frame pixels) are one constant row, computed once and written, "
             "the GEMM runs the other rows (exact, DESIGN.md 4.1): mfma_frac = dense FLOP x (1 - skipped_fraction) / time / "
             "peak; tflops_dense_equivalent = dense FLOP / time")
+_WG_NOTE = ("backward pair (weight gradient + backward data, equal dense FLOP): the weight-gradient tiles reduce over the "
+            "non-background rows only - a background row's im2col row is the layer's constant input row, its share a rank-1 "
+            "term added in the reduction (DESIGN.md §6): mfma_frac = dense FLOP x (1 - skipped_fraction / 2) / time / peak; "
+            "tflops_dense_equivalent = dense FLOP / time")
 ZERO_STEP_SCOPES = {
+    "f32_conv2_bwd": (_WG_NOTE, ("train_batches", "conv2_background_rows"), 0.5),
+    "f32_conv3_bwd": (_WG_NOTE, ("train_batches", "conv3_background_rows"), 0.5),
     "f32_conv1_fwd": (_C1_NOTE, ("train_batches", "conv1_fwd_zero_steps")),
     "f32_conv1_fwd_big": (_C1_NOTE, ("acting", "conv1_fwd_zero_steps")),
     "f32_conv1_wgrad": (_C1_NOTE, ("train_batches", "conv1_wgrad_zero_steps")),
@@ -491,6 +512,12 @@ ZERO_STEP_SCOPES = {
     "f32_conv3_fwd": (_BG_NOTE, ("train_batches", "conv3_background_rows")),
     "f32_conv3_fwd_big": (_BG_NOTE, ("acting", "conv3_background_rows")),
 }
+
+
+def zero_step_scope(k):
+    """(note, (half, key), share of the launch's dense work the skipped fraction applies to)"""
+    v = ZERO_STEP_SCOPES[k]
+    return (v[0], v[1], v[2] if len(v) > 2 else 1.0)
 
 
 def pmc_traffic(precision, scope):
