@@ -5,7 +5,8 @@ the dense conv2 / conv3 forward without background rows (QLX_F32_BG=0) and conv1
 (QLX_F32_C1_SKIP=0), alone and together; the dense variables' update on the model's second stream beside the conv backward
 (QLX_F32_DENSE_OVERLAP=1) or on the learner stream (=0); and the grid shapes of a part with few CUs (QLX_NUM_CUS=8: a CPX partition
 of an MI300X / MI355X - conv1 then runs more than two blocks per CU so that no block holds more than 64 samples).
-Each must give the oracle's bits (oracle/qnet32_ref.cpp, the same chains as tests/test_gpu_qnet32.py): Q values and the
+Each must give the oracle's bits (oracle/qnet32_ref.cpp, the same chains as tests/test_gpu_qnet32.py; QLX_F32_BG=0 those of its dense
+mode, orc_qnet32_set_dense: the conv weight gradients over every row): Q values and the
 conv2 / conv3 activations of a 1,024-sample forward, Q of a 3,000-sample (chunk-size kernels) forward, and one training
 step at B = 1,024 (loss, all ten gradients, the clip norms, w / m / v after Adam).
 
