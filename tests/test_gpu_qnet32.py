@@ -111,12 +111,17 @@ def test_forward_bit_exact(B, kind):
     assert same(mx, qr.max(axis=1))
 
 
-@pytest.mark.parametrize("B", [32, 320, 1024])
-def test_train_step_bit_exact(B):
+# (round 6) ragged batches and frames with no / only background rows exercise the compacted weight gradients' chunk
+# tables (a partial last chunk, chunks with nothing kept, every row kept) and B > 2,048 the persistent conv1 forward's
+# step masks and row flags
+@pytest.mark.parametrize("B,kind", [(32, "mixed"), (320, "mixed"), (1024, "mixed"), (37, "mixed"), (1000, "env"), (64, "zero"),
+                                    (96, "rand"), (3000, "sparse")])
+def test_train_step_bit_exact(B, kind):
     m = _qlx().DeepQLearningModel(seed=7)
     ref = O.QNet(seed=7, f32=True)
     randomize(m, ref, 100 + B)
-    x = mixed_states(B, B)
+    x = {"env": lambda: env_states(B), "rand": lambda: rand_states(B, B), "sparse": lambda: rand_states(B, B, True),
+         "mixed": lambda: mixed_states(B, B), "zero": lambda: np.zeros((B, 84, 84, 4), np.uint8)}[kind]()
     rng = np.random.default_rng(B)
     a = rng.integers(0, 3, B).astype(np.uint8)
     q0 = ref.forward(x)
